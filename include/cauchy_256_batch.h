@@ -1,0 +1,58 @@
+/*
+ * cauchy_256_batch.h -- batched, device-resident extension of the cauchy_256.h ABI.
+ *
+ * Not part of the reference API: the reference codes one stripe per call from host
+ * memory (cauchy_256.h:78, :103).  These entry points code `stripes` independent
+ * stripes that already live in HIP device memory, asynchronously on a caller stream,
+ * with exactly the per-stripe results of cauchy_256_encode / cauchy_256_decode.
+ *
+ * Layout (all pointers are device pointers, strides in bytes):
+ *   data block x of stripe s       d_data     + s * data_stride     + x * block_bytes
+ *   recovery block r of stripe s   d_recovery + s * recovery_stride + r * block_bytes
+ *   decode slot i of stripe s      d_blocks   + s * stripe_stride   + i * block_bytes
+ *   row of decode slot i           d_rows[s * k + i]   (the Block.row of that slot)
+ *
+ * `stream` is a hipStream_t (NULL = the null stream).  Calls only enqueue work.
+ * Return codes: 0 ok, -1 invalid parameters, -2 no device, -3 HIP error.
+ * All work runs on the GPU; there is no CPU fallback.
+ */
+#ifndef LONGHAIR_AMD_CAUCHY_256_BATCH_H
+#define LONGHAIR_AMD_CAUCHY_256_BATCH_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Encode every stripe: recovery = G * data (as cauchy_256_encode).  Parameter checks
+ * follow the reference: recovery block 0 is written for every stripe, then -1 is
+ * returned when m > 1 and (k + m > 256 or block_bytes % 8 != 0). */
+int cauchy_256_encode_batch(int k, int m, int block_bytes, int stripes,
+                            const void *d_data, long long data_stride,
+                            void *d_recovery, long long recovery_stride, void *stream);
+
+/* Decode every stripe in place (as cauchy_256_decode applied to the k slots of each
+ * stripe in array order).  d_status, if not NULL, receives one signed byte per stripe:
+ * 0 = ok, -1 = the stripe's rows are invalid (duplicate or >= k + m); such a stripe is
+ * left untouched.  Returns -1 (nothing done) when m > 1 and k + m > 256 or
+ * block_bytes % 8 != 0. */
+int cauchy_256_decode_batch(int k, int m, int block_bytes, int stripes,
+                            void *d_blocks, long long stripe_stride,
+                            unsigned char *d_rows, signed char *d_status, void *stream);
+
+/* Optional: compile the specialised kernels and reserve workspace for up to
+ * `max_stripes` stripes of this shape ahead of time (e.g. before hipGraph capture or
+ * a timed region).  Synchronous.  Returns 0 or an error code. */
+int cauchy_256_batch_prepare(int k, int m, int block_bytes, int max_stripes);
+
+/* Which kernel family serves this shape: 1 = run-time specialised (JIT) network,
+ * 0 = generic table-driven kernel.  `what` = 0 for encode, 1 for decode. */
+int cauchy_256_batch_path(int k, int m, int block_bytes, int what);
+
+/* Last error message of the calling thread (empty string if none). */
+const char *cauchy_256_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LONGHAIR_AMD_CAUCHY_256_BATCH_H */

@@ -1,0 +1,131 @@
+"""longhair_amd -- MI355X-native Cauchy Reed-Solomon codec with the cauchy_256.h ABI.
+
+Python view of the C-ABI library `liblonghair_amd.so` (built from longhair_amd/csrc by
+`make -C longhair_amd/csrc` or `__graft_entry__.build()`):
+
+* the reference interface, one stripe per call (catid/longhair cauchy_256.h:47-103):
+  `cauchy_256_init()`, `cauchy_256_encode(k, m, data_ptrs, recovery_blocks, block_bytes)`,
+  `cauchy_256_decode(k, m, blocks, block_bytes)` and the `Block` structure, taking the same
+  arguments as the C functions (ctypes pointers / arrays) and returning the same codes;
+* batched device-resident helpers on torch uint8 tensors: `encode_batch`, `decode_batch`.
+
+There is no CPU implementation: importing works without a GPU, but every codec call
+goes through the HIP library and fails loudly (LonghairError / non-zero codes) when no
+device or no library is available.
+"""
+import ctypes
+import os
+
+from ._native import Block, lib, library_path  # noqa: F401
+
+CAUCHY_256_VERSION = 2
+
+OK, EINVAL, ENODEV, EHIP = 0, -1, -2, -3
+
+
+class LonghairError(RuntimeError):
+    def __init__(self, code, what):
+        msg = lib().cauchy_256_last_error().decode(errors="replace")
+        super().__init__(f"{what} failed with code {code}: {msg}")
+        self.code = code
+
+
+def _cauchy_256_init(expected_version):
+    return lib()._cauchy_256_init(ctypes.c_int(expected_version))
+
+
+def cauchy_256_init():
+    """Reference `cauchy_256_init()` macro: 0 on success (-1 version mismatch, -2 no GPU)."""
+    return _cauchy_256_init(CAUCHY_256_VERSION)
+
+
+def cauchy_256_encode(k, m, data_ptrs, recovery_blocks, block_bytes):
+    """Reference cauchy_256_encode (cauchy_256.h:78): `data_ptrs` is a ctypes array of k
+    `POINTER(c_ubyte)` (host or device memory), `recovery_blocks` a pointer/address with
+    room for m * block_bytes bytes.  Returns 0 / -1 like the reference."""
+    return lib().cauchy_256_encode(ctypes.c_int(k), ctypes.c_int(m), data_ptrs,
+                                   ctypes.c_void_p(_addr(recovery_blocks)), ctypes.c_int(block_bytes))
+
+
+def cauchy_256_decode(k, m, blocks, block_bytes):
+    """Reference cauchy_256_decode (cauchy_256.h:103): `blocks` is a ctypes array of k
+    `Block`; recovered originals are written in place and their `row` rewritten."""
+    return lib().cauchy_256_decode(ctypes.c_int(k), ctypes.c_int(m), blocks, ctypes.c_int(block_bytes))
+
+
+def _addr(x):
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if isinstance(x, ctypes.Array) or isinstance(x, ctypes._Pointer):
+        return ctypes.cast(x, ctypes.c_void_p).value
+    if hasattr(x, "ctypes"):
+        return x.ctypes.data
+    raise TypeError(f"cannot take the address of {type(x)}")
+
+
+def _stream_handle(stream):
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+
+def encode_batch(data, m, recovery=None, stream=None):
+    """Encode a batch of stripes resident on the GPU.
+
+    data: uint8 CUDA tensor [stripes, k, block_bytes] (stripe-contiguous blocks).
+    Returns the recovery tensor [stripes, m, block_bytes] (allocated if not given).
+    Runs asynchronously on `stream` (default: torch's current stream)."""
+    import torch
+    assert data.dtype == torch.uint8 and data.is_cuda and data.dim() == 3
+    assert data.stride(2) == 1 and data.stride(1) == data.shape[2]
+    stripes, k, nbytes = data.shape
+    if recovery is None:
+        recovery = torch.empty((stripes, m, nbytes), dtype=torch.uint8, device=data.device)
+    assert recovery.stride(2) == 1 and recovery.stride(1) == nbytes and recovery.shape[1] == m
+    rc = lib().cauchy_256_encode_batch(k, m, nbytes, stripes, ctypes.c_void_p(data.data_ptr()),
+                                       ctypes.c_longlong(data.stride(0)),
+                                       ctypes.c_void_p(recovery.data_ptr()),
+                                       ctypes.c_longlong(recovery.stride(0)),
+                                       ctypes.c_void_p(_stream_handle(stream)))
+    if rc != 0:
+        raise LonghairError(rc, "cauchy_256_encode_batch")
+    return recovery
+
+
+def decode_batch(blocks, rows, m, status=None, stream=None):
+    """Decode a batch of stripes in place on the GPU.
+
+    blocks: uint8 CUDA tensor [stripes, k, block_bytes] -- the k received blocks of each
+            stripe in array order (the reference's Block[] order).
+    rows:   uint8 CUDA tensor [stripes, k] -- each slot's Block.row; rewritten in place.
+    Returns `status` (int8 [stripes], 0 ok / -1 invalid rows)."""
+    import torch
+    assert blocks.dtype == torch.uint8 and blocks.is_cuda and blocks.dim() == 3
+    assert blocks.stride(2) == 1 and blocks.stride(1) == blocks.shape[2]
+    stripes, k, nbytes = blocks.shape
+    assert rows.dtype == torch.uint8 and rows.is_contiguous() and tuple(rows.shape) == (stripes, k)
+    if status is None:
+        status = torch.empty((stripes,), dtype=torch.int8, device=blocks.device)
+    rc = lib().cauchy_256_decode_batch(k, m, nbytes, stripes, ctypes.c_void_p(blocks.data_ptr()),
+                                       ctypes.c_longlong(blocks.stride(0)),
+                                       ctypes.c_void_p(rows.data_ptr()),
+                                       ctypes.c_void_p(status.data_ptr()),
+                                       ctypes.c_void_p(_stream_handle(stream)))
+    if rc != 0:
+        raise LonghairError(rc, "cauchy_256_decode_batch")
+    return status
+
+
+def prepare(k, m, block_bytes, max_stripes=0):
+    """Compile the specialised kernels / reserve workspace for a shape (synchronous)."""
+    rc = lib().cauchy_256_batch_prepare(k, m, block_bytes, max_stripes)
+    if rc != 0:
+        raise LonghairError(rc, "cauchy_256_batch_prepare")
+
+
+def batch_path(k, m, block_bytes, decode=False):
+    """'jit' when a run-time specialised network serves the shape, else 'generic'."""
+    return "jit" if lib().cauchy_256_batch_path(k, m, block_bytes, 1 if decode else 0) else "generic"

@@ -1,0 +1,45 @@
+"""Loader for the in-tree C-ABI library (no CPU fallback: a missing library raises)."""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+library_path = os.path.join(_HERE, "liblonghair_amd.so")
+_lib = None
+
+
+class Block(ctypes.Structure):
+    """Same layout as the reference Block (cauchy_256.h:52-55)."""
+    _fields_ = [("data", ctypes.POINTER(ctypes.c_ubyte)), ("row", ctypes.c_ubyte)]
+
+
+# Every symbol include/cauchy_256.h and include/cauchy_256_batch.h declare.
+EXPORTS = {
+    "_cauchy_256_init": (ctypes.c_int, [ctypes.c_int]),
+    "cauchy_256_encode": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "cauchy_256_decode": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
+    "cauchy_256_encode_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
+                                               ctypes.c_longlong, ctypes.c_void_p]),
+    "cauchy_256_decode_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_void_p]),
+    "cauchy_256_batch_prepare": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "cauchy_256_batch_path": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "cauchy_256_last_error": (ctypes.c_char_p, []),
+}
+
+
+def lib():
+    """The loaded library (loads on first use; raises OSError if it was never built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(library_path):
+            raise OSError(f"{library_path} is missing: run `make -C longhair_amd/csrc` "
+                          "(longhair_amd has no CPU fallback)")
+        l = ctypes.CDLL(library_path)
+        for name, (res, args) in EXPORTS.items():
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = l
+    return _lib

@@ -1,0 +1,522 @@
+// codec.cpp -- the C ABI: drop-in cauchy_256.h entry points and the batched
+// device-resident extension (cauchy_256_batch.h).
+//
+// Host code only validates parameters, looks up plans/kernels and enqueues work; every
+// byte of encode/decode output is produced by GPU kernels (kernels.hip, jit_codec.hip).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/cauchy_256.h"
+#include "../../include/cauchy_256_batch.h"
+#include "field.hpp"
+#include "jit.hpp"
+#include "kernels.hpp"
+
+namespace lh {
+
+enum { kOk = 0, kInvalid = -1, kNoDevice = -2, kHipError = -3 };
+
+thread_local std::string g_last_error;
+
+static int fail(int code, const std::string &msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define LH_HIP(expr)                                                                       \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return fail(kHipError, std::string(#expr) + ": " + hipGetErrorString(e_));     \
+    } while (0)
+
+// Grow-only device buffer.
+struct DevBuf {
+    uint8_t *ptr = nullptr;
+    size_t size = 0;
+    hipError_t reserve(size_t n) {
+        if (n <= size) return hipSuccess;
+        if (ptr) {
+            hipError_t e = hipDeviceSynchronize();  // the old buffer may still be in use
+            if (e != hipSuccess) return e;
+            (void)hipFree(ptr);
+            ptr = nullptr;
+            size = 0;
+        }
+        hipError_t e = hipMalloc(&ptr, n);
+        if (e == hipSuccess) size = n;
+        return e;
+    }
+};
+
+struct HostPinned {
+    uint8_t *ptr = nullptr;
+    size_t size = 0;
+    hipError_t reserve(size_t n) {
+        if (n <= size) return hipSuccess;
+        if (ptr) (void)hipHostFree(ptr);
+        ptr = nullptr;
+        size = 0;
+        hipError_t e = hipHostMalloc(&ptr, n, hipHostMallocDefault);
+        if (e == hipSuccess) size = n;
+        return e;
+    }
+};
+
+// Per-stream scratch (decode plans and the generic path's output workspace).
+struct Workspace {
+    DevBuf plan, work;
+};
+
+// Per-device state.
+struct Device {
+    int id = 0;
+    std::mutex mu;                       // guards maps below and the drop-in staging
+    uint8_t *gf_exp = nullptr;           // 512 B
+    int16_t *gf_log = nullptr;           // 256 x int16
+    std::map<std::pair<int, int>, uint8_t *> generators;  // (k, m) -> m x k on device
+    DevBuf zero;                         // zero page (>= block bytes)
+    std::map<hipStream_t, Workspace> ws;
+    JitCache jit;
+    // drop-in (single stripe, host pointers) staging
+    std::mutex dropin_mu;
+    hipStream_t stream = nullptr;
+    DevBuf stage, stage_rows, stage_status;
+    HostPinned host_stage;
+};
+
+static std::mutex g_devices_mu;
+static std::map<int, std::unique_ptr<Device>> g_devices;
+
+static int current_device(Device **out) {
+    int id = 0;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+        return fail(kNoDevice, "longhair_amd: no HIP device available (the codec has no CPU path)");
+    LH_HIP(hipGetDevice(&id));
+    std::lock_guard<std::mutex> g(g_devices_mu);
+    auto &slot = g_devices[id];
+    if (!slot) {
+        std::unique_ptr<Device> d(new Device());
+        d->id = id;
+        const Field &F = Field::get();
+        LH_HIP(hipMalloc(&d->gf_exp, 512));
+        LH_HIP(hipMalloc(&d->gf_log, 256 * sizeof(int16_t)));
+        LH_HIP(hipMemcpy(d->gf_exp, F.exp, 512, hipMemcpyHostToDevice));
+        LH_HIP(hipMemcpy(d->gf_log, F.log, 256 * sizeof(int16_t), hipMemcpyHostToDevice));
+        LH_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        slot = std::move(d);
+    }
+    *out = slot.get();
+    return kOk;
+}
+
+static int device_generator(Device *d, int k, int m, const uint8_t **out) {
+    std::lock_guard<std::mutex> g(d->mu);
+    auto it = d->generators.find({k, m});
+    if (it == d->generators.end()) {
+        const std::vector<uint8_t> G = generator_matrix(k, m);
+        uint8_t *p = nullptr;
+        LH_HIP(hipMalloc(&p, G.size()));
+        LH_HIP(hipMemcpy(p, G.data(), G.size(), hipMemcpyHostToDevice));
+        it = d->generators.emplace(std::make_pair(k, m), p).first;
+    }
+    *out = it->second;
+    return kOk;
+}
+
+static int zero_page(Device *d, size_t bytes, const uint8_t **out) {
+    std::lock_guard<std::mutex> g(d->mu);
+    if (d->zero.size < bytes) {
+        LH_HIP(d->zero.reserve(bytes));
+        LH_HIP(hipMemset(d->zero.ptr, 0, d->zero.size));
+    }
+    *out = d->zero.ptr;
+    return kOk;
+}
+
+static int workspace(Device *d, hipStream_t st, size_t plan_bytes, size_t work_bytes, Workspace **out) {
+    std::lock_guard<std::mutex> g(d->mu);
+    Workspace &w = d->ws[st];
+    LH_HIP(w.plan.reserve(plan_bytes));
+    if (work_bytes) LH_HIP(w.work.reserve(work_bytes));
+    *out = &w;
+    return kOk;
+}
+
+static int generic_word(int sub) {
+    if (sub >= 4) return 4;
+    if (sub >= 2) return 2;
+    return 1;
+}
+
+// ------------------------------------------------------------------------ encode
+static int xor_rows(int k, int n_rep, int bytes, int stripes, const uint8_t *in, long long in_stride,
+                    uint8_t *out, long long out_stride, hipStream_t st) {
+    XorArgs a{};
+    a.in = in;
+    a.in_stride = in_stride;
+    a.out = out;
+    a.out_stride = out_stride;
+    a.plan = nullptr;
+    a.n_in = k;
+    a.n_rep = n_rep;
+    a.bytes = bytes;
+    a.stripes = stripes;
+    a.nch = bytes / 16 + ((bytes % 16) ? 1 : 0);
+    LH_HIP(launch_xor_reduce(a, st));
+    return kOk;
+}
+
+static int encode_batch(int k, int m, int bytes, int stripes, const uint8_t *d_data, long long data_stride,
+                        uint8_t *d_rec, long long rec_stride, hipStream_t st, bool allow_compile) {
+    if (k < 1 || m < 1 || bytes <= 0 || stripes < 0 || k > 256 || m > 256)
+        return fail(kInvalid, "invalid k, m, block_bytes or stripes");
+    if (stripes == 0) return kOk;
+    if (data_stride < (long long)k * bytes || rec_stride < (long long)m * bytes)
+        return fail(kInvalid, "stripe strides smaller than the stripe");
+    Device *d = nullptr;
+    if (int rc = current_device(&d)) return rc;
+
+    if (k == 1) return xor_rows(1, m, bytes, stripes, d_data, data_stride, d_rec, rec_stride, st);
+    if (m == 1 || k + m > 256 || bytes % 8 != 0) {
+        // Recovery block 0 first, as the reference (cauchy_256.cpp:1511-1527).
+        if (int rc = xor_rows(k, 1, bytes, stripes, d_data, data_stride, d_rec, rec_stride, st)) return rc;
+        return m == 1 ? kOk : fail(kInvalid, "k + m > 256 or block_bytes % 8 != 0");
+    }
+
+    JitConfig cfg;
+    if (jit_config_for(k, m, bytes, false, &cfg)) {
+        std::string err;
+        const JitKernels *jk = allow_compile ? d->jit.get(cfg, &err) : d->jit.peek(cfg);
+        if (jk) {
+            const long long waves = cfg.spw ? (stripes + cfg.spw - 1) / cfg.spw : (long long)stripes * cfg.wps;
+            const long long blocks = (waves + 3) / 4;
+            if (blocks > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
+            long long in_stride = data_stride, out_stride = rec_stride;
+            int n = stripes;
+            void *args[] = {(void *)&d_data, &in_stride, (void *)&d_rec, &out_stride, &n};
+            LH_HIP(hipModuleLaunchKernel(jk->encode, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr));
+            return kOk;
+        }
+        if (allow_compile) return fail(kHipError, err);
+    }
+    const uint8_t *G = nullptr;
+    if (int rc = device_generator(d, k, m, &G)) return rc;
+    ApplyArgs a{};
+    a.in = d_data;
+    a.in_stride = data_stride;
+    a.out = d_rec;
+    a.out_stride = rec_stride;
+    a.coef = G;
+    a.coef_stride = 0;
+    a.n_in = k;
+    a.n_out = m;
+    a.bytes = bytes;
+    a.sub = bytes / 8;
+    a.stripes = stripes;
+    const int W = generic_word(a.sub);
+    a.nch = (a.sub + W - 1) / W;
+    LH_HIP(launch_apply_generic(a, W, st));
+    return kOk;
+}
+
+// ------------------------------------------------------------------------ decode
+static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks, long long stride,
+                        uint8_t *d_rows, int8_t *d_status, hipStream_t st, bool allow_compile) {
+    if (k < 1 || m < 1 || bytes <= 0 || stripes < 0 || k > 256 || m > 256)
+        return fail(kInvalid, "invalid k, m, block_bytes or stripes");
+    if (stripes == 0) return kOk;
+    if (stride < (long long)k * bytes) return fail(kInvalid, "stripe stride smaller than the stripe");
+    if (m > 1 && k > 1 && (k + m > 256 || bytes % 8 != 0))
+        return fail(kInvalid, "k + m > 256 or block_bytes % 8 != 0");
+    Device *d = nullptr;
+    if (int rc = current_device(&d)) return rc;
+
+    const int e_max = (m == 1 || k <= 1) ? 1 : (k < m ? k : m);
+    const long long plan_stride = PlanView::bytes(k, m, e_max);
+    JitConfig cfg;
+    const bool jit_ok = (k > 1 && m > 1) && jit_config_for(k, m, bytes, true, &cfg);
+    const JitKernels *jk = nullptr;
+    std::string err;
+    if (jit_ok) {
+        jk = allow_compile ? d->jit.get(cfg, &err) : d->jit.peek(cfg);
+        if (!jk && allow_compile) return fail(kHipError, err);
+    }
+    const bool generic = (k > 1 && m > 1) && !jk;
+    const size_t work_bytes = generic ? (size_t)stripes * e_max * bytes : 0;
+    Workspace *w = nullptr;
+    if (int rc = workspace(d, st, (size_t)stripes * plan_stride, work_bytes, &w)) return rc;
+    const uint8_t *G = nullptr;
+    if (int rc = device_generator(d, k, m, &G)) return rc;
+
+    PlanArgs pa{};
+    pa.rows = d_rows;
+    pa.status = d_status;
+    pa.plan = w->plan.ptr;
+    pa.plan_stride = plan_stride;
+    pa.G = G;
+    pa.gf_exp = d->gf_exp;
+    pa.gf_log = d->gf_log;
+    pa.k = k;
+    pa.m = m;
+    pa.e_max = e_max;
+    pa.stripes = stripes;
+    LH_HIP(launch_plan(pa, st));
+    if (k <= 1) return kOk;
+
+    if (m == 1) {
+        XorArgs a{};
+        a.in = d_blocks;
+        a.in_stride = stride;
+        a.out = d_blocks;
+        a.out_stride = stride;
+        a.plan = w->plan.ptr;
+        a.plan_stride = plan_stride;
+        a.k = k;
+        a.m = m;
+        a.e_max = e_max;
+        a.n_in = k;
+        a.n_rep = 1;
+        a.bytes = bytes;
+        a.stripes = stripes;
+        a.nch = bytes / 16 + ((bytes % 16) ? 1 : 0);
+        LH_HIP(launch_xor_reduce(a, st));
+        return kOk;
+    }
+    if (jk) {
+        const uint8_t *zero = nullptr;
+        if (int rc = zero_page(d, (size_t)bytes, &zero)) return rc;
+        const long long waves = cfg.spw ? (stripes + cfg.spw - 1) / cfg.spw : (long long)stripes * cfg.wps;
+        const long long blocks = (waves + 3) / 4;
+        long long s1 = stride, s2 = plan_stride;
+        const uint8_t *plan = w->plan.ptr;
+        int n = stripes;
+        void *args[] = {(void *)&d_blocks, &s1, (void *)&plan, &s2, (void *)&zero, &n};
+        LH_HIP(hipModuleLaunchKernel(jk->decode, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr));
+        return kOk;
+    }
+    // Generic: recovered originals into the workspace, then into their slots.
+    ApplyArgs a{};
+    a.in = d_blocks;
+    a.in_stride = stride;
+    a.out = w->work.ptr;
+    a.out_stride = (long long)e_max * bytes;
+    a.coef = w->plan.ptr + PlanView::w_offset(k, m, e_max);
+    a.coef_stride = plan_stride;
+    a.nout_per_stripe = w->plan.ptr;
+    a.nout_stride = plan_stride;
+    a.n_in = k;
+    a.n_out = e_max;
+    a.bytes = bytes;
+    a.sub = bytes / 8;
+    a.stripes = stripes;
+    const int W = generic_word(a.sub);
+    a.nch = (a.sub + W - 1) / W;
+    LH_HIP(launch_apply_generic(a, W, st));
+    ScatterArgs sa{};
+    sa.work = w->work.ptr;
+    sa.work_stride = (long long)e_max * bytes;
+    sa.blocks = d_blocks;
+    sa.blocks_stride = stride;
+    sa.plan = w->plan.ptr;
+    sa.plan_stride = plan_stride;
+    sa.k = k;
+    sa.m = m;
+    sa.e_max = e_max;
+    sa.bytes = bytes;
+    sa.stripes = stripes;
+    LH_HIP(launch_scatter(sa, st));
+    return kOk;
+}
+
+// -------------------------------------------------------------- drop-in helpers
+static bool is_device_pointer(const void *p) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+static int dropin_encode(int k, int m, const unsigned char *data_ptrs[], void *recovery, int bytes) {
+    if (k < 1 || m < 1 || bytes <= 0 || k > 256 || m > 256) return fail(kInvalid, "invalid k, m or block_bytes");
+    Device *d = nullptr;
+    if (int rc = current_device(&d)) return rc;
+    std::lock_guard<std::mutex> g(d->dropin_mu);
+    const size_t in_n = (size_t)k * bytes, out_n = (size_t)m * bytes;
+    LH_HIP(d->stage.reserve(in_n + out_n));
+    LH_HIP(d->host_stage.reserve(in_n + out_n));
+    hipStream_t st = d->stream;
+    const bool dev_in = is_device_pointer(data_ptrs[0]);
+    const bool dev_out = is_device_pointer(recovery);
+    uint8_t *din = d->stage.ptr, *dout = d->stage.ptr + in_n;
+    if (dev_in) {
+        for (int x = 0; x < k; ++x) LH_HIP(hipMemcpyAsync(din + (size_t)x * bytes, data_ptrs[x], bytes, hipMemcpyDefault, st));
+    } else {
+        for (int x = 0; x < k; ++x) std::memcpy(d->host_stage.ptr + (size_t)x * bytes, data_ptrs[x], bytes);
+        LH_HIP(hipMemcpyAsync(din, d->host_stage.ptr, in_n, hipMemcpyHostToDevice, st));
+    }
+    const int rc = encode_batch(k, m, bytes, 1, din, (long long)in_n, dout, (long long)out_n, st, false);
+    if (rc != kOk && rc != kInvalid) {
+        (void)hipStreamSynchronize(st);
+        return rc;
+    }
+    // On kInvalid only recovery block 0 was produced (reference behaviour).
+    const size_t n = (rc == kOk) ? out_n : (size_t)bytes;
+    if (dev_out) {
+        LH_HIP(hipMemcpyAsync(recovery, dout, n, hipMemcpyDefault, st));
+        LH_HIP(hipStreamSynchronize(st));
+    } else {
+        LH_HIP(hipMemcpyAsync(d->host_stage.ptr + in_n, dout, n, hipMemcpyDeviceToHost, st));
+        LH_HIP(hipStreamSynchronize(st));
+        std::memcpy(recovery, d->host_stage.ptr + in_n, n);
+    }
+    return rc;
+}
+
+static int dropin_decode(int k, int m, Block *blocks, int bytes) {
+    if (k <= 1) {  // cauchy_256.cpp:1252-1256: the only block is the data
+        if (k == 1) blocks[0].row = 0;
+        return k == 1 ? kOk : fail(kInvalid, "k < 1");
+    }
+    if (m < 1 || bytes <= 0 || k > 256 || m > 256) return fail(kInvalid, "invalid m or block_bytes");
+    int n_rcv = 0;
+    for (int i = 0; i < k; ++i) n_rcv += blocks[i].row >= k;
+    if (m > 1) {
+        if (n_rcv == 0) return kOk;  // nothing erased (:1282-1284)
+        if (k + m > 256 || bytes % 8 != 0) return fail(kInvalid, "k + m > 256 or block_bytes % 8 != 0");
+    }
+    Device *d = nullptr;
+    if (int rc = current_device(&d)) return rc;
+    std::lock_guard<std::mutex> g(d->dropin_mu);
+    const size_t in_n = (size_t)k * bytes;
+    LH_HIP(d->stage.reserve(in_n));
+    LH_HIP(d->stage_rows.reserve(256));
+    LH_HIP(d->stage_status.reserve(16));
+    LH_HIP(d->host_stage.reserve(in_n + 1024));
+    hipStream_t st = d->stream;
+    const bool dev = is_device_pointer(blocks[0].data);
+    uint8_t *hs = d->host_stage.ptr;
+    uint8_t *hrows = hs + in_n;  // [0,256) rows in, [256,512) rows out, [512] status
+    for (int i = 0; i < k; ++i) hrows[i] = blocks[i].row;
+    if (dev) {
+        for (int i = 0; i < k; ++i)
+            LH_HIP(hipMemcpyAsync(d->stage.ptr + (size_t)i * bytes, blocks[i].data, bytes, hipMemcpyDefault, st));
+    } else {
+        for (int i = 0; i < k; ++i) std::memcpy(hs + (size_t)i * bytes, blocks[i].data, bytes);
+        LH_HIP(hipMemcpyAsync(d->stage.ptr, hs, in_n, hipMemcpyHostToDevice, st));
+    }
+    LH_HIP(hipMemcpyAsync(d->stage_rows.ptr, hrows, k, hipMemcpyHostToDevice, st));
+    int rc = decode_batch(k, m, bytes, 1, d->stage.ptr, (long long)in_n, d->stage_rows.ptr,
+                          (int8_t *)d->stage_status.ptr, st, false);
+    if (rc != kOk) {
+        (void)hipStreamSynchronize(st);
+        return rc;
+    }
+    uint8_t *hout = hrows + 256;
+    LH_HIP(hipMemcpyAsync(hout, d->stage_rows.ptr, k, hipMemcpyDeviceToHost, st));
+    LH_HIP(hipMemcpyAsync(hout + 256, d->stage_status.ptr, 1, hipMemcpyDeviceToHost, st));
+    // Slots whose bytes can change: recovery slots (m > 1); for m == 1 the recovery slot
+    // or, when none is present, slot 0 (cauchy_decode_m1's quirk).
+    std::vector<int> changed;
+    if (m == 1) {
+        int out = 0;
+        for (int i = 0; i < k; ++i) if (blocks[i].row >= k) out = i;
+        changed.push_back(out);
+    } else {
+        for (int i = 0; i < k; ++i) if (blocks[i].row >= k) changed.push_back(i);
+    }
+    if (dev) {
+        for (int i : changed)
+            LH_HIP(hipMemcpyAsync(blocks[i].data, d->stage.ptr + (size_t)i * bytes, bytes, hipMemcpyDefault, st));
+        LH_HIP(hipStreamSynchronize(st));
+    } else {
+        for (int i : changed)
+            LH_HIP(hipMemcpyAsync(hs + (size_t)i * bytes, d->stage.ptr + (size_t)i * bytes, bytes, hipMemcpyDeviceToHost, st));
+        LH_HIP(hipStreamSynchronize(st));
+    }
+    if ((int8_t)hout[256] != 0) return fail(kInvalid, "invalid or duplicated block rows");
+    if (!dev)
+        for (int i : changed) std::memcpy(blocks[i].data, hs + (size_t)i * bytes, bytes);
+    for (int i = 0; i < k; ++i) blocks[i].row = hout[i];
+    return kOk;
+}
+
+}  // namespace lh
+
+// =============================================================================== C ABI
+
+#define LH_API __attribute__((visibility("default")))
+
+extern "C" {
+
+LH_API int _cauchy_256_init(int expected_version) {
+    if (expected_version != CAUCHY_256_VERSION) return -1;  // cauchy_256.cpp:392-394
+    (void)lh::Field::get();
+    lh::Device *d = nullptr;
+    return lh::current_device(&d);
+}
+
+LH_API int cauchy_256_encode(int k, int m, const unsigned char *data_ptrs[], void *recovery_blocks, int block_bytes) {
+    return lh::dropin_encode(k, m, data_ptrs, recovery_blocks, block_bytes);
+}
+
+LH_API int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes) {
+    return lh::dropin_decode(k, m, blocks, block_bytes);
+}
+
+LH_API int cauchy_256_encode_batch(int k, int m, int block_bytes, int stripes, const void *d_data, long long data_stride,
+                            void *d_recovery, long long recovery_stride, void *stream) {
+    return lh::encode_batch(k, m, block_bytes, stripes, (const uint8_t *)d_data, data_stride, (uint8_t *)d_recovery,
+                            recovery_stride, (hipStream_t)stream, true);
+}
+
+LH_API int cauchy_256_decode_batch(int k, int m, int block_bytes, int stripes, void *d_blocks, long long stripe_stride,
+                            unsigned char *d_rows, signed char *d_status, void *stream) {
+    return lh::decode_batch(k, m, block_bytes, stripes, (uint8_t *)d_blocks, stripe_stride, d_rows,
+                            (int8_t *)d_status, (hipStream_t)stream, true);
+}
+
+LH_API int cauchy_256_batch_prepare(int k, int m, int block_bytes, int max_stripes) {
+    lh::Device *d = nullptr;
+    if (int rc = lh::current_device(&d)) return rc;
+    std::string err;
+    for (int dec = 0; dec < 2; ++dec) {
+        lh::JitConfig cfg;
+        if (lh::jit_config_for(k, m, block_bytes, dec == 1, &cfg) && !d->jit.get(cfg, &err))
+            return lh::fail(lh::kHipError, err);
+    }
+    if (max_stripes > 0 && k > 1 && m > 1) {
+        const int e_max = k < m ? k : m;
+        lh::JitConfig cfg;
+        const bool generic = !lh::jit_config_for(k, m, block_bytes, true, &cfg);
+        lh::Workspace *w = nullptr;
+        hipStream_t st = nullptr;
+        if (int rc = lh::workspace(d, st, (size_t)max_stripes * lh::PlanView::bytes(k, m, e_max),
+                                   generic ? (size_t)max_stripes * e_max * block_bytes : 0, &w))
+            return rc;
+        const uint8_t *G = nullptr, *z = nullptr;
+        if (int rc = lh::device_generator(d, k, m, &G)) return rc;
+        if (int rc = lh::zero_page(d, (size_t)block_bytes, &z)) return rc;
+    }
+    return 0;
+}
+
+LH_API int cauchy_256_batch_path(int k, int m, int block_bytes, int what) {
+    lh::JitConfig cfg;
+    return lh::jit_config_for(k, m, block_bytes, what == 1, &cfg) ? 1 : 0;
+}
+
+LH_API const char *cauchy_256_last_error(void) { return lh::g_last_error.c_str(); }
+
+}  // extern "C"

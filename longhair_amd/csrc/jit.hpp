@@ -1,0 +1,55 @@
+// jit.hpp -- run-time specialisation of the XOR network per (k, m, bytes).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+namespace lh {
+
+struct JitConfig {
+    int k, m, bytes, sub;
+    int W;     // bytes per lane per sub-block
+    int nch;   // lanes per stripe = ceil(sub / W)
+    int spw;   // stripes per wave (nch <= 64) or 0
+    int wps;   // waves per stripe (nch > 64) or 0
+    int lanes_per_launch_unit() const { return 64; }
+};
+
+struct JitKernels {
+    hipModule_t module = nullptr;
+    hipFunction_t encode = nullptr;
+    hipFunction_t decode = nullptr;
+    JitConfig cfg{};
+};
+
+// Chooses the specialised configuration for a shape, or returns false when the shape
+// is served by the generic kernel (too many recovery rows for the register budget, or
+// a network too large for the instruction cache).
+bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg);
+
+// Number of ones in the expanded generator (= XORs of the straight-line network).
+long long generator_ones(int k, int m);
+
+class JitCache {
+public:
+    // Returns compiled kernels for the configuration (compiling on first use).  On
+    // failure returns nullptr and fills *err.
+    const JitKernels *get(const JitConfig &cfg, std::string *err);
+    // Only returns an already compiled entry (no compilation).
+    const JitKernels *peek(const JitConfig &cfg);
+
+private:
+    using Key = std::tuple<int, int, int, int>;
+    std::mutex mu_;
+    std::map<Key, JitKernels> cache_;
+};
+
+std::string jit_source_for(const JitConfig &cfg);
+
+}  // namespace lh

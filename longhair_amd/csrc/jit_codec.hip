@@ -1,0 +1,321 @@
+// jit_codec.hip -- run-time specialised encode/decode kernels (compiled by hiprtc).
+//
+// The host (jit.cpp) prepends a configuration header defining LH_K, LH_M, LH_BYTES,
+// LH_SUB, LH_W, LH_NCH, LH_SPW and the constant expanded generator LH_BM[m][k][8] (row
+// y of element G[r][x] is G[r][x] * 2^y, the bit-sliced form of cauchy_256.cpp:1553-1587),
+// then compiles this file for gfx950.  Because every bit of the generator is a compile-
+// time constant, the XOR network below unrolls into exactly the XORs the bit-matrix
+// needs (the reference executes the same network one 162-byte memcpy-sized XOR at a time
+// through gf256_add_mem); hipcc fuses chains into v_xor3 / v_bitop3.
+//
+// Mapping ("small sub-block" regime, nch = ceil(sub / W) <= 64 lanes per stripe):
+//   a wave holds LH_SPW whole stripes; lane = (stripe in wave, column chunk c).  A lane
+//   owns bytes [p, p + W) of every sub-block of its stripe (p = c * W, the last chunk
+//   shifted back to sub - W so it never leaves the sub-block; the overlap is recomputed
+//   identically by both lanes of the same wave).  Stripes never straddle waves, so the
+//   in-place decode is race free: every load of a wave completes before its first store.
+//
+// This file is also compiled by hipcc at build time with the defaults below as a
+// syntax check; the product only uses the hiprtc-compiled code objects.
+
+#ifndef LH_K
+#define LH_K 4
+#define LH_M 2
+#define LH_BYTES 64
+#define LH_SUB 8
+#define LH_W 8
+#define LH_NCH 1
+#define LH_SPW 64
+#define LH_WPS 0
+static constexpr unsigned char LH_BM[LH_M][LH_K][8] = {
+    {{1, 2, 4, 8, 16, 32, 64, 128}, {1, 2, 4, 8, 16, 32, 64, 128},
+     {1, 2, 4, 8, 16, 32, 64, 128}, {1, 2, 4, 8, 16, 32, 64, 128}},
+    {{1, 2, 4, 8, 16, 32, 64, 128}, {2, 4, 8, 16, 32, 64, 128, 135},
+     {3, 6, 12, 24, 48, 96, 192, 7}, {4, 8, 16, 32, 64, 128, 135, 137}}};
+#include <hip/hip_runtime.h>
+#endif
+
+#define LH_NW ((LH_W + 3) / 4)
+
+struct lh_word {
+    unsigned int v[LH_NW];
+};
+
+__device__ __forceinline__ lh_word lh_load(const unsigned char *p) {
+    lh_word w;
+#pragma unroll
+    for (int i = 0; i < LH_NW; ++i) w.v[i] = 0;
+    __builtin_memcpy(&w.v[0], p, LH_W);
+    return w;
+}
+
+__device__ __forceinline__ void lh_store(unsigned char *p, const lh_word &w) {
+    __builtin_memcpy(p, &w.v[0], LH_W);
+}
+
+__device__ __forceinline__ void lh_xor(lh_word &a, const lh_word &b) {
+#pragma unroll
+    for (int i = 0; i < LH_NW; ++i) a.v[i] ^= b.v[i];
+}
+
+// acc[r][y] ^= sum_x B(G[r][x]) d_x, one column x at a time, all constants.
+template <int X>
+__device__ __forceinline__ void lh_column(lh_word (&acc)[LH_M][8], const lh_word (&d)[8]) {
+#pragma unroll
+    for (int r = 0; r < LH_M; ++r)
+#pragma unroll
+        for (int y = 0; y < 8; ++y)
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                if ((LH_BM[r][X][y] >> b) & 1) lh_xor(acc[r][y], d[b]);
+}
+
+struct lh_lane {
+    long long stripe;
+    int p;
+    bool active;
+};
+
+__device__ __forceinline__ lh_lane lh_map_lane(int stripes) {
+    const int lane = threadIdx.x & 63;
+    const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    lh_lane l;
+#if LH_NCH <= 64
+    // LH_SPW whole stripes per wave.
+    const int sl = lane / LH_NCH;
+    const int c = lane - sl * LH_NCH;
+    l.stripe = wave * LH_SPW + sl;
+    l.active = (sl < LH_SPW) && (l.stripe < stripes);
+#else
+    // LH_WPS waves per stripe (the host only picks this when LH_SUB % LH_W == 0, so no
+    // chunk overlaps another wave's bytes).
+    const long long c0 = (wave % LH_WPS) * 64 + lane;
+    const int c = (int)c0;
+    l.stripe = wave / LH_WPS;
+    l.active = (c0 < LH_NCH) && (l.stripe < stripes);
+#endif
+    l.p = (c == LH_NCH - 1) ? (LH_SUB - LH_W) : c * LH_W;
+    return l;
+}
+
+// Keeps the accumulators in registers between columns: stops the compiler from
+// re-associating XORs across columns (which lengthens live ranges past the register file).
+__device__ __forceinline__ void lh_opaque(lh_word (&acc)[LH_M][8]) {
+#pragma unroll
+    for (int r = 0; r < LH_M; ++r)
+#pragma unroll
+        for (int y = 0; y < 8; ++y)
+#pragma unroll
+            for (int i = 0; i < LH_NW; ++i) asm volatile("" : "+v"(acc[r][y].v[i]));
+}
+
+// Column loop, unrolled at compile time, with the next LH_PF columns' loads in flight
+// while column X is combined.
+#ifndef LH_PF
+#define LH_PF 2
+#endif
+template <int X>
+struct lh_unroll_encode {
+    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], lh_word (&ring)[LH_PF][8],
+                                               const unsigned char *base) {
+        if (X + LH_PF < LH_K) {
+            lh_word nxt[8];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) nxt[b] = lh_load(base + (long long)(X + LH_PF) * LH_BYTES + b * LH_SUB);
+            lh_column<X>(acc, ring[X % LH_PF]);
+            lh_opaque(acc);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) ring[X % LH_PF][b] = nxt[b];
+        } else {
+            lh_column<X>(acc, ring[X % LH_PF]);
+            lh_opaque(acc);
+        }
+        lh_unroll_encode<X + 1>::run(acc, ring, base);
+    }
+};
+template <>
+struct lh_unroll_encode<LH_K> {
+    __device__ __forceinline__ static void run(lh_word (&)[LH_M][8], lh_word (&)[LH_PF][8], const unsigned char *) {}
+};
+
+// recovery[s][r] = sum_x B(G[r][x]) data[s][x]   (cauchy_256_encode for m > 1, valid k, m)
+extern "C" __global__ void __launch_bounds__(256)
+lh_jit_encode(const unsigned char *__restrict__ in, long long in_stride,
+              unsigned char *__restrict__ out, long long out_stride, int stripes) {
+    const lh_lane l = lh_map_lane(stripes);
+    if (!l.active) return;
+    lh_word acc[LH_M][8];
+#pragma unroll
+    for (int r = 0; r < LH_M; ++r)
+#pragma unroll
+        for (int y = 0; y < 8; ++y)
+#pragma unroll
+            for (int i = 0; i < LH_NW; ++i) acc[r][y].v[i] = 0;
+    const unsigned char *base = in + l.stripe * in_stride + l.p;
+    lh_word ring[LH_PF][8];
+#pragma unroll
+    for (int q = 0; q < LH_PF; ++q)
+        if (q < LH_K)
+#pragma unroll
+            for (int b = 0; b < 8; ++b) ring[q][b] = lh_load(base + (long long)q * LH_BYTES + b * LH_SUB);
+    lh_unroll_encode<0>::run(acc, ring, base);
+    unsigned char *o = out + l.stripe * out_stride + l.p;
+#pragma unroll
+    for (int r = 0; r < LH_M; ++r)
+#pragma unroll
+        for (int y = 0; y < 8; ++y) lh_store(o + (long long)r * LH_BYTES + y * LH_SUB, acc[r][y]);
+}
+
+// ------------------------------------------------------------------------ decode
+// Plan record layout: kernels.hpp PlanView (e at [0], out_slot at [16], then src_slot[k],
+// rec_slot[m], coef[e_max][m]).  e_max = min(k, m) for m > 1.
+#define LH_EMAX (LH_K < LH_M ? LH_K : LH_M)
+#define LH_P_OUT 16
+#define LH_P_SRC (16 + LH_EMAX)
+#define LH_P_REC (16 + LH_EMAX + LH_K)
+#define LH_P_COEF (16 + LH_EMAX + LH_K + LH_M)
+
+// Plan bytes are fetched as packed dwords (one load per 4 slots) and unpacked with
+// constant shifts where used, so per-column slot indices cost no registers up front.
+#define LH_NSRC ((LH_K + 3) / 4)
+#define LH_NREC ((LH_M + 3) / 4)
+#define LH_NCOEF ((LH_EMAX * LH_M + 3) / 4)
+#define LH_NOUT ((LH_EMAX + 3) / 4)
+
+__device__ __forceinline__ unsigned int lh_load32(const unsigned char *p) {
+    unsigned int w;
+    __builtin_memcpy(&w, p, 4);
+    return w;
+}
+
+template <int N>
+__device__ __forceinline__ void lh_load_packed(unsigned int (&w)[N], const unsigned char *p) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) w[j] = lh_load32(p + 4 * j);
+}
+
+#define LH_BYTE(w, idx) (((w)[(idx) / 4] >> (8 * ((idx) % 4))) & 0xFFu)
+
+__device__ __forceinline__ const unsigned char *lh_slot_ptr(unsigned int slot, const unsigned char *base,
+                                                            const unsigned char *zero) {
+    return (slot == 0xFFu) ? zero : base + (long long)slot * LH_BYTES;
+}
+
+template <int X>
+struct lh_unroll_decode {
+    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], lh_word (&ring)[LH_PF][8],
+                                               const unsigned char *base, const unsigned char *zero,
+                                               const unsigned int (&srcw)[LH_NSRC]) {
+        if (X + LH_PF < LH_K) {
+            const unsigned char *src = lh_slot_ptr(LH_BYTE(srcw, X + LH_PF), base, zero);
+            lh_word nxt[8];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) nxt[b] = lh_load(src + b * LH_SUB);
+            lh_column<X>(acc, ring[X % LH_PF]);
+            lh_opaque(acc);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) ring[X % LH_PF][b] = nxt[b];
+        } else {
+            lh_column<X>(acc, ring[X % LH_PF]);
+            lh_opaque(acc);
+        }
+        lh_unroll_decode<X + 1>::run(acc, ring, base, zero, srcw);
+    }
+};
+template <>
+struct lh_unroll_decode<LH_K> {
+    __device__ __forceinline__ static void run(lh_word (&)[LH_M][8], lh_word (&)[LH_PF][8], const unsigned char *,
+                                               const unsigned char *, const unsigned int (&)[LH_NSRC]) {}
+};
+
+// In-place erasure decode.  Phase A: V_r = R_r + sum_{x present} B(G[r][x]) D_x for every
+// recovery row r (erased columns read the zero page, absent rows contribute R_r = 0).
+// Phase B: D_{E_i} = sum_r B(coef[i][r]) V_r with the per-stripe inverse from the plan,
+// by Horner over the coefficient bits: B(c) v = B(2)(...B(2)(c_7 v)...) + c_0 v.
+extern "C" __global__ void __launch_bounds__(256)
+lh_jit_decode(unsigned char *__restrict__ blocks, long long stripe_stride,
+              const unsigned char *__restrict__ plan, long long plan_stride,
+              const unsigned char *__restrict__ zero_page, int stripes) {
+    const lh_lane l = lh_map_lane(stripes);
+    if (!l.active) return;
+    const unsigned char *pl = plan + l.stripe * plan_stride;
+    const int e = pl[0];
+    if (e == 0) return;
+    unsigned char *base = blocks + l.stripe * stripe_stride + l.p;
+    const unsigned char *zero = zero_page + l.p;
+
+    lh_word v[LH_M][8];
+#pragma unroll
+    for (int r = 0; r < LH_M; ++r)
+#pragma unroll
+        for (int y = 0; y < 8; ++y)
+#pragma unroll
+            for (int i = 0; i < LH_NW; ++i) v[r][y].v[i] = 0;
+    {
+        unsigned int srcw[LH_NSRC];
+        lh_load_packed(srcw, pl + LH_P_SRC);
+        lh_word ring[LH_PF][8];
+#pragma unroll
+        for (int q = 0; q < LH_PF; ++q)
+            if (q < LH_K) {
+                const unsigned char *src = lh_slot_ptr(LH_BYTE(srcw, q), base, zero);
+#pragma unroll
+                for (int b = 0; b < 8; ++b) ring[q][b] = lh_load(src + b * LH_SUB);
+            }
+        lh_unroll_decode<0>::run(v, ring, base, zero, srcw);
+    }
+    asm volatile("" ::: "memory");  // keep the recovery-row loads below phase A
+    {
+        unsigned int recw[LH_NREC];
+        lh_load_packed(recw, pl + LH_P_REC);
+#pragma unroll
+        for (int r = 0; r < LH_M; ++r) {
+            const unsigned char *src = lh_slot_ptr(LH_BYTE(recw, r), base, zero);
+#pragma unroll
+            for (int y = 0; y < 8; ++y) lh_xor(v[r][y], lh_load(src + y * LH_SUB));
+        }
+    }
+    unsigned int coefw[LH_NCOEF], outw[LH_NOUT];
+    lh_load_packed(coefw, pl + LH_P_COEF);
+    lh_load_packed(outw, pl + LH_P_OUT);
+
+#pragma unroll
+    for (int i = 0; i < LH_EMAX; ++i) {
+        if (i < e) {
+            lh_word o[8];
+#pragma unroll
+            for (int y = 0; y < 8; ++y)
+#pragma unroll
+                for (int q = 0; q < LH_NW; ++q) o[y].v[q] = 0;
+#pragma unroll
+            for (int t = 7; t >= 0; --t) {
+                if (t != 7) {  // o = B(2) o
+                    lh_word t7;
+#pragma unroll
+                    for (int q = 0; q < LH_NW; ++q) t7.v[q] = o[0].v[q] ^ o[1].v[q] ^ o[2].v[q] ^ o[7].v[q];
+#pragma unroll
+                    for (int y = 0; y < 7; ++y) o[y] = o[y + 1];
+                    o[7] = t7;
+                }
+#pragma unroll
+                for (int r = 0; r < LH_M; ++r) {
+                    const int idx = i * LH_M + r;
+                    // 0 or ~0: bit t of coef[i][r], sign-extended (one v_bfe_i32)
+                    const unsigned int mask =
+                        (unsigned int)((int)(coefw[idx / 4] << (31 - (8 * (idx % 4) + t))) >> 31);
+#pragma unroll
+                    for (int y = 0; y < 8; ++y)
+#pragma unroll
+                        for (int q = 0; q < LH_NW; ++q) o[y].v[q] ^= v[r][y].v[q] & mask;
+                }
+#pragma unroll
+                for (int y = 0; y < 8; ++y)
+#pragma unroll
+                    for (int q = 0; q < LH_NW; ++q) asm volatile("" : "+v"(o[y].v[q]));
+            }
+            unsigned char *dst = base + (long long)LH_BYTE(outw, i) * LH_BYTES;
+#pragma unroll
+            for (int y = 0; y < 8; ++y) lh_store(dst + y * LH_SUB, o[y]);
+        }
+    }
+}

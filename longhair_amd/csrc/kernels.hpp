@@ -1,0 +1,94 @@
+// kernels.hpp -- argument blocks and launchers shared by the host code and kernels.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lh {
+
+constexpr int kGenericTileOut = 4;  // outputs per lane in lh_apply_generic_kernel
+
+// Per-stripe decode plan record (written by lh_plan_kernel):
+//   [0] e (erasures to recover)   [1] status (int8)   [2..15] reserved
+//   [16]                     out_slot[e_max]   slot receiving the i-th recovered original
+//   [16+e_max]               src_slot[k]       slot of original x, 0xFF if erased
+//   [16+e_max+k]             rec_slot[m]       slot of recovery row r, 0xFF if absent
+//   [16+e_max+k+m]           coef[e_max][m]    A^-1 over recovery rows (0 = unused row)
+//   [16+e_max+k+m+e_max*m]   w[e_max][k]       per-slot coefficients of the recovered
+//                                              originals (single-pass form)
+struct PlanView {
+    uint8_t *p;
+    int k, m, e_max;
+    __host__ __device__ PlanView(uint8_t *p_, int k_, int m_, int e_max_) : p(p_), k(k_), m(m_), e_max(e_max_) {}
+    __host__ __device__ PlanView(const uint8_t *p_, int k_, int m_, int e_max_)
+        : p(const_cast<uint8_t *>(p_)), k(k_), m(m_), e_max(e_max_) {}
+    __host__ __device__ static long long bytes(int k, int m, int e_max) {
+        long long n = 16 + e_max + k + m + (long long)e_max * m + (long long)e_max * k;
+        return (n + 15) / 16 * 16;
+    }
+    __host__ __device__ int e() const { return p[0]; }
+    __host__ __device__ int out_slot(int i) const { return p[16 + i]; }
+    __host__ __device__ void set_out_slot(int i, uint8_t v) { p[16 + i] = v; }
+    __host__ __device__ int src_slot(int x) const { return p[16 + e_max + x]; }
+    __host__ __device__ void set_src_slot(int x, uint8_t v) { p[16 + e_max + x] = v; }
+    __host__ __device__ int rec_slot(int r) const { return p[16 + e_max + k + r]; }
+    __host__ __device__ void set_rec_slot(int r, uint8_t v) { p[16 + e_max + k + r] = v; }
+    __host__ __device__ uint8_t *coef_ptr() const { return p + 16 + e_max + k + m; }
+    __host__ __device__ void set_coef(int i, int r, uint8_t v) { coef_ptr()[i * m + r] = v; }
+    __host__ __device__ uint8_t *w_ptr() const { return p + 16 + e_max + k + m + e_max * m; }
+    __host__ __device__ void set_w(int i, int slot, uint8_t v) { w_ptr()[i * k + slot] = v; }
+    __host__ __device__ static long long w_offset(int k, int m, int e_max) {
+        return 16 + e_max + k + m + (long long)e_max * m;
+    }
+};
+
+struct ApplyArgs {
+    const uint8_t *in;            // stripe s, input j: in + s*in_stride + j*bytes
+    long long in_stride;
+    uint8_t *out;                 // stripe s, output i: out + s*out_stride + i*bytes
+    long long out_stride;
+    const uint8_t *coef;          // coef[s*coef_stride + i*n_in + j]  (stride 0: shared)
+    long long coef_stride;
+    const uint8_t *nout_per_stripe;  // optional: valid outputs of stripe s at [s*nout_stride]
+    long long nout_stride;
+    int n_in, n_out, bytes, sub, stripes, nch;
+};
+
+struct XorArgs {
+    const uint8_t *in;            // stripe s, input j: in + s*in_stride + j*bytes
+    long long in_stride;
+    uint8_t *out;                 // stripe s: out + s*out_stride (+ out_slot*bytes with plan)
+    long long out_stride;
+    const uint8_t *plan;          // optional (decode m == 1): output slot from the plan
+    long long plan_stride;
+    int k, m, e_max;
+    int n_in, n_rep, bytes, stripes, nch;
+};
+
+struct ScatterArgs {
+    const uint8_t *work;
+    long long work_stride;
+    uint8_t *blocks;
+    long long blocks_stride;
+    const uint8_t *plan;
+    long long plan_stride;
+    int k, m, e_max, bytes, stripes;
+};
+
+struct PlanArgs {
+    uint8_t *rows;                // stripes x k, rewritten
+    int8_t *status;               // optional, stripes
+    uint8_t *plan;
+    long long plan_stride;
+    const uint8_t *G;             // m x k generator (row 0 = ones)
+    const uint8_t *gf_exp;        // 512
+    const int16_t *gf_log;        // 256
+    int k, m, e_max, stripes;
+};
+
+hipError_t launch_apply_generic(const ApplyArgs &a, int W, hipStream_t st);
+hipError_t launch_xor_reduce(const XorArgs &a, hipStream_t st);
+hipError_t launch_scatter(const ScatterArgs &a, hipStream_t st);
+hipError_t launch_plan(const PlanArgs &a, hipStream_t st);
+
+}  // namespace lh

@@ -1,0 +1,72 @@
+"""CPU-only checks of the C-ABI boundary (no compute without a GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import lhutil
+
+REPO = lhutil.REPO
+
+
+def _declared_functions():
+    names = set()
+    for h in ("cauchy_256.h", "cauchy_256_batch.h"):
+        text = open(os.path.join(REPO, "include", h)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for m in re.finditer(r"^\s*(?:extern\s+)?(?:const\s+)?\w+\s*\*?\s*(\w+)\s*\(", text, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_headers_declare_reference_entry_points():
+    names = _declared_functions()
+    for ref_name in ("_cauchy_256_init", "cauchy_256_encode", "cauchy_256_decode"):
+        assert ref_name in names
+    assert {"cauchy_256_encode_batch", "cauchy_256_decode_batch"} <= names
+
+
+def test_library_exports_every_declared_symbol():
+    import longhair_amd
+    from longhair_amd import _native
+    lib = ctypes.CDLL(_native.library_path)
+    for name in _declared_functions():
+        assert hasattr(lib, name), name
+    assert set(_native.EXPORTS) == _declared_functions()
+    assert longhair_amd.lib() is not None
+
+
+def test_block_layout_matches_reference():
+    import longhair_amd
+    assert ctypes.sizeof(longhair_amd.Block) == 16
+    assert longhair_amd.Block.row.offset == 8
+
+
+def test_version_mismatch_rejected_without_gpu():
+    import longhair_amd
+    assert longhair_amd._cauchy_256_init(1) == -1
+
+
+def test_specialisation_policy():
+    import longhair_amd
+    assert longhair_amd.batch_path(29, 4, 1296) == "jit"
+    assert longhair_amd.batch_path(29, 4, 1296, decode=True) == "jit"
+    assert longhair_amd.batch_path(128, 32, 8192) == "generic"
+
+
+def test_no_silent_cpu_path():
+    """Without a GPU every codec call must fail loudly (-2), never compute on the CPU."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import numpy as np
+    import longhair_amd
+    k, m, nbytes = 4, 2, 16
+    data = lhutil.fill(1, k * nbytes)
+    ptrs = (ctypes.POINTER(ctypes.c_ubyte) * k)()
+    for x in range(k):
+        ptrs[x] = ctypes.cast(data.ctypes.data + x * nbytes, ctypes.POINTER(ctypes.c_ubyte))
+    rec = np.zeros(m * nbytes, dtype=np.uint8)
+    assert longhair_amd.cauchy_256_encode(k, m, ptrs, rec, nbytes) == -2
+    assert not rec.any()

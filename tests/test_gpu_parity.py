@@ -1,0 +1,218 @@
+"""GPU parity: the HIP codec (through the C ABI) against the reference's golden fixtures and
+the C oracle.  Bit-exact everywhere (integer/byte work).  Run with `-m gpu` on an MI355X."""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+import lhutil
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lh():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need an MI355X"
+    import longhair_amd
+    assert longhair_amd.cauchy_256_init() == 0
+    return longhair_amd
+
+
+@pytest.fixture(params=["jit", "generic"])
+def path(request, monkeypatch):
+    if request.param == "generic":
+        monkeypatch.setenv("LONGHAIR_AMD_PATH", "generic")
+    else:
+        monkeypatch.delenv("LONGHAIR_AMD_PATH", raising=False)
+    return request.param
+
+
+def _load(name):
+    return json.load(open(os.path.join(lhutil.GOLDEN, name)))
+
+
+class DropIn(lhutil._Codec):
+    """The product's drop-in entry points driven exactly like the reference (host memory)."""
+
+    def __init__(self, lh):
+        lib = lh.lib()
+        super().__init__(lib, lib.cauchy_256_encode, lib.cauchy_256_decode)
+
+
+def _gpu_tensor(arr):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(arr)).cuda()
+
+
+# ----------------------------------------------------------------- drop-in ABI
+
+
+def test_dropin_encode_golden_grid(lh):
+    codec = DropIn(lh)
+    for k, m, bytes_, seed, rc, digest in _load("encode_grid.json")["cases"]:
+        data = lhutil.fill(seed, k * bytes_)
+        got_rc, rec = codec.encode(k, m, data, bytes_)
+        assert got_rc == rc, (k, m, bytes_)
+        if rc != 0:
+            rec = rec[:bytes_]
+        assert lhutil.h64(rec) == digest, (k, m, bytes_)
+
+
+def test_dropin_encode_full_bytes(lh):
+    codec = DropIn(lh)
+    for c in _load("encode_full.json"):
+        data = np.frombuffer(bytes.fromhex(c["data"]), dtype=np.uint8)
+        rc, rec = codec.encode(c["k"], c["m"], data, c["bytes"])
+        assert rc == c["rc"]
+        assert rec.tobytes().hex() == c["recovery"]
+
+
+def test_dropin_decode_golden(lh):
+    codec = DropIn(lh)
+    for c in _load("decode_cases.json"):
+        k, m, bytes_ = c["k"], c["m"], c["bytes"]
+        data = lhutil.fill(c["seed"], k * bytes_).reshape(k, bytes_)
+        rc_e, rec = codec.encode(k, m, data, bytes_)
+        assert rc_e == c["rc_encode"], c["tag"]
+        rec = rec.reshape(m, bytes_)
+        bufs = [(data[x] if kind == "d" else rec[x]).copy() for kind, x in c["slots"]]
+        rc, rows = codec.decode(k, m, bufs, list(c["rows_in"]), bytes_)
+        assert rc == c["rc"], c["tag"]
+        assert rows == c["rows_out"], c["tag"]
+        assert [lhutil.h64(b) for b in bufs] == c["digests"], c["tag"]
+
+
+def test_dropin_device_pointers(lh):
+    """Blocks that already live in device memory go through the same entry points."""
+    import torch
+    k, m, nbytes = 29, 4, 1296
+    data = lhutil.fill(77, k * nbytes)
+    ref_rc, ref_rec = lhutil.Oracle().encode(k, m, data, nbytes)
+    d = _gpu_tensor(data)
+    r = torch.zeros(m * nbytes, dtype=torch.uint8, device="cuda")
+    ptrs = (ctypes.POINTER(ctypes.c_ubyte) * k)()
+    for x in range(k):
+        ptrs[x] = ctypes.cast(d.data_ptr() + x * nbytes, ctypes.POINTER(ctypes.c_ubyte))
+    assert lh.cauchy_256_encode(k, m, ptrs, r.data_ptr(), nbytes) == 0
+    assert r.cpu().numpy().tobytes() == ref_rec.tobytes()
+
+
+# ---------------------------------------------------------------- batched API
+
+
+def _encode_batch_vs_oracle(lh, oracle, k, m, nbytes, stripes, seed):
+    import torch
+    host = lhutil.fill(seed, stripes * k * nbytes).reshape(stripes, k, nbytes)
+    rec = lh.encode_batch(_gpu_tensor(host), m)
+    torch.cuda.synchronize()
+    got = rec.cpu().numpy()
+    for s in range(stripes):
+        rc, exp = oracle.encode(k, m, host[s], nbytes)
+        assert rc == 0
+        assert got[s].tobytes() == exp.tobytes(), (k, m, nbytes, s)
+    return host, got
+
+
+@pytest.mark.parametrize("k,m,nbytes,stripes", [
+    (29, 4, 1296, 257), (29, 2, 1296, 64), (29, 3, 1296, 64), (29, 8, 1296, 32), (4, 2, 16, 100),
+    (10, 6, 8, 200), (17, 6, 520, 40), (64, 5, 4096, 8), (3, 250, 24, 6), (250, 3, 24, 6),
+    (128, 32, 8192, 3), (200, 56, 65536, 1), (2, 2, 8, 1000), (29, 4, 1304, 33), (9, 7, 72, 129),
+])
+def test_encode_batch_vs_oracle(lh, oracle, path, k, m, nbytes, stripes):
+    _encode_batch_vs_oracle(lh, oracle, k, m, nbytes, stripes, seed=k * 7 + m + nbytes)
+
+
+def _decode_scenarios(k, m, nbytes, stripes, seed, e=None):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    slots, rows = [], []
+    for s in range(stripes):
+        ee = e if e is not None else int(rng.integers(0, min(k, m) + 1))
+        sl, rw = lhutil.erasure_case(int(rng.integers(0, 2**31)), k, m, ee)
+        slots.append(sl)
+        rows.append(rw)
+    return slots, rows
+
+
+@pytest.mark.parametrize("k,m,nbytes,stripes,e", [
+    (29, 4, 1296, 300, 4), (29, 4, 1296, 300, None), (29, 2, 16, 100, None), (10, 8, 24, 64, None),
+    (17, 6, 520, 40, None), (128, 32, 8192, 3, 32), (128, 32, 1024, 8, None), (200, 56, 65536, 1, 56),
+    (5, 3, 8, 200, None), (2, 2, 8, 50, 2), (29, 1, 1296, 50, None), (29, 1, 20, 50, None),
+    (1, 3, 16, 10, None),
+])
+def test_decode_batch_vs_oracle(lh, oracle, path, k, m, nbytes, stripes, e):
+    import torch
+    data = lhutil.fill(k + m + nbytes, stripes * k * nbytes).reshape(stripes, k, nbytes)
+    slots, rows = _decode_scenarios(k, m, nbytes, stripes, seed=nbytes + k, e=e)
+    blocks = np.zeros((stripes, k, nbytes), dtype=np.uint8)
+    recs = []
+    for s in range(stripes):
+        rc, rec = oracle.encode(k, m, data[s], nbytes)
+        rec = rec.reshape(m, nbytes)
+        recs.append(rec)
+        for i, (kind, x) in enumerate(slots[s]):
+            blocks[s, i] = data[s, x] if kind == "d" else rec[x]
+    d_blocks = _gpu_tensor(blocks)
+    d_rows = _gpu_tensor(np.array(rows, dtype=np.uint8))
+    status = lh.decode_batch(d_blocks, d_rows, m)
+    torch.cuda.synchronize()
+    got_blocks, got_rows, got_status = d_blocks.cpu().numpy(), d_rows.cpu().numpy(), status.cpu().numpy()
+    assert (got_status == 0).all()
+    for s in range(stripes):
+        bufs = [blocks[s, i].copy() for i in range(k)]
+        rc, exp_rows = oracle.decode(k, m, bufs, list(rows[s]), nbytes)
+        assert rc == 0
+        assert list(got_rows[s]) == exp_rows, s
+        for i in range(k):
+            assert got_blocks[s, i].tobytes() == bufs[i].tobytes(), (s, i)
+
+
+def test_decode_batch_invalid_rows(lh):
+    import torch
+    k, m, nbytes = 6, 3, 16
+    blocks = torch.zeros((2, k, nbytes), dtype=torch.uint8, device="cuda")
+    rows = torch.tensor([[0, 1, 2, 3, 4, 4], [0, 1, 2, 3, 4, 9]], dtype=torch.uint8, device="cuda")
+    status = lh.decode_batch(blocks, rows, m)
+    assert status.cpu().tolist() == [-1, -1]
+    assert rows.cpu().tolist() == [[0, 1, 2, 3, 4, 4], [0, 1, 2, 3, 4, 9]]
+
+
+def test_batch_invalid_params(lh):
+    import torch
+    x = torch.zeros((2, 200, 16), dtype=torch.uint8, device="cuda")
+    with pytest.raises(lh.LonghairError):
+        lh.encode_batch(x, 57)
+    # Recovery block 0 was still produced, as the reference does before validating.
+    y = torch.full((2, 200, 12), 3, dtype=torch.uint8, device="cuda")
+    with pytest.raises(lh.LonghairError):
+        lh.encode_batch(y, 4)
+
+
+def test_baseline_scale_roundtrip(lh):
+    """BASELINE.json configs[1] at full size: 65536 stripes of k=29, m=4, 1296 B: encode,
+    erase 4 random originals per stripe, decode; every stripe must return its data, and a
+    sample of stripes must match the oracle byte for byte."""
+    import torch
+    k, m, nbytes, stripes = 29, 4, 1296, 65536
+    g = torch.Generator(device="cuda").manual_seed(1)
+    data = torch.randint(0, 256, (stripes, k, nbytes), dtype=torch.uint8, device="cuda", generator=g)
+    rec = lh.encode_batch(data, m)
+    # Per stripe: erase 4 originals (random), keep order of the rest, recovery at the end.
+    perm = torch.argsort(torch.rand(stripes, k, device="cuda", generator=g), dim=1)
+    keep = perm[:, : k - 4].sort(dim=1).values
+    blocks = torch.empty_like(data)
+    blocks[:, : k - 4] = torch.gather(data, 1, keep.unsqueeze(-1).expand(-1, -1, nbytes))
+    blocks[:, k - 4:] = rec
+    rows = torch.cat([keep, torch.arange(k, k + 4, device="cuda").expand(stripes, 4)], dim=1).to(torch.uint8)
+    status = lh.decode_batch(blocks, rows, m)
+    torch.cuda.synchronize()
+    assert int((status != 0).sum()) == 0
+    order = rows.long().argsort(dim=1)
+    restored = torch.gather(blocks, 1, order.unsqueeze(-1).expand(-1, -1, nbytes))
+    assert torch.equal(restored, data)
+    oracle = lhutil.Oracle()
+    for s in [0, 1, 2, 4095, 30000, stripes - 1]:
+        rc, exp = oracle.encode(k, m, data[s].cpu().numpy(), nbytes)
+        assert rec[s].cpu().numpy().tobytes() == exp.tobytes()
