@@ -152,6 +152,18 @@ static int workspace(Device *d, hipStream_t st, size_t plan_bytes, size_t work_b
     return kOk;
 }
 
+// Grid for a specialised kernel: one 4-wave block per 4 waves of work, optionally capped
+// (LONGHAIR_AMD_GRID) to run persistent, grid-stride waves.
+static long long jit_blocks(const JitConfig &cfg, int stripes) {
+    const long long waves = cfg.spw ? (stripes + cfg.spw - 1) / cfg.spw : (long long)stripes * cfg.wps;
+    long long blocks = (waves + 3) / 4;
+    if (const char *g = std::getenv("LONGHAIR_AMD_GRID")) {
+        const long long cap = std::atoll(g);
+        if (cap > 0 && blocks > cap) blocks = cap;
+    }
+    return blocks;
+}
+
 static int generic_word(int sub) {
     if (sub >= 4) return 4;
     if (sub >= 2) return 2;
@@ -198,8 +210,7 @@ static int encode_batch(int k, int m, int bytes, int stripes, const uint8_t *d_d
         std::string err;
         const JitKernels *jk = allow_compile ? d->jit.get(cfg, &err) : d->jit.peek(cfg);
         if (jk) {
-            const long long waves = cfg.spw ? (stripes + cfg.spw - 1) / cfg.spw : (long long)stripes * cfg.wps;
-            const long long blocks = (waves + 3) / 4;
+            const long long blocks = jit_blocks(cfg, stripes);
             if (blocks > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
             long long in_stride = data_stride, out_stride = rec_stride;
             int n = stripes;
@@ -270,6 +281,7 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
     pa.m = m;
     pa.e_max = e_max;
     pa.stripes = stripes;
+    pa.want_w = generic ? 1 : 0;
     LH_HIP(launch_plan(pa, st));
     if (k <= 1) return kOk;
 
@@ -295,8 +307,7 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
     if (jk) {
         const uint8_t *zero = nullptr;
         if (int rc = zero_page(d, (size_t)bytes, &zero)) return rc;
-        const long long waves = cfg.spw ? (stripes + cfg.spw - 1) / cfg.spw : (long long)stripes * cfg.wps;
-        const long long blocks = (waves + 3) / 4;
+        const long long blocks = jit_blocks(cfg, stripes);
         long long s1 = stride, s2 = plan_stride;
         const uint8_t *plan = w->plan.ptr;
         int n = stripes;

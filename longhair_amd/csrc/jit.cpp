@@ -55,6 +55,14 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
             best_nch = nch;
         }
     }
+    if (const char *fw = std::getenv("LONGHAIR_AMD_JIT_W")) {  // tuning override
+        const int W = std::atoi(fw);
+        if ((W == 1 || W == 2 || W == 4 || W == 8 || W == 16) && W <= sub &&
+            rows * 8 * ((W + 3) / 4) <= 2 * kMaxAccDwords) {
+            const int nch = (sub + W - 1) / W;
+            if (!(nch > 64 && decode && sub % W != 0)) { best_w = W; best_nch = nch; }
+        }
+    }
     if (!best_w) return false;
     const int W = best_w, nch2 = best_nch;
     if (nch2 <= 64) spw = 64 / nch2;
@@ -68,11 +76,26 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     cfg->nch = nch2;
     cfg->spw = spw;
     cfg->wps = wps;
+    cfg->defines.clear();
+    if (const char *d = std::getenv("LONGHAIR_AMD_JIT_DEFINES")) cfg->defines = d;
     return true;
 }
 
 std::string jit_source_for(const JitConfig &c) {
     std::ostringstream os;
+    // Tuning knobs "NAME=VALUE" separated by spaces or commas.
+    {
+        std::string tok;
+        for (char ch : c.defines + " ") {
+            if (ch == ' ' || ch == ',') {
+                const size_t eq = tok.find('=');
+                if (!tok.empty()) os << "#define " << (eq == std::string::npos ? tok : tok.substr(0, eq) + " " + tok.substr(eq + 1)) << "\n";
+                tok.clear();
+            } else {
+                tok += ch;
+            }
+        }
+    }
     os << "#define LH_K " << c.k << "\n#define LH_M " << c.m << "\n#define LH_BYTES " << c.bytes
        << "\n#define LH_SUB " << c.sub << "\n#define LH_W " << c.W << "\n#define LH_NCH " << c.nch
        << "\n#define LH_SPW " << (c.spw ? c.spw : 1) << "\n#define LH_WPS " << (c.wps ? c.wps : 1) << "\n";
@@ -95,13 +118,13 @@ std::string jit_source_for(const JitConfig &c) {
 
 const JitKernels *JitCache::peek(const JitConfig &cfg) {
     std::lock_guard<std::mutex> g(mu_);
-    auto it = cache_.find(Key(cfg.k, cfg.m, cfg.bytes, cfg.W));
+    auto it = cache_.find(Key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines));
     return it == cache_.end() ? nullptr : &it->second;
 }
 
 const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err) {
     std::lock_guard<std::mutex> g(mu_);
-    const Key key(cfg.k, cfg.m, cfg.bytes, cfg.W);
+    const Key key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines);
     auto it = cache_.find(key);
     if (it != cache_.end()) return &it->second;
 

@@ -18,6 +18,7 @@ struct JitConfig {
     int nch;   // lanes per stripe = ceil(sub / W)
     int spw;   // stripes per wave (nch <= 64) or 0
     int wps;   // waves per stripe (nch > 64) or 0
+    std::string defines;  // extra -D style tuning knobs (LONGHAIR_AMD_JIT_DEFINES)
     int lanes_per_launch_unit() const { return 64; }
 };
 
@@ -45,7 +46,7 @@ public:
     const JitKernels *peek(const JitConfig &cfg);
 
 private:
-    using Key = std::tuple<int, int, int, int>;
+    using Key = std::tuple<int, int, int, int, std::string>;
     std::mutex mu_;
     std::map<Key, JitKernels> cache_;
 };

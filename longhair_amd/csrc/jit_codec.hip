@@ -41,16 +41,44 @@ struct lh_word {
     unsigned int v[LH_NW];
 };
 
+#ifndef LH_NT
+#define LH_NT 1  // non-temporal (streaming) loads and stores: +3% on k29/m4 (tools/tune.py)
+#endif
+typedef unsigned int lh_u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int lh_u32x4 __attribute__((ext_vector_type(4)));
+
+// W-byte loads/stores at the sub-block's natural (often 2-byte) alignment: gfx950
+// serves unaligned global accesses in hardware.
 __device__ __forceinline__ lh_word lh_load(const unsigned char *p) {
     lh_word w;
+#if LH_NT && LH_W == 16
+    const lh_u32x4 v = __builtin_nontemporal_load((const lh_u32x4 *)p);
+    w.v[0] = v.x; w.v[1] = v.y; w.v[2] = v.z; w.v[3] = v.w;
+#elif LH_NT && LH_W == 8
+    const lh_u32x2 v = __builtin_nontemporal_load((const lh_u32x2 *)p);
+    w.v[0] = v.x; w.v[1] = v.y;
+#elif LH_NT && LH_W == 4
+    w.v[0] = __builtin_nontemporal_load((const unsigned int *)p);
+#else
 #pragma unroll
     for (int i = 0; i < LH_NW; ++i) w.v[i] = 0;
     __builtin_memcpy(&w.v[0], p, LH_W);
+#endif
     return w;
 }
 
 __device__ __forceinline__ void lh_store(unsigned char *p, const lh_word &w) {
+#if LH_NT && LH_W == 16
+    lh_u32x4 v = {w.v[0], w.v[1], w.v[2], w.v[3]};
+    __builtin_nontemporal_store(v, (lh_u32x4 *)p);
+#elif LH_NT && LH_W == 8
+    lh_u32x2 v = {w.v[0], w.v[1]};
+    __builtin_nontemporal_store(v, (lh_u32x2 *)p);
+#elif LH_NT && LH_W == 4
+    __builtin_nontemporal_store(w.v[0], (unsigned int *)p);
+#else
     __builtin_memcpy(p, &w.v[0], LH_W);
+#endif
 }
 
 __device__ __forceinline__ void lh_xor(lh_word &a, const lh_word &b) {
@@ -76,9 +104,18 @@ struct lh_lane {
     bool active;
 };
 
-__device__ __forceinline__ lh_lane lh_map_lane(int stripes) {
+// Waves needed for a batch; kernels loop over them (grid-stride) so the host may launch
+// either one wave per work item or a persistent grid.
+__device__ __forceinline__ long long lh_total_waves(int stripes) {
+#if LH_NCH <= 64
+    return ((long long)stripes + LH_SPW - 1) / LH_SPW;
+#else
+    return (long long)stripes * LH_WPS;
+#endif
+}
+
+__device__ __forceinline__ lh_lane lh_map_lane(int stripes, long long wave) {
     const int lane = threadIdx.x & 63;
-    const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     lh_lane l;
 #if LH_NCH <= 64
     // LH_SPW whole stripes per wave.
@@ -87,8 +124,8 @@ __device__ __forceinline__ lh_lane lh_map_lane(int stripes) {
     l.stripe = wave * LH_SPW + sl;
     l.active = (sl < LH_SPW) && (l.stripe < stripes);
 #else
-    // LH_WPS waves per stripe (the host only picks this when LH_SUB % LH_W == 0, so no
-    // chunk overlaps another wave's bytes).
+    // LH_WPS waves per stripe (the host only picks this when LH_SUB % LH_W == 0 for
+    // decode, so no chunk overlaps another wave's bytes).
     const long long c0 = (wave % LH_WPS) * 64 + lane;
     const int c = (int)c0;
     l.stripe = wave / LH_WPS;
@@ -97,6 +134,12 @@ __device__ __forceinline__ lh_lane lh_map_lane(int stripes) {
     l.p = (c == LH_NCH - 1) ? (LH_SUB - LH_W) : c * LH_W;
     return l;
 }
+
+#define LH_WAVE_LOOP(stripes)                                                                   \
+    const long long lh_nw = lh_total_waves(stripes);                                           \
+    const long long lh_ws = (long long)gridDim.x * (blockDim.x >> 6);                          \
+    for (long long lh_w = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; lh_w < lh_nw; \
+         lh_w += lh_ws)
 
 // Keeps the accumulators in registers between columns: stops the compiler from
 // re-associating XORs across columns (which lengthens live ranges past the register file).
@@ -112,7 +155,7 @@ __device__ __forceinline__ void lh_opaque(lh_word (&acc)[LH_M][8]) {
 // Column loop, unrolled at compile time, with the next LH_PF columns' loads in flight
 // while column X is combined.
 #ifndef LH_PF
-#define LH_PF 2
+#define LH_PF 3  // columns in flight ahead of the one being combined
 #endif
 template <int X>
 struct lh_unroll_encode {
@@ -138,11 +181,10 @@ struct lh_unroll_encode<LH_K> {
     __device__ __forceinline__ static void run(lh_word (&)[LH_M][8], lh_word (&)[LH_PF][8], const unsigned char *) {}
 };
 
-// recovery[s][r] = sum_x B(G[r][x]) data[s][x]   (cauchy_256_encode for m > 1, valid k, m)
-extern "C" __global__ void __launch_bounds__(256)
-lh_jit_encode(const unsigned char *__restrict__ in, long long in_stride,
-              unsigned char *__restrict__ out, long long out_stride, int stripes) {
-    const lh_lane l = lh_map_lane(stripes);
+__device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned char *__restrict__ in,
+                                               long long in_stride, unsigned char *__restrict__ out,
+                                               long long out_stride, int stripes) {
+    const lh_lane l = lh_map_lane(stripes, wave);
     if (!l.active) return;
     lh_word acc[LH_M][8];
 #pragma unroll
@@ -164,6 +206,13 @@ lh_jit_encode(const unsigned char *__restrict__ in, long long in_stride,
     for (int r = 0; r < LH_M; ++r)
 #pragma unroll
         for (int y = 0; y < 8; ++y) lh_store(o + (long long)r * LH_BYTES + y * LH_SUB, acc[r][y]);
+}
+
+// recovery[s][r] = sum_x B(G[r][x]) data[s][x]   (cauchy_256_encode for m > 1, valid k, m)
+extern "C" __global__ void __launch_bounds__(256)
+lh_jit_encode(const unsigned char *__restrict__ in, long long in_stride,
+              unsigned char *__restrict__ out, long long out_stride, int stripes) {
+    LH_WAVE_LOOP(stripes) { lh_encode_wave(lh_w, in, in_stride, out, out_stride, stripes); }
 }
 
 // ------------------------------------------------------------------------ decode
@@ -232,11 +281,11 @@ struct lh_unroll_decode<LH_K> {
 // recovery row r (erased columns read the zero page, absent rows contribute R_r = 0).
 // Phase B: D_{E_i} = sum_r B(coef[i][r]) V_r with the per-stripe inverse from the plan,
 // by Horner over the coefficient bits: B(c) v = B(2)(...B(2)(c_7 v)...) + c_0 v.
-extern "C" __global__ void __launch_bounds__(256)
-lh_jit_decode(unsigned char *__restrict__ blocks, long long stripe_stride,
-              const unsigned char *__restrict__ plan, long long plan_stride,
-              const unsigned char *__restrict__ zero_page, int stripes) {
-    const lh_lane l = lh_map_lane(stripes);
+__device__ __forceinline__ void lh_decode_wave(long long wave, unsigned char *__restrict__ blocks,
+                                               long long stripe_stride, const unsigned char *__restrict__ plan,
+                                               long long plan_stride, const unsigned char *__restrict__ zero_page,
+                                               int stripes) {
+    const lh_lane l = lh_map_lane(stripes, wave);
     if (!l.active) return;
     const unsigned char *pl = plan + l.stripe * plan_stride;
     const int e = pl[0];
@@ -318,4 +367,11 @@ lh_jit_decode(unsigned char *__restrict__ blocks, long long stripe_stride,
             for (int y = 0; y < 8; ++y) lh_store(dst + y * LH_SUB, o[y]);
         }
     }
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+lh_jit_decode(unsigned char *__restrict__ blocks, long long stripe_stride,
+              const unsigned char *__restrict__ plan, long long plan_stride,
+              const unsigned char *__restrict__ zero_page, int stripes) {
+    LH_WAVE_LOOP(stripes) { lh_decode_wave(lh_w, blocks, stripe_stride, plan, plan_stride, zero_page, stripes); }
 }

@@ -353,6 +353,157 @@ __global__ void __launch_bounds__(64) lh_plan_kernel(lh::PlanArgs a) {
     for (int i = lane; i < k; i += 64) rws[i] = rows[i];
 }
 
+// ------------------------------------------------------- decode plan, small e_max
+// One thread per stripe for e_max <= EM (m <= 8 or k <= 8): the e x e inverse lives in
+// registers (padded to EM x EM with an identity block so every loop bound is a compile-
+// time constant), GF(256) log/exp tables in LDS.  Same record as lh_plan_kernel.
+template <int EM>
+__global__ void __launch_bounds__(256) lh_plan_small_kernel(lh::PlanArgs a) {
+    __shared__ uint8_t gexp[512];
+    __shared__ int16_t glog[256];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        gexp[i] = a.gf_exp[i];
+        gexp[i + 256] = a.gf_exp[i + 256];
+        glog[i] = a.gf_log[i];
+    }
+    __syncthreads();
+    const long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.stripes) return;
+    const int k = a.k, m = a.m, e_max = a.e_max;
+    auto gmul = [&](uint32_t x, uint32_t y) -> uint32_t {
+        return (x && y) ? gexp[glog[x] + glog[y]] : 0u;
+    };
+    uint8_t *rws = a.rows + s * k;
+    uint8_t *rec = a.plan + s * a.plan_stride;
+    lh::PlanView pv(rec, k, m, e_max);
+
+    // Classify slots (reference sort_blocks): seen-bitmap over rows, recovery slots in
+    // array order; rows outside the code or repeated invalidate the stripe.
+    uint32_t seen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int n_rcv = 0, status = 0;
+    uint32_t rslot[EM], rrow[EM];
+#pragma unroll
+    for (int i = 0; i < EM; ++i) rslot[i] = rrow[i] = 0;
+    for (int x = 0; x < k; ++x) pv.set_src_slot(x, 0xFF);
+    for (int i = 0; i < k; ++i) {
+        const uint32_t r = rws[i];
+        const uint32_t bit = 1u << (r & 31);
+        uint32_t w = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) if ((int)(r >> 5) == q) w = seen[q];
+        if (r >= (uint32_t)(k + m) || (w & bit)) status = -1;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) if ((int)(r >> 5) == q) seen[q] |= bit;
+        if (r < (uint32_t)k) {
+            pv.set_src_slot(r, (uint8_t)i);
+        } else {
+#pragma unroll
+            for (int q = 0; q < EM; ++q) if (q == n_rcv) { rslot[q] = i; rrow[q] = r - k; }
+            ++n_rcv;
+        }
+    }
+    if (n_rcv > e_max) status = -1;
+    if (a.status) a.status[s] = (int8_t)status;
+    rec[1] = (uint8_t)(int8_t)status;
+    if (status != 0 || n_rcv == 0) {
+        rec[0] = 0;
+        return;
+    }
+    const int e = n_rcv;
+    rec[0] = (uint8_t)e;
+    // Missing originals, ascending.
+    uint32_t er[EM];
+#pragma unroll
+    for (int i = 0; i < EM; ++i) er[i] = 0;
+    for (int x = 0, j = 0; x < k && j < e; ++x) {
+        if (!((seen[x >> 5] >> (x & 31)) & 1u)) {
+#pragma unroll
+            for (int q = 0; q < EM; ++q) if (q == j) er[q] = x;
+            ++j;
+        }
+    }
+    // [A | I], A[i][j] = G[r_i][E_j], identity padding beyond e.
+    uint32_t A[EM][EM], I[EM][EM];
+#pragma unroll
+    for (int i = 0; i < EM; ++i)
+#pragma unroll
+        for (int j = 0; j < EM; ++j) {
+            uint32_t v;
+            if (i < e && j < e) v = a.G[rrow[i] * k + er[j]];
+            else v = (i == j) ? 1u : 0u;
+            A[i][j] = v;
+            I[i][j] = (i == j) ? 1u : 0u;
+        }
+#pragma unroll
+    for (int c = 0; c < EM; ++c) {
+        // Pivot: first row p >= c with A[p][c] != 0; swap into row c.
+        int p = -1;
+#pragma unroll
+        for (int r = EM - 1; r >= c; --r) if (A[r][c]) p = r;
+        if (p < 0) { status = -1; break; }
+#pragma unroll
+        for (int r = c + 1; r < EM; ++r) {
+            if (r == p) {
+#pragma unroll
+                for (int j = 0; j < EM; ++j) {
+                    uint32_t t = A[c][j]; A[c][j] = A[r][j]; A[r][j] = t;
+                    t = I[c][j]; I[c][j] = I[r][j]; I[r][j] = t;
+                }
+            }
+        }
+        const uint32_t inv = gexp[255 - glog[A[c][c]]];
+#pragma unroll
+        for (int j = 0; j < EM; ++j) { A[c][j] = gmul(A[c][j], inv); I[c][j] = gmul(I[c][j], inv); }
+#pragma unroll
+        for (int r = 0; r < EM; ++r) {
+            if (r == c) continue;
+            const uint32_t f = A[r][c];
+            if (f) {
+#pragma unroll
+                for (int j = 0; j < EM; ++j) { A[r][j] ^= gmul(f, A[c][j]); I[r][j] ^= gmul(f, I[c][j]); }
+            }
+        }
+    }
+    if (status != 0) {
+        rec[0] = 0;
+        rec[1] = 0xFF;
+        if (a.status) a.status[s] = -1;
+        return;
+    }
+    // Emit out slots, recovery slot map and coef[i][r] (A^-1 over recovery rows).
+    for (int r = 0; r < m; ++r) pv.set_rec_slot(r, 0xFF);
+    for (int q = 0; q < e_max * m; ++q) pv.set_coef(q / m, q % m, 0);
+#pragma unroll
+    for (int i = 0; i < EM; ++i) {
+        if (i < e) {
+            pv.set_out_slot(i, (uint8_t)rslot[i]);
+            pv.set_rec_slot(rrow[i], (uint8_t)rslot[i]);
+#pragma unroll
+            for (int j = 0; j < EM; ++j) if (j < e) pv.set_coef(i, rrow[j], (uint8_t)I[i][j]);
+        }
+    }
+    if (a.want_w) {
+        for (int slot = 0; slot < k; ++slot) {
+            const uint32_t r = rws[slot];
+#pragma unroll
+            for (int i = 0; i < EM; ++i) {
+                if (i >= e) continue;
+                uint32_t v = 0;
+#pragma unroll
+                for (int j = 0; j < EM; ++j) {
+                    if (j >= e) continue;
+                    if (r >= (uint32_t)k) { if (rslot[j] == (uint32_t)slot) v = I[i][j]; }
+                    else v ^= gmul(I[i][j], a.G[rrow[j] * k + r]);
+                }
+                pv.set_w(i, slot, (uint8_t)v);
+            }
+        }
+    }
+    // Recovery slot i takes missing row E_i (reference generate_bitmatrix, :786).
+#pragma unroll
+    for (int i = 0; i < EM; ++i) if (i < e) rws[rslot[i]] = (uint8_t)er[i];
+}
+
 // ------------------------------------------------------------------ host launchers
 namespace lh {
 
@@ -381,6 +532,12 @@ hipError_t launch_scatter(const ScatterArgs &a, hipStream_t st) {
 }
 
 hipError_t launch_plan(const PlanArgs &a, hipStream_t st) {
+    if (a.k > 1 && a.m > 1 && a.e_max <= 8) {
+        const unsigned blocks = (unsigned)((a.stripes + 255) / 256);
+        if (a.e_max <= 4) hipLaunchKernelGGL(lh_plan_small_kernel<4>, dim3(blocks), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL(lh_plan_small_kernel<8>, dim3(blocks), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     const size_t lds = (size_t)a.e_max * 2 * a.e_max;
     hipLaunchKernelGGL(lh_plan_kernel, dim3((unsigned)a.stripes), dim3(64), lds, st, a);
     return hipGetLastError();

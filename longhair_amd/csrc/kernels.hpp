@@ -84,6 +84,7 @@ struct PlanArgs {
     const uint8_t *gf_exp;        // 512
     const int16_t *gf_log;        // 256
     int k, m, e_max, stripes;
+    int want_w;                   // emit the single-pass coefficients (generic path)
 };
 
 hipError_t launch_apply_generic(const ApplyArgs &a, int W, hipStream_t st);

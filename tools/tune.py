@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Tuning sweep for the specialised kernels (one process, interleaved variants).
+
+For each variant (env knobs read by the library at JIT time: LONGHAIR_AMD_JIT_DEFINES,
+LONGHAIR_AMD_JIT_W, LONGHAIR_AMD_GRID) it times encode_batch and decode_batch on the
+bench workload with HIP events and checks the bytes against the default variant.
+Usage: python tools/tune.py [k m bytes stripes] > gpurun_out/tune.txt
+"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import longhair_amd as lh  # noqa: E402
+
+VARIANTS = [
+    ("base", {}),
+    ("pf1", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=1"}),
+    ("pf3", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=3"}),
+    ("pf4", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=4"}),
+    ("nt", {"LONGHAIR_AMD_JIT_DEFINES": "LH_NT=1"}),
+    ("nt_pf3", {"LONGHAIR_AMD_JIT_DEFINES": "LH_NT=1,LH_PF=3"}),
+    ("w4", {"LONGHAIR_AMD_JIT_W": "4"}),
+    ("w16", {"LONGHAIR_AMD_JIT_W": "16"}),
+    ("grid1024", {"LONGHAIR_AMD_GRID": "1024"}),
+    ("grid2048", {"LONGHAIR_AMD_GRID": "2048"}),
+    ("grid4096", {"LONGHAIR_AMD_GRID": "4096"}),
+]
+KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID"]
+
+
+def main():
+    k, m, nbytes, stripes = (int(a) for a in sys.argv[1:5]) if len(sys.argv) >= 5 else (29, 4, 1296, 65536)
+    torch.cuda.set_device(0)
+    assert lh.cauchy_256_init() == 0
+    X, D, rows0 = bench.make_workload(k, m, nbytes, stripes, seed=7)
+    e = min(k, m)
+    rec_view = D[:, k - e:]
+    rows = rows0.clone()
+    ref_rec = None
+    results = {name: ([], []) for name, _ in VARIANTS}
+    reps = 10
+    for rnd in range(3):
+        for name, env in VARIANTS:
+            for key in KNOBS:
+                os.environ.pop(key, None)
+            os.environ.update(env)
+            lh.prepare(k, m, nbytes, stripes)
+            lh.encode_batch(X, m, recovery=rec_view)
+            torch.cuda.synchronize()
+            if ref_rec is None:
+                ref_rec = rec_view.clone()
+            elif rnd == 0:
+                assert torch.equal(rec_view, ref_rec), f"{name}: encode bytes differ"
+            rows.copy_(rows0)
+            lh.decode_batch(D, rows, m)
+            torch.cuda.synchronize()
+            if rnd == 0:
+                order = rows.long().argsort(dim=1)
+                ok = torch.equal(torch.gather(D, 1, order.unsqueeze(-1).expand(-1, -1, nbytes)), X)
+                assert ok, f"{name}: decode did not restore the data"
+            s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s0.record()
+            for _ in range(reps):
+                lh.encode_batch(X, m, recovery=rec_view)
+            s1.record()
+            torch.cuda.synchronize()
+            results[name][0].append(s0.elapsed_time(s1) / reps)
+            tot = 0.0
+            for _ in range(reps):
+                lh.encode_batch(X, m, recovery=rec_view)
+                rows.copy_(rows0)
+                d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                d0.record()
+                lh.decode_batch(D, rows, m)
+                d1.record()
+                torch.cuda.synchronize()
+                tot += d0.elapsed_time(d1)
+            results[name][1].append(tot / reps)
+    inb = k * nbytes * stripes
+    print(f"k={k} m={m} bytes={nbytes} stripes={stripes} path enc={lh.batch_path(k, m, nbytes)} "
+          f"dec={lh.batch_path(k, m, nbytes, True)}")
+    for name, (enc, dec) in results.items():
+        em, dm = min(enc), min(dec)
+        print(f"{name:10s} encode {em:.4f} ms {inb / em / 1e6:8.1f} GB/s in ({(k + m) * nbytes * stripes / em / 1e6:7.1f} alg)"
+              f" | decode {dm:.4f} ms {inb / dm / 1e6:8.1f} GB/s in   [enc runs {['%.3f' % x for x in enc]}]")
+
+
+if __name__ == "__main__":
+    main()
