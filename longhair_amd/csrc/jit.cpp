@@ -159,6 +159,10 @@ const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err) {
         *err = "hipModuleLoadData/GetFunction failed for the specialised kernels";
         return nullptr;
     }
+    if (hipModuleGetFunction(&kern.encode_dma, kern.module, "lh_jit_encode_dma") != hipSuccess) {
+        (void)hipGetLastError();
+        kern.encode_dma = nullptr;
+    }
     auto res = cache_.emplace(key, kern);
     return &res.first->second;
 }

@@ -26,6 +26,7 @@ struct JitKernels {
     hipModule_t module = nullptr;
     hipFunction_t encode = nullptr;
     hipFunction_t decode = nullptr;
+    hipFunction_t encode_dma = nullptr;  // present when compiled with LH_DMA=1
     JitConfig cfg{};
 };
 

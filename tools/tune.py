@@ -19,16 +19,12 @@ import longhair_amd as lh  # noqa: E402
 
 VARIANTS = [
     ("base", {}),
-    ("pf1", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=1"}),
-    ("pf3", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=3"}),
-    ("pf4", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=4"}),
-    ("nt", {"LONGHAIR_AMD_JIT_DEFINES": "LH_NT=1"}),
-    ("nt_pf3", {"LONGHAIR_AMD_JIT_DEFINES": "LH_NT=1,LH_PF=3"}),
-    ("w4", {"LONGHAIR_AMD_JIT_W": "4"}),
-    ("w16", {"LONGHAIR_AMD_JIT_W": "16"}),
-    ("grid1024", {"LONGHAIR_AMD_GRID": "1024"}),
-    ("grid2048", {"LONGHAIR_AMD_GRID": "2048"}),
-    ("grid4096", {"LONGHAIR_AMD_GRID": "4096"}),
+    ("dma_x1d2", {"LONGHAIR_AMD_JIT_DEFINES": "LH_DMA=1,LH_DMA_X=1,LH_DMA_D=2"}),
+    ("dma_x1d3", {"LONGHAIR_AMD_JIT_DEFINES": "LH_DMA=1,LH_DMA_X=1,LH_DMA_D=3"}),
+    ("dma_x1d4", {"LONGHAIR_AMD_JIT_DEFINES": "LH_DMA=1,LH_DMA_X=1,LH_DMA_D=4"}),
+    ("dma_x2d2", {"LONGHAIR_AMD_JIT_DEFINES": "LH_DMA=1,LH_DMA_X=2,LH_DMA_D=2"}),
+    ("dma_x2d3", {"LONGHAIR_AMD_JIT_DEFINES": "LH_DMA=1,LH_DMA_X=2,LH_DMA_D=3"}),
+    ("dma_x1d3nt0", {"LONGHAIR_AMD_JIT_DEFINES": "LH_DMA=1,LH_DMA_X=1,LH_DMA_D=3,LH_NT=0"}),
 ]
 KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID"]
 

@@ -49,6 +49,19 @@ __global__ void stripe_pattern(const uint8_t* __restrict__ in, uint8_t* __restri
   for (int y = 0; y < 8; ++y) __builtin_memcpy(o + y * sub, &acc[y], W);
 }
 
+// Ideal traffic for k=29/m=4: every input byte read once with 16 B/lane coalesced
+// loads, every output byte written once with 16 B/lane stores (outputs are XORs of
+// disjoint column sets).  Lower bound on encode time for this read/write mix.
+__global__ void ideal_stripe(const u32x4* __restrict__ in, u32x4* __restrict__ out, long nout, int k, int m, int cpb) {
+  for (long o = blockIdx.x * (long)blockDim.x + threadIdx.x; o < nout; o += (long)gridDim.x * blockDim.x) {
+    long s = o / (m * cpb); int rem = (int)(o % (m * cpb)); int r = rem / cpb, c = rem % cpb;
+    u32x4 acc = {0,0,0,0};
+    const u32x4* src = in + s * (long)k * cpb + c;
+    for (int x = r; x < k; x += m) acc ^= __builtin_nontemporal_load(src + (long)x * cpb);
+    __builtin_nontemporal_store(acc, out + o);
+  }
+}
+
 int main() {
   const int k = 29, bytes = 1296, stripes = 65536;
   size_t in_bytes = (size_t)stripes * k * bytes, out_bytes = (size_t)stripes * bytes;
@@ -77,6 +90,11 @@ int main() {
 #define PAT(W) { int nch = (bytes/8 + W - 1)/W; long thr = (long)stripes * nch; int grid = (int)((thr + 255)/256); \
     timeit("pattern W=" #W, (double)in_bytes, [&]{ stripe_pattern<W><<<grid,256>>>(din, dout, stripes, k, bytes); }); }
   PAT(2) PAT(4) PAT(8) PAT(16)
+  { const int m = 4, cpb = bytes / 16; long nout = (long)stripes * m * cpb;
+    uint8_t* dout2; CK(hipMalloc(&dout2, nout * 16));
+    for (int grid : {2048, 4096, 8192, 16384}) { char nm[64]; snprintf(nm, 64, "ideal 29r/4w grid=%d", grid);
+      timeit(nm, (double)in_bytes, [&] { ideal_stripe<<<grid, 256>>>((const u32x4*)din, (u32x4*)dout2, nout, k, m, cpb); }); }
+    printf("  (ideal traffic per launch: %.3f GB read + %.3f GB written)\n", in_bytes / 1e9, nout * 16 / 1e9); }
   CK(hipGetLastError());
   return 0;
 }
