@@ -264,6 +264,20 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         if (!jk && allow_compile) return fail(kHipError, err);
     }
     const bool generic = (k > 1 && m > 1) && !jk;
+    if (jk && jk->decode_fused && std::getenv("LONGHAIR_AMD_NO_FUSED_PLAN") == nullptr) {
+        // Plan computed inside the decode kernel: one launch, no plan workspace.
+        const uint8_t *zero = nullptr;
+        if (int rc = zero_page(d, (size_t)bytes, &zero)) return rc;
+        const long long blocks = jit_blocks(cfg, stripes);
+        long long s1 = stride;
+        const uint8_t *gexp = d->gf_exp;
+        const int16_t *glog = d->gf_log;
+        int n = stripes;
+        void *args[] = {(void *)&d_blocks, &s1, (void *)&d_rows, (void *)&d_status, (void *)&zero,
+                        (void *)&gexp, (void *)&glog, &n};
+        LH_HIP(hipModuleLaunchKernel(jk->decode_fused, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr));
+        return kOk;
+    }
     const size_t work_bytes = generic ? (size_t)stripes * e_max * bytes : 0;
     Workspace *w = nullptr;
     if (int rc = workspace(d, st, (size_t)stripes * plan_stride, work_bytes, &w)) return rc;

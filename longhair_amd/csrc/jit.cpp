@@ -112,6 +112,13 @@ std::string jit_source_for(const JitConfig &c) {
         os << "}" << (r + 1 < c.m ? "," : "");
     }
     os << "};\n";
+    os << "#define LH_G_INIT {";
+    for (int r = 0; r < c.m; ++r) {
+        os << "{";
+        for (int x = 0; x < c.k; ++x) os << (unsigned)g[(size_t)r * c.k + x] << (x + 1 < c.k ? "," : "");
+        os << "}" << (r + 1 < c.m ? "," : "");
+    }
+    os << "}\n";
     os << lh_jit_source;
     return os.str();
 }
@@ -162,6 +169,10 @@ const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err) {
     if (hipModuleGetFunction(&kern.encode_dma, kern.module, "lh_jit_encode_dma") != hipSuccess) {
         (void)hipGetLastError();
         kern.encode_dma = nullptr;
+    }
+    if (hipModuleGetFunction(&kern.decode_fused, kern.module, "lh_jit_decode_fused") != hipSuccess) {
+        (void)hipGetLastError();
+        kern.decode_fused = nullptr;
     }
     auto res = cache_.emplace(key, kern);
     return &res.first->second;

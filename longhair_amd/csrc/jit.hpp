@@ -26,7 +26,8 @@ struct JitKernels {
     hipModule_t module = nullptr;
     hipFunction_t encode = nullptr;
     hipFunction_t decode = nullptr;
-    hipFunction_t encode_dma = nullptr;  // present when compiled with LH_DMA=1
+    hipFunction_t encode_dma = nullptr;    // present when compiled with LH_DMA=1
+    hipFunction_t decode_fused = nullptr;  // plan computed in-kernel (e_max <= 4)
     JitConfig cfg{};
 };
 

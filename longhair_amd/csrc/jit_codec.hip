@@ -32,6 +32,7 @@ static constexpr unsigned char LH_BM[LH_M][LH_K][8] = {
      {1, 2, 4, 8, 16, 32, 64, 128}, {1, 2, 4, 8, 16, 32, 64, 128}},
     {{1, 2, 4, 8, 16, 32, 64, 128}, {2, 4, 8, 16, 32, 64, 128, 135},
      {3, 6, 12, 24, 48, 96, 192, 7}, {4, 8, 16, 32, 64, 128, 135, 137}}};
+#define LH_G_INIT {{1, 1, 1, 1}, {1, 2, 3, 4}}
 #include <hip/hip_runtime.h>
 #endif
 
@@ -483,46 +484,78 @@ __device__ __forceinline__ const unsigned char *lh_slot_ptr(unsigned int slot, c
     return (slot == 0xFFu) ? zero : base + (long long)slot * LH_BYTES;
 }
 
+// Phase A streams LH_K data columns (erased ones read the zero page) and then the LH_M
+// recovery rows (absent ones read the zero page) through one prefetch ring, so the
+// recovery loads are in flight while the last data columns combine.
+#define LH_DCOLS (LH_K + LH_M)
+#ifndef LH_PF_DEC
+#define LH_PF_DEC 1  // decode prefetch depth (tools/tune.py, fused plan: 1 > 2 > 3)
+#endif
+
+template <int X>
+__device__ __forceinline__ const unsigned char *lh_dcol_src(const unsigned int (&srcw)[LH_NSRC],
+                                                            const unsigned int (&recw)[LH_NREC],
+                                                            const unsigned char *base, const unsigned char *zero) {
+    if (X < LH_K) return lh_slot_ptr(LH_BYTE(srcw, X < LH_K ? X : 0), base, zero);
+    return lh_slot_ptr(LH_BYTE(recw, X >= LH_K ? X - LH_K : 0), base, zero);
+}
+
+template <int X>
+__device__ __forceinline__ void lh_dcombine(lh_word (&acc)[LH_M][8], const lh_word (&d)[8]) {
+    if (X < LH_K) {
+        lh_column<(X < LH_K ? X : 0)>(acc, d);
+    } else {
+#pragma unroll
+        for (int y = 0; y < 8; ++y) lh_xor(acc[X >= LH_K ? X - LH_K : 0][y], d[y]);
+    }
+}
+
 template <int X>
 struct lh_unroll_decode {
-    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], lh_word (&ring)[LH_PF][8],
+    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], lh_word (&ring)[LH_PF_DEC][8],
                                                const unsigned char *base, const unsigned char *zero,
-                                               const unsigned int (&srcw)[LH_NSRC]) {
-        if (X + LH_PF < LH_K) {
-            const unsigned char *src = lh_slot_ptr(LH_BYTE(srcw, X + LH_PF), base, zero);
+                                               const unsigned int (&srcw)[LH_NSRC], const unsigned int (&recw)[LH_NREC]) {
+        if (X + LH_PF_DEC < LH_DCOLS) {
+            const unsigned char *src = lh_dcol_src<(X + LH_PF_DEC < LH_DCOLS ? X + LH_PF_DEC : 0)>(srcw, recw, base, zero);
             lh_word nxt[8];
 #pragma unroll
             for (int b = 0; b < 8; ++b) nxt[b] = lh_load(src + b * LH_SUB);
-            lh_column<X>(acc, ring[X % LH_PF]);
+            lh_dcombine<X>(acc, ring[X % LH_PF_DEC]);
             lh_opaque(acc);
 #pragma unroll
-            for (int b = 0; b < 8; ++b) ring[X % LH_PF][b] = nxt[b];
+            for (int b = 0; b < 8; ++b) ring[X % LH_PF_DEC][b] = nxt[b];
         } else {
-            lh_column<X>(acc, ring[X % LH_PF]);
+            lh_dcombine<X>(acc, ring[X % LH_PF_DEC]);
             lh_opaque(acc);
         }
-        lh_unroll_decode<X + 1>::run(acc, ring, base, zero, srcw);
+        lh_unroll_decode<X + 1>::run(acc, ring, base, zero, srcw, recw);
     }
 };
 template <>
-struct lh_unroll_decode<LH_K> {
-    __device__ __forceinline__ static void run(lh_word (&)[LH_M][8], lh_word (&)[LH_PF][8], const unsigned char *,
-                                               const unsigned char *, const unsigned int (&)[LH_NSRC]) {}
+struct lh_unroll_decode<LH_DCOLS> {
+    __device__ __forceinline__ static void run(lh_word (&)[LH_M][8], lh_word (&)[LH_PF_DEC][8], const unsigned char *,
+                                               const unsigned char *, const unsigned int (&)[LH_NSRC],
+                                               const unsigned int (&)[LH_NREC]) {}
+};
+
+// Per-stripe decode plan in registers: e, packed src/rec slot maps, coef, out slots.
+struct lh_plan_regs {
+    int e;
+    unsigned int srcw[LH_NSRC], recw[LH_NREC], coefw[LH_NCOEF], outw[LH_NOUT];
+};
+
+struct lh_no_prep {
+    __device__ __forceinline__ void operator()(lh_plan_regs &) const {}
 };
 
 // In-place erasure decode.  Phase A: V_r = R_r + sum_{x present} B(G[r][x]) D_x for every
-// recovery row r (erased columns read the zero page, absent rows contribute R_r = 0).
-// Phase B: D_{E_i} = sum_r B(coef[i][r]) V_r with the per-stripe inverse from the plan,
+// recovery row r.  Phase B: D_{E_i} = sum_r B(coef[i][r]) V_r with the per-stripe inverse,
 // by Horner over the coefficient bits: B(c) v = B(2)(...B(2)(c_7 v)...) + c_0 v.
-__device__ __forceinline__ void lh_decode_wave(long long wave, unsigned char *__restrict__ blocks,
-                                               long long stripe_stride, const unsigned char *__restrict__ plan,
-                                               long long plan_stride, const unsigned char *__restrict__ zero_page,
-                                               int stripes) {
-    const lh_lane l = lh_map_lane(stripes, wave);
-    if (!l.active) return;
-    const unsigned char *pl = plan + l.stripe * plan_stride;
-    const int e = pl[0];
-    if (e == 0) return;
+// `prep` runs while the first columns are in flight (the fused kernel solves its plan there).
+template <class PREP>
+__device__ __forceinline__ void lh_decode_body(const lh_lane &l, unsigned char *__restrict__ blocks,
+                                               long long stripe_stride, lh_plan_regs &pr,
+                                               const unsigned char *__restrict__ zero_page, const PREP &prep) {
     unsigned char *base = blocks + l.stripe * stripe_stride + l.p;
     const unsigned char *zero = zero_page + l.p;
 
@@ -534,32 +567,22 @@ __device__ __forceinline__ void lh_decode_wave(long long wave, unsigned char *__
 #pragma unroll
             for (int i = 0; i < LH_NW; ++i) v[r][y].v[i] = 0;
     {
-        unsigned int srcw[LH_NSRC];
-        lh_load_packed(srcw, pl + LH_P_SRC);
-        lh_word ring[LH_PF][8];
+        lh_word ring[LH_PF_DEC][8];
 #pragma unroll
-        for (int q = 0; q < LH_PF; ++q)
-            if (q < LH_K) {
-                const unsigned char *src = lh_slot_ptr(LH_BYTE(srcw, q), base, zero);
+        for (int q = 0; q < LH_PF_DEC; ++q) {
+            const unsigned char *src = (q == 0) ? lh_dcol_src<0>(pr.srcw, pr.recw, base, zero)
+                                     : (q == 1) ? lh_dcol_src<1>(pr.srcw, pr.recw, base, zero)
+                                     : (q == 2) ? lh_dcol_src<2>(pr.srcw, pr.recw, base, zero)
+                                                : lh_dcol_src<3>(pr.srcw, pr.recw, base, zero);
 #pragma unroll
-                for (int b = 0; b < 8; ++b) ring[q][b] = lh_load(src + b * LH_SUB);
-            }
-        lh_unroll_decode<0>::run(v, ring, base, zero, srcw);
-    }
-    asm volatile("" ::: "memory");  // keep the recovery-row loads below phase A
-    {
-        unsigned int recw[LH_NREC];
-        lh_load_packed(recw, pl + LH_P_REC);
-#pragma unroll
-        for (int r = 0; r < LH_M; ++r) {
-            const unsigned char *src = lh_slot_ptr(LH_BYTE(recw, r), base, zero);
-#pragma unroll
-            for (int y = 0; y < 8; ++y) lh_xor(v[r][y], lh_load(src + y * LH_SUB));
+            for (int b = 0; b < 8; ++b) ring[q][b] = lh_load(src + b * LH_SUB);
         }
+        prep(pr);
+        lh_unroll_decode<0>::run(v, ring, base, zero, pr.srcw, pr.recw);
     }
-    unsigned int coefw[LH_NCOEF], outw[LH_NOUT];
-    lh_load_packed(coefw, pl + LH_P_COEF);
-    lh_load_packed(outw, pl + LH_P_OUT);
+    const int e = pr.e;
+    const unsigned int(&coefw)[LH_NCOEF] = pr.coefw;
+    const unsigned int(&outw)[LH_NOUT] = pr.outw;
 
 #pragma unroll
     for (int i = 0; i < LH_EMAX; ++i) {
@@ -602,9 +625,209 @@ __device__ __forceinline__ void lh_decode_wave(long long wave, unsigned char *__
     }
 }
 
+__device__ __forceinline__ void lh_decode_wave(long long wave, unsigned char *__restrict__ blocks,
+                                               long long stripe_stride, const unsigned char *__restrict__ plan,
+                                               long long plan_stride, const unsigned char *__restrict__ zero_page,
+                                               int stripes) {
+    const lh_lane l = lh_map_lane(stripes, wave);
+    if (!l.active) return;
+    const unsigned char *pl = plan + l.stripe * plan_stride;
+    lh_plan_regs pr;
+    pr.e = pl[0];
+    if (pr.e == 0) return;
+    lh_load_packed(pr.srcw, pl + LH_P_SRC);
+    lh_load_packed(pr.recw, pl + LH_P_REC);
+    lh_load_packed(pr.coefw, pl + LH_P_COEF);
+    lh_load_packed(pr.outw, pl + LH_P_OUT);
+    lh_decode_body(l, blocks, stripe_stride, pr, zero_page, lh_no_prep());
+}
+
 extern "C" __global__ void __launch_bounds__(256)
 lh_jit_decode(unsigned char *__restrict__ blocks, long long stripe_stride,
               const unsigned char *__restrict__ plan, long long plan_stride,
               const unsigned char *__restrict__ zero_page, int stripes) {
     LH_WAVE_LOOP(stripes) { lh_decode_wave(lh_w, blocks, stripe_stride, plan, plan_stride, zero_page, stripes); }
 }
+
+// ------------------------------------------------------------ fused decode planner
+// LH_EMAX <= 4: the plan is computed inside the decode kernel, per lane (every lane of a
+// stripe derives the same plan; the wave is SIMD, so redundancy costs no extra time).
+// Slot maps are built in a per-wave LDS scratch; the e x e inverse runs in registers with
+// GF(256) log/exp tables in LDS.  Semantics follow lh_plan_small_kernel (kernels.hip):
+// reference sort_blocks (cauchy_256.cpp:538-570) and generate_bitmatrix's row
+// assignment (:786); duplicate / out-of-range rows mark the stripe invalid, untouched.
+#if LH_EMAX <= 4 && LH_NCH <= 64 && LH_K <= 64
+#define LH_FUSED 1
+static constexpr unsigned char LH_GRAW[LH_M][LH_K] = LH_G_INIT;
+#define LH_P4(n) (((n) + 3) / 4 * 4)
+#define LH_SR (2 * LH_P4(LH_K) + LH_P4(LH_M))  // per-stripe scratch: rows | src map | rec map
+
+__device__ __forceinline__ unsigned int lh_gmul(const unsigned char *gexp, const short *glog, unsigned int a,
+                                                unsigned int b) {
+    return (a && b) ? gexp[glog[a] + glog[b]] : 0u;
+}
+
+// Returns false when the stripe has nothing to do (no erasure or invalid rows).
+// Part 2 of the fused plan (run while the first columns load): invert, pack, rewrite rows.
+struct lh_fused_solve {
+    unsigned int rs[LH_EMAX], rr[LH_EMAX], er[LH_EMAX];
+    unsigned char *grow;
+    const unsigned char *gexp;
+    const short *glog;
+    int c;
+    __device__ __forceinline__ void operator()(lh_plan_regs &pr) const;
+};
+
+// Part 1: slot maps, validity and the erasure / recovery lists.  Returns false when the
+// stripe has nothing to do (no erasure or invalid rows).
+__device__ __forceinline__ bool lh_fused_plan(const lh_lane &l, int c, int sl, unsigned char *scr,
+                                              unsigned char *__restrict__ rows, signed char *__restrict__ status,
+                                              lh_fused_solve &sv, lh_plan_regs &pr) {
+    unsigned char *lrows = scr;
+    unsigned char *lsrc = scr + LH_P4(LH_K);
+    unsigned char *lrec = lsrc + LH_P4(LH_K);
+    unsigned char *grow = rows + l.stripe * LH_K;
+    // Clear the maps (0xFF = absent), then every lane records the rows of its slots.
+    for (int q = c; q < (LH_P4(LH_K) + LH_P4(LH_M)) / 4; q += LH_NCH) ((unsigned int *)lsrc)[q] = 0xFFFFFFFFu;
+    bool bad = false;
+    for (int i = c; i < LH_K; i += LH_NCH) {
+        const unsigned int r = grow[i];
+        lrows[i] = (unsigned char)r;
+        if (r < LH_K) lsrc[r] = (unsigned char)i;
+        else if (r < LH_K + LH_M) lrec[r - LH_K] = (unsigned char)i;
+        else bad = true;
+    }
+    for (int i = c; i < LH_K; i += LH_NCH) {  // a repeated row leaves another slot in the map
+        const unsigned int r = lrows[i];
+        if (r < LH_K + LH_M && (r < LH_K ? lsrc[r] : lrec[r - LH_K]) != i) bad = true;
+    }
+    const unsigned long long lanes_bad = __ballot(bad);
+    const unsigned long long my = ((1ull << LH_NCH) - 1) << (sl * LH_NCH);
+    const bool invalid = (lanes_bad & my) != 0;
+    // Recovery slots in array order and missing originals ascending, as per-stripe bit
+    // masks gathered with wave ballots (slot/row i = c + t * LH_NCH), then unpacked by
+    // lowest-set-bit extraction.
+    unsigned long long rcvmask = 0, ermask = 0;
+#pragma unroll
+    for (int t = 0; t < (LH_K + LH_NCH - 1) / LH_NCH; ++t) {
+        const int i = c + t * LH_NCH;
+        const bool isrcv = (i < LH_K) && (lrows[i] >= LH_K);
+        const bool iser = (i < LH_K) && (lsrc[i] == 0xFF);
+        const unsigned long long lanes = (1ull << LH_NCH) - 1;
+        rcvmask |= ((__ballot(isrcv) >> (sl * LH_NCH)) & lanes) << (t * LH_NCH);
+        ermask |= ((__ballot(iser) >> (sl * LH_NCH)) & lanes) << (t * LH_NCH);
+    }
+    const int nr = __builtin_popcountll(rcvmask);
+    unsigned int rs[LH_EMAX], rr[LH_EMAX], er[LH_EMAX];
+#pragma unroll
+    for (int q = 0; q < LH_EMAX; ++q) {
+        rs[q] = rcvmask ? (unsigned int)__builtin_ctzll(rcvmask) : 0u;
+        er[q] = ermask ? (unsigned int)__builtin_ctzll(ermask) : 0u;
+        rcvmask &= rcvmask - 1;
+        ermask &= ermask - 1;
+        rr[q] = (unsigned int)lrows[rs[q]] - LH_K;
+    }
+    if (invalid || nr > LH_EMAX) {
+        if (c == 0 && status) status[l.stripe] = -1;
+        return false;
+    }
+    if (c == 0 && status) status[l.stripe] = 0;
+    pr.e = nr;
+    if (nr == 0) return false;
+#pragma unroll
+    for (int q = 0; q < LH_EMAX; ++q) { sv.rs[q] = rs[q]; sv.rr[q] = rr[q]; sv.er[q] = er[q]; }
+    sv.grow = grow;
+    sv.c = c;
+#pragma unroll
+    for (int q = 0; q < LH_NSRC; ++q) pr.srcw[q] = ((const unsigned int *)lsrc)[q];
+#pragma unroll
+    for (int q = 0; q < LH_NREC; ++q) pr.recw[q] = ((const unsigned int *)lrec)[q];
+    return true;
+}
+
+__device__ __forceinline__ void lh_fused_solve::operator()(lh_plan_regs &pr) const {
+    const int nr = pr.e;
+    // Gauss-Jordan on A = G[rr_i][er_j], identity-padded to LH_EMAX.
+    unsigned int A[LH_EMAX][LH_EMAX], I[LH_EMAX][LH_EMAX];
+#pragma unroll
+    for (int i = 0; i < LH_EMAX; ++i)
+#pragma unroll
+        for (int j = 0; j < LH_EMAX; ++j) {
+            A[i][j] = (i < nr && j < nr) ? LH_GRAW[rr[i]][er[j]] : (i == j ? 1u : 0u);
+            I[i][j] = (i == j) ? 1u : 0u;
+        }
+#pragma unroll
+    for (int cc = 0; cc < LH_EMAX; ++cc) {
+        int p = cc;
+#pragma unroll
+        for (int r = LH_EMAX - 1; r >= cc; --r) if (A[r][cc]) p = r;
+#pragma unroll
+        for (int r = cc + 1; r < LH_EMAX; ++r)
+            if (r == p)
+#pragma unroll
+                for (int j = 0; j < LH_EMAX; ++j) {
+                    unsigned int t = A[cc][j]; A[cc][j] = A[r][j]; A[r][j] = t;
+                    t = I[cc][j]; I[cc][j] = I[r][j]; I[r][j] = t;
+                }
+        const unsigned int inv = gexp[255 - glog[A[cc][cc]]];
+#pragma unroll
+        for (int j = 0; j < LH_EMAX; ++j) { A[cc][j] = lh_gmul(gexp, glog, A[cc][j], inv); I[cc][j] = lh_gmul(gexp, glog, I[cc][j], inv); }
+#pragma unroll
+        for (int r = 0; r < LH_EMAX; ++r) {
+            if (r == cc) continue;
+            const unsigned int f = A[r][cc];
+#pragma unroll
+            for (int j = 0; j < LH_EMAX; ++j) { A[r][j] ^= lh_gmul(gexp, glog, f, A[cc][j]); I[r][j] ^= lh_gmul(gexp, glog, f, I[cc][j]); }
+        }
+    }
+    // Pack: coef[i][r] = Ainv[i][j] for the recovery row r = rr[j]; out slots; maps.
+#pragma unroll
+    for (int q = 0; q < LH_NCOEF; ++q) pr.coefw[q] = 0;
+#pragma unroll
+    for (int i = 0; i < LH_EMAX; ++i)
+#pragma unroll
+        for (int r = 0; r < LH_M; ++r) {
+            unsigned int v = 0;
+#pragma unroll
+            for (int j = 0; j < LH_EMAX; ++j) if (j < nr && rr[j] == (unsigned int)r) v = I[i][j];
+            const int idx = i * LH_M + r;
+            pr.coefw[idx / 4] |= v << (8 * (idx % 4));
+        }
+#pragma unroll
+    for (int q = 0; q < LH_NOUT; ++q) pr.outw[q] = 0;
+#pragma unroll
+    for (int i = 0; i < LH_EMAX; ++i) pr.outw[i / 4] |= rs[i] << (8 * (i % 4));
+    // Recovery slot i takes missing row er[i] (reference generate_bitmatrix, :786).
+    if (c == 0)
+#pragma unroll
+        for (int i = 0; i < LH_EMAX; ++i) if (i < nr) grow[rs[i]] = (unsigned char)er[i];
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+lh_jit_decode_fused(unsigned char *__restrict__ blocks, long long stripe_stride, unsigned char *__restrict__ rows,
+                    signed char *__restrict__ status, const unsigned char *__restrict__ zero_page,
+                    const unsigned char *__restrict__ gf_exp, const short *__restrict__ gf_log, int stripes) {
+    __shared__ unsigned char gexp[512];
+    __shared__ short glog[256];
+    __shared__ __attribute__((aligned(16))) unsigned char scratch[4][LH_SPW > 0 ? LH_SPW : 1][LH_SR];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        gexp[i] = gf_exp[i];
+        gexp[i + 256] = gf_exp[i + 256];
+        glog[i] = gf_log[i];
+    }
+    __syncthreads();
+    const int wid = threadIdx.x >> 6;
+    LH_WAVE_LOOP(stripes) {
+        const lh_lane l = lh_map_lane(stripes, lh_w);
+        const int lane = threadIdx.x & 63;
+        const int sl = lane / LH_NCH;
+        const int c = lane - sl * LH_NCH;
+        lh_plan_regs pr;
+        lh_fused_solve sv;
+        sv.gexp = gexp;
+        sv.glog = glog;
+        if (l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rows, status, sv, pr))
+            lh_decode_body(l, blocks, stripe_stride, pr, zero_page, sv);
+    }
+}
+#endif  // LH_EMAX <= 4 && LH_NCH <= 64 && LH_K <= 64

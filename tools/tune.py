@@ -19,14 +19,13 @@ import longhair_amd as lh  # noqa: E402
 
 VARIANTS = [
     ("base", {}),
-    ("dma_x1d2", {"LONGHAIR_AMD_JIT_DEFINES": "LH_DMA=1,LH_DMA_X=1,LH_DMA_D=2"}),
-    ("dma_x1d3", {"LONGHAIR_AMD_JIT_DEFINES": "LH_DMA=1,LH_DMA_X=1,LH_DMA_D=3"}),
-    ("dma_x1d4", {"LONGHAIR_AMD_JIT_DEFINES": "LH_DMA=1,LH_DMA_X=1,LH_DMA_D=4"}),
-    ("dma_x2d2", {"LONGHAIR_AMD_JIT_DEFINES": "LH_DMA=1,LH_DMA_X=2,LH_DMA_D=2"}),
-    ("dma_x2d3", {"LONGHAIR_AMD_JIT_DEFINES": "LH_DMA=1,LH_DMA_X=2,LH_DMA_D=3"}),
-    ("dma_x1d3nt0", {"LONGHAIR_AMD_JIT_DEFINES": "LH_DMA=1,LH_DMA_X=1,LH_DMA_D=3,LH_NT=0"}),
+    ("fused_pfd1", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF_DEC=1"}),
+    ("fused_pfd3", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF_DEC=3"}),
+    ("nofused_pfd2", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1"}),
+    ("nofused_pfd3", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1", "LONGHAIR_AMD_JIT_DEFINES": "LH_PF_DEC=3"}),
+    ("nofused_pfd1", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1", "LONGHAIR_AMD_JIT_DEFINES": "LH_PF_DEC=1"}),
 ]
-KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID"]
+KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID", "LONGHAIR_AMD_NO_FUSED_PLAN"]
 
 
 def main():
