@@ -186,12 +186,12 @@ def main():
     value = in_bytes * args.steps / elapsed / 1e9
     enc_alg = float(k + m) * nbytes * stripes           # read k, write m blocks per stripe
     dec_alg = float(k + e) * nbytes * stripes           # read k slots, write e blocks
+    enc_k, dec_k = lh.kernel_names(k, m, nbytes)
     roof = {
-        "encode": {"kernel": "lh_jit_encode" if lh.batch_path(k, m, nbytes) == "jit" else "lh_apply_generic_kernel",
-                   "ms": round(enc_ms, 4), "achieved": round(enc_alg / (enc_ms * 1e-3) / 1e9, 1)},
-        "decode": {"kernel": ("lh_plan_kernel+lh_jit_decode" if lh.batch_path(k, m, nbytes, True) == "jit"
-                              else "lh_plan_kernel+lh_apply_generic_kernel+lh_scatter_kernel"),
-                   "ms": round(dec_ms, 4), "achieved": round(dec_alg / (dec_ms * 1e-3) / 1e9, 1)},
+        "encode": {"kernel": "+".join(enc_k), "ms": round(enc_ms, 4),
+                   "achieved": round(enc_alg / (enc_ms * 1e-3) / 1e9, 1)},
+        "decode": {"kernel": "+".join(dec_k), "ms": round(dec_ms, 4),
+                   "achieved": round(dec_alg / (dec_ms * 1e-3) / 1e9, 1)},
     }
     dom = "decode" if dec_ms > enc_ms else "encode"
     traffic = None

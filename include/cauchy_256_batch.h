@@ -44,8 +44,9 @@ int cauchy_256_decode_batch(int k, int m, int block_bytes, int stripes,
  * a timed region).  Synchronous.  Returns 0 or an error code. */
 int cauchy_256_batch_prepare(int k, int m, int block_bytes, int max_stripes);
 
-/* Which kernel family serves this shape: 1 = run-time specialised (JIT) network,
- * 0 = generic table-driven kernel.  `what` = 0 for encode, 1 for decode. */
+/* Which kernel family serves this shape: 0 = generic coefficient-driven kernels,
+ * 1 = run-time specialised (JIT) network, 2 (decode only) = specialised network with the
+ * erasure plan computed inside the same kernel.  `what` = 0 for encode, 1 for decode. */
 int cauchy_256_batch_path(int k, int m, int block_bytes, int what);
 
 /* Last error message of the calling thread (empty string if none). */

@@ -127,5 +127,18 @@ def prepare(k, m, block_bytes, max_stripes=0):
 
 
 def batch_path(k, m, block_bytes, decode=False):
-    """'jit' when a run-time specialised network serves the shape, else 'generic'."""
-    return "jit" if lib().cauchy_256_batch_path(k, m, block_bytes, 1 if decode else 0) else "generic"
+    """'jit' when a run-time specialised network serves the shape ('jit-fused' for a
+    decode whose plan is computed in the same kernel), else 'generic'."""
+    code = lib().cauchy_256_batch_path(k, m, block_bytes, 1 if decode else 0)
+    return {0: "generic", 1: "jit", 2: "jit-fused"}[code]
+
+
+def kernel_names(k, m, block_bytes):
+    """Names of the kernels one encode_batch / decode_batch launches for this shape."""
+    enc = {"generic": ["lh_apply_generic_kernel"], "jit": ["lh_jit_encode"]}[batch_path(k, m, block_bytes)]
+    dec = {"generic": ["lh_plan_kernel", "lh_apply_generic_kernel", "lh_scatter_kernel"],
+           "jit": ["lh_plan_small_kernel" if min(k, m) <= 8 else "lh_plan_kernel", "lh_jit_decode"],
+           "jit-fused": ["lh_jit_decode_fused"]}[batch_path(k, m, block_bytes, True)]
+    if m == 1 or k == 1:
+        enc, dec = ["lh_xor_reduce_kernel"], ["lh_plan_kernel", "lh_xor_reduce_kernel"]
+    return enc, dec

@@ -540,7 +540,13 @@ LH_API int cauchy_256_batch_prepare(int k, int m, int block_bytes, int max_strip
 
 LH_API int cauchy_256_batch_path(int k, int m, int block_bytes, int what) {
     lh::JitConfig cfg;
-    return lh::jit_config_for(k, m, block_bytes, what == 1, &cfg) ? 1 : 0;
+    if (!lh::jit_config_for(k, m, block_bytes, what == 1, &cfg)) return 0;
+    // Decode: 2 when the plan is computed inside the specialised kernel (jit_codec.hip,
+    // LH_FUSED: e_max <= 4, one stripe per <= 64 lanes, k <= 64).
+    const int e_max = k < m ? k : m;
+    if (what == 1 && e_max <= 4 && cfg.nch <= 64 && k <= 64 && std::getenv("LONGHAIR_AMD_NO_FUSED_PLAN") == nullptr)
+        return 2;
+    return 1;
 }
 
 LH_API const char *cauchy_256_last_error(void) { return lh::g_last_error.c_str(); }

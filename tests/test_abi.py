@@ -51,7 +51,8 @@ def test_version_mismatch_rejected_without_gpu():
 def test_specialisation_policy():
     import longhair_amd
     assert longhair_amd.batch_path(29, 4, 1296) == "jit"
-    assert longhair_amd.batch_path(29, 4, 1296, decode=True) == "jit"
+    assert longhair_amd.batch_path(29, 4, 1296, decode=True) == "jit-fused"
+    assert longhair_amd.batch_path(29, 8, 1296, decode=True) == "jit"
     assert longhair_amd.batch_path(128, 32, 8192) == "generic"
 
 
