@@ -47,9 +47,8 @@ def parse():
 def setup_dist():
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from longhair_amd.shard import world_info
+    world, rank, local = world_info()
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
@@ -65,13 +64,8 @@ def barrier(world):
 
 
 def max_over_ranks(world, value):
-    import torch
-    import torch.distributed as dist
-    if world == 1:
-        return value
-    t = torch.tensor([value], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    from longhair_amd.shard import max_over_ranks as mx
+    return value if world == 1 else mx(value, device="cuda")
 
 
 def make_workload(k, m, nbytes, stripes, seed):

@@ -1,0 +1,80 @@
+"""N > 1 path on CPU: world_size-2 gloo groups exercise the sharding and the
+max-over-ranks aggregation bench.py uses; each rank codes its stripe shard with the
+oracle (no GPU here) and the union must equal the single-process result."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import lhutil
+from longhair_amd.shard import aggregate_rate, max_over_ranks, shard_range
+
+
+def test_shard_range_partitions():
+    for total in (0, 1, 7, 65536, 524288, 1000003):
+        for world in (1, 2, 3, 4, 8):
+            ranges = [shard_range(total, world, r) for r in range(world)]
+            assert ranges[0][0] == 0 and ranges[-1][1] == total
+            for (a, b), (c, d) in zip(ranges, ranges[1:]):
+                assert b == c
+            sizes = [b - a for a, b in ranges]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, total, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    k, m, nbytes = 29, 4, 48
+    oracle = lhutil.Oracle()
+    lo, hi = shard_range(total, world, rank)
+    data = lhutil.fill(11, total * k * nbytes).reshape(total, k, nbytes)
+    digests = {}
+    for s in range(lo, hi):
+        rc, rec = oracle.encode(k, m, data[s], nbytes)
+        assert rc == 0
+        digests[s] = lhutil.h64(rec)
+    elapsed = 0.5 + rank  # deterministic stand-in for a rank's timed region
+    slowest = max_over_ranks(elapsed)
+    rate = aggregate_rate((hi - lo) * k * nbytes, elapsed)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, digests)
+    dist.destroy_process_group()
+    q.put((rank, slowest, rate, gathered))
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_sharded_encode_matches_single_process(world):
+    total = 37
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    oracle = lhutil.Oracle()
+    k, m, nbytes = 29, 4, 48
+    data = lhutil.fill(11, total * k * nbytes).reshape(total, k, nbytes)
+    expect = {s: lhutil.h64(oracle.encode(k, m, data[s], nbytes)[1]) for s in range(total)}
+    for rank, slowest, rate, gathered in results:
+        assert slowest == 0.5 + (world - 1)
+        assert abs(rate - total * k * nbytes / slowest) < 1e-6
+        merged = {}
+        for d in gathered:
+            assert not (set(d) & set(merged))   # shards are disjoint
+            merged.update(d)
+        assert merged == expect
