@@ -25,9 +25,10 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 CONFIGS = {
-    # name: (k, m, bytes, stripes per GPU)
-    "k29m4": (29, 4, 1296, 65536),      # BASELINE configs[1] / [3] (per GPU)
-    "k128m32": (128, 32, 8192, 8192),   # BASELINE configs[2]
+    # name: (k, m, bytes, stripes per GPU, erasures per stripe)
+    "k29m4": (29, 4, 1296, 65536, "max"),        # BASELINE configs[1] / [3] (per GPU)
+    "k128m32": (128, 32, 8192, 8192, "max"),     # BASELINE configs[2]
+    "k200m56": (200, 56, 65536, 64, "random"),   # BASELINE configs[4] (device-resident part)
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -68,25 +69,48 @@ def max_over_ranks(world, value):
     return value if world == 1 else mx(value, device="cuda")
 
 
-def make_workload(k, m, nbytes, stripes, seed):
-    """Data X [S, k, bytes]; decode buffer D whose slots 0..k-e-1 hold the surviving
-    originals (random per stripe, shuffled) and slots k-e..k-1 receive recovery rows
-    0..e-1 from the encode; rows0 = the matching Block.row bytes."""
+def make_workload(k, m, nbytes, stripes, seed, erasures="max"):
+    """Data X [S, k, bytes] and a decode buffer D [S, k, bytes] whose first slots hold the
+    surviving originals of each stripe in a shuffled order and whose last e_s slots
+    receive recovery blocks; rows0 = the matching Block.row bytes.
+
+    erasures="max": e = m erased originals per stripe (m <= k), recovery rows 0..m-1 --
+    the encode then writes straight into D's recovery slots (rec_index is None).
+    erasures="random": e_s uniform in [1, min(k, m)] per stripe, a random subset of the
+    recovery rows; rec_index = (dst, src) row indices that copy the needed recovery
+    blocks from the encode output R [S, m, bytes] into D each step."""
     import torch
-    e = min(k, m)
-    assert e == m, "bench writes all m recovery rows into the decode buffer"
     g = torch.Generator(device="cuda").manual_seed(seed)
     X = torch.randint(0, 256, (stripes, k, nbytes), dtype=torch.uint8, device="cuda", generator=g)
-    keys = torch.rand(stripes, k, device="cuda", generator=g)
-    perm = torch.argsort(keys, dim=1)
-    keep = perm[:, : k - e]                     # surviving originals, shuffled order
+    perm = torch.argsort(torch.rand(stripes, k, device="cuda", generator=g), dim=1)
     D = torch.empty_like(X)
-    D[:, : k - e] = torch.gather(X, 1, keep.unsqueeze(-1).expand(-1, -1, nbytes))
-    rows0 = torch.cat([keep, torch.arange(k, k + e, device="cuda").expand(stripes, e)], dim=1).to(torch.uint8)
-    return X, D, rows0.contiguous()
+    if erasures == "max":
+        e = min(k, m)
+        assert e == m, "erasures='max' writes all m recovery rows into the decode buffer"
+        keep = perm[:, : k - e]
+        D[:, : k - e] = torch.gather(X, 1, keep.unsqueeze(-1).expand(-1, -1, nbytes))
+        rows0 = torch.cat([keep, torch.arange(k, k + e, device="cuda").expand(stripes, e)], dim=1)
+        return X, D, rows0.to(torch.uint8).contiguous(), None
+    rng = torch.Generator().manual_seed(seed)
+    rows0 = torch.empty((stripes, k), dtype=torch.long)
+    dst, src = [], []
+    perm_c = perm.cpu()
+    for s in range(stripes):
+        e = int(torch.randint(1, min(k, m) + 1, (1,), generator=rng))
+        rec_rows = torch.randperm(m, generator=rng)[:e]
+        rows0[s, : k - e] = perm_c[s, : k - e]
+        rows0[s, k - e:] = k + rec_rows
+        for j in range(e):
+            dst.append(s * k + k - e + j)
+            src.append(s * m + int(rec_rows[j]))
+    rows0 = rows0.cuda()
+    keep_all = torch.where(rows0 < k, rows0, torch.zeros_like(rows0))
+    D.copy_(torch.gather(X, 1, keep_all.unsqueeze(-1).expand(-1, -1, nbytes)))
+    idx = (torch.tensor(dst, device="cuda"), torch.tensor(src, device="cuda"))
+    return X, D, rows0.to(torch.uint8).contiguous(), idx
 
 
-def cpu_baseline(k, m, nbytes, target_seconds):
+def cpu_baseline(k, m, nbytes, target_seconds, stripes=4096):
     """Reference codec (oracle/_ref, compiled from the reference sources) -- or, if that
     build is absent, the oracle restatement -- on the host cores, same step definition,
     a bounded sample of stripes."""
@@ -104,7 +128,6 @@ def cpu_baseline(k, m, nbytes, target_seconds):
         lib, kind = lhutil.Oracle(), "port"
         enc, dec = lib.lib.lho_encode, lib.lib.lho_decode
     e = min(k, m)
-    stripes = 4096
     data = lhutil.fill(99, stripes * k * nbytes)
     rng = np.random.Generator(np.random.PCG64(5))
     erased = np.stack([rng.choice(k, size=e, replace=False) for _ in range(stripes)]).astype(np.uint8)
@@ -131,14 +154,19 @@ def main():
     world, rank, local = setup_dist()
     import longhair_amd as lh
 
-    k, m, nbytes, stripes = CONFIGS[args.config]
+    k, m, nbytes, stripes, erasures = CONFIGS[args.config]
     if args.stripes:
         stripes = args.stripes
     assert lh.cauchy_256_init() == 0, lh.lib().cauchy_256_last_error()
     lh.prepare(k, m, nbytes, stripes)
-    X, D, rows0 = make_workload(k, m, nbytes, stripes, seed=1234 + rank)
-    e = min(k, m)
-    rec_view = D[:, k - e:]
+    X, D, rows0, rec_index = make_workload(k, m, nbytes, stripes, seed=1234 + rank, erasures=erasures)
+    e_mean = float((rows0 >= k).sum()) / stripes
+    if rec_index is None:
+        rec_view = D[:, k - m:]     # the encode writes straight into D's recovery slots
+    else:
+        R = torch.empty((stripes, m, nbytes), dtype=torch.uint8, device="cuda")
+        rec_view = R
+        Dflat, Rflat = D.view(-1, nbytes), R.view(-1, nbytes)
     rows = rows0.clone()
     stream = torch.cuda.current_stream()
 
@@ -148,6 +176,8 @@ def main():
         lh.encode_batch(X, m, recovery=rec_view)
         if ev is not None:
             ev[1].record(stream)
+        if rec_index is not None:   # deliver the received recovery blocks to their slots
+            Dflat.index_copy_(0, rec_index[0], Rflat.index_select(0, rec_index[1]))
         rows.copy_(rows0)
         if ev is not None:
             ev[2].record(stream)
@@ -179,7 +209,7 @@ def main():
     in_bytes = 2.0 * k * nbytes * stripes * world
     value = in_bytes * args.steps / elapsed / 1e9
     enc_alg = float(k + m) * nbytes * stripes           # read k, write m blocks per stripe
-    dec_alg = float(k + e) * nbytes * stripes           # read k slots, write e blocks
+    dec_alg = (k + e_mean) * nbytes * stripes           # read k slots, write e blocks
     enc_k, dec_k = lh.kernel_names(k, m, nbytes)
     roof = {
         "encode": {"kernel": "+".join(enc_k), "ms": round(enc_ms, 4),
@@ -207,7 +237,8 @@ def main():
         "dtype": "u8",
         "data": "synthetic",
         "config": {"workload": f"k={k} m={m} bytes={nbytes}, {stripes} stripes per GPU, encode + "
-                               f"decode with {e} random erasures per stripe",
+                               f"decode with {'e=' + str(min(k, m)) if erasures == 'max' else 'random e in [1,' + str(min(k, m)) + ']'}"
+                               f" erased originals per stripe (mean {e_mean:.1f})",
                    "k": k, "m": m, "block_bytes": nbytes, "stripes_per_gpu": stripes,
                    "parallelism": f"stripes sharded over {world} rank(s), no collective"},
         "encode_GBps": round(k * nbytes * stripes / (enc_ms * 1e-3) / 1e9, 1),
@@ -218,7 +249,8 @@ def main():
         "kernels": roof,
     }
     if rank == 0 and world == 1 and args.cpu_baseline != "off":
-        out["cpu_baseline"] = cpu_baseline(k, m, nbytes, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(k, m, nbytes, args.cpu_seconds,
+                                           stripes=max(2, min(4096, (256 << 20) // (k * nbytes))))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

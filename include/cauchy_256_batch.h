@@ -39,6 +39,18 @@ int cauchy_256_decode_batch(int k, int m, int block_bytes, int stripes,
                             void *d_blocks, long long stripe_stride,
                             unsigned char *d_rows, signed char *d_status, void *stream);
 
+/* Host-memory batches: the same operations on stripes that live
+ * in host memory, pipelined in chunks of `chunk_stripes` (0 = about 64 MiB) over three
+ * streams so the PCIe copies overlap the kernels.  Host buffers should be pinned
+ * (hipHostMalloc / hipHostRegister).  Synchronous: returns when the results are in
+ * host memory.  Decode copies back only the slots that change and the rows. */
+int cauchy_256_encode_host_batch(int k, int m, int block_bytes, int stripes,
+                                 const void *h_data, long long data_stride,
+                                 void *h_recovery, long long recovery_stride, int chunk_stripes);
+int cauchy_256_decode_host_batch(int k, int m, int block_bytes, int stripes,
+                                 void *h_blocks, long long stripe_stride,
+                                 unsigned char *h_rows, signed char *h_status, int chunk_stripes);
+
 /* Optional: compile the specialised kernels and reserve workspace for up to
  * `max_stripes` stripes of this shape ahead of time (e.g. before hipGraph capture or
  * a timed region).  Synchronous.  Returns 0 or an error code. */
@@ -46,8 +58,15 @@ int cauchy_256_batch_prepare(int k, int m, int block_bytes, int max_stripes);
 
 /* Which kernel family serves this shape: 0 = generic coefficient-driven kernels,
  * 1 = run-time specialised (JIT) network, 2 (decode only) = specialised network with the
- * erasure plan computed inside the same kernel.  `what` = 0 for encode, 1 for decode. */
+ * erasure plan computed inside the same kernel, 3 (encode only) = run-time specialised
+ * 4-bit-windowed network for large m, 4 (decode only) = windowed phase A + per-stripe
+ * inverse kernel for large m.  `what` = 0 for encode, 1 for decode. */
 int cauchy_256_batch_path(int k, int m, int block_bytes, int what);
+
+/* Compile the specialised kernels of a shape into the on-disk code-object cache
+ * ($LONGHAIR_AMD_CACHE_DIR, else jit_cache/ beside the library).  Needs no GPU.
+ * Returns 0 or -3. */
+int cauchy_256_jit_precompile(int k, int m, int block_bytes);
 
 /* Last error message of the calling thread (empty string if none). */
 const char *cauchy_256_last_error(void);

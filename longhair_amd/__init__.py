@@ -119,6 +119,36 @@ def decode_batch(blocks, rows, m, status=None, stream=None):
     return status
 
 
+def encode_host_batch(data, m, recovery=None, chunk_stripes=0):
+    """Encode stripes held in host memory (numpy uint8 [stripes, k, bytes], ideally pinned
+    via a pinned torch CPU tensor's .numpy()); pipelined H2D / kernel / D2H."""
+    import numpy as np
+    assert data.dtype == np.uint8 and data.ndim == 3 and data.flags.c_contiguous
+    stripes, k, nbytes = data.shape
+    if recovery is None:
+        recovery = np.empty((stripes, m, nbytes), dtype=np.uint8)
+    rc = lib().cauchy_256_encode_host_batch(k, m, nbytes, stripes, data.ctypes.data, data.strides[0],
+                                            recovery.ctypes.data, recovery.strides[0], chunk_stripes)
+    if rc != 0:
+        raise LonghairError(rc, "cauchy_256_encode_host_batch")
+    return recovery
+
+
+def decode_host_batch(blocks, rows, m, chunk_stripes=0):
+    """Decode stripes held in host memory in place (numpy uint8 [stripes, k, bytes] and
+    rows [stripes, k]); returns the int8 status per stripe."""
+    import numpy as np
+    assert blocks.dtype == np.uint8 and blocks.ndim == 3 and blocks.flags.c_contiguous
+    stripes, k, nbytes = blocks.shape
+    assert rows.dtype == np.uint8 and rows.shape == (stripes, k) and rows.flags.c_contiguous
+    status = np.zeros(stripes, dtype=np.int8)
+    rc = lib().cauchy_256_decode_host_batch(k, m, nbytes, stripes, blocks.ctypes.data, blocks.strides[0],
+                                            rows.ctypes.data, status.ctypes.data, chunk_stripes)
+    if rc != 0:
+        raise LonghairError(rc, "cauchy_256_decode_host_batch")
+    return status
+
+
 def prepare(k, m, block_bytes, max_stripes=0):
     """Compile the specialised kernels / reserve workspace for a shape (synchronous)."""
     rc = lib().cauchy_256_batch_prepare(k, m, block_bytes, max_stripes)
@@ -130,15 +160,17 @@ def batch_path(k, m, block_bytes, decode=False):
     """'jit' when a run-time specialised network serves the shape ('jit-fused' for a
     decode whose plan is computed in the same kernel), else 'generic'."""
     code = lib().cauchy_256_batch_path(k, m, block_bytes, 1 if decode else 0)
-    return {0: "generic", 1: "jit", 2: "jit-fused"}[code]
+    return {0: "generic", 1: "jit", 2: "jit-fused", 3: "jit-win", 4: "jit-wide"}[code]
 
 
 def kernel_names(k, m, block_bytes):
     """Names of the kernels one encode_batch / decode_batch launches for this shape."""
-    enc = {"generic": ["lh_apply_generic_kernel"], "jit": ["lh_jit_encode"]}[batch_path(k, m, block_bytes)]
+    enc = {"generic": ["lh_apply_generic_kernel"], "jit": ["lh_jit_encode"],
+           "jit-win": ["lh_jit_encode_win"]}[batch_path(k, m, block_bytes)]
     dec = {"generic": ["lh_plan_kernel", "lh_apply_generic_kernel", "lh_scatter_kernel"],
            "jit": ["lh_plan_small_kernel" if min(k, m) <= 8 else "lh_plan_kernel", "lh_jit_decode"],
-           "jit-fused": ["lh_jit_decode_fused"]}[batch_path(k, m, block_bytes, True)]
+           "jit-fused": ["lh_jit_decode_fused"],
+           "jit-wide": ["lh_plan_kernel", "lh_jit_elim_win", "lh_apply_wide_kernel"]}[batch_path(k, m, block_bytes, True)]
     if m == 1 or k == 1:
         enc, dec = ["lh_xor_reduce_kernel"], ["lh_plan_kernel", "lh_xor_reduce_kernel"]
     return enc, dec

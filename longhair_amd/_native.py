@@ -23,8 +23,15 @@ EXPORTS = {
     "cauchy_256_decode_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
                                                ctypes.c_void_p, ctypes.c_void_p]),
+    "cauchy_256_encode_host_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                    ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
+                                                    ctypes.c_longlong, ctypes.c_int]),
+    "cauchy_256_decode_host_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                    ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
+                                                    ctypes.c_void_p, ctypes.c_int]),
     "cauchy_256_batch_prepare": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "cauchy_256_batch_path": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "cauchy_256_jit_precompile": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "cauchy_256_last_error": (ctypes.c_char_p, []),
 }
 

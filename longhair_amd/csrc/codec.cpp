@@ -73,7 +73,7 @@ struct HostPinned {
 
 // Per-stream scratch (decode plans and the generic path's output workspace).
 struct Workspace {
-    DevBuf plan, work;
+    DevBuf plan, work, wide;
 };
 
 // Per-device state.
@@ -91,6 +91,10 @@ struct Device {
     hipStream_t stream = nullptr;
     DevBuf stage, stage_rows, stage_status;
     HostPinned host_stage;
+    // host-batch pipeline: per ring slot a stream, device buffers and an event
+    std::mutex pipe_mu;
+    hipStream_t pipe_stream[3] = {nullptr, nullptr, nullptr};
+    DevBuf pipe_blocks[3], pipe_out[3], pipe_rows[3], pipe_status[3];
 };
 
 static std::mutex g_devices_mu;
@@ -221,6 +225,21 @@ static int encode_batch(int k, int m, int bytes, int stripes, const uint8_t *d_d
         }
         if (allow_compile) return fail(kHipError, err);
     }
+    if (jit_win_config_for(k, m, bytes, &cfg)) {
+        std::string err;
+        const JitKernels *jk = allow_compile ? d->jit.get(cfg, &err) : d->jit.peek(cfg);
+        if (jk && jk->encode_win) {
+            const long long blocks = (long long)stripes * (cfg.sub / (64 * cfg.W));
+            if (blocks > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
+            const unsigned threads = 64u * (unsigned)((m + cfg.rows_per_wave - 1) / cfg.rows_per_wave);
+            long long in_stride = data_stride, out_stride = rec_stride;
+            int n = stripes;
+            void *args[] = {(void *)&d_data, &in_stride, (void *)&d_rec, &out_stride, &n};
+            LH_HIP(hipModuleLaunchKernel(jk->encode_win, (unsigned)blocks, 1, 1, threads, 1, 1, 0, st, args, nullptr));
+            return kOk;
+        }
+        if (allow_compile && !jk) return fail(kHipError, err);
+    }
     const uint8_t *G = nullptr;
     if (int rc = device_generator(d, k, m, &G)) return rc;
     ApplyArgs a{};
@@ -278,7 +297,15 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         LH_HIP(hipModuleLaunchKernel(jk->decode_fused, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr));
         return kOk;
     }
-    const size_t work_bytes = generic ? (size_t)stripes * e_max * bytes : 0;
+    // Large m: windowed phase A into a V workspace, then the wide phase B (sub % 256 == 0).
+    JitConfig wcfg;
+    const JitKernels *wk = nullptr;
+    if (generic && e_max <= 64 && jit_win_config_for(k, m, bytes, &wcfg, true)) {
+        wk = allow_compile ? d->jit.get(wcfg, &err) : d->jit.peek(wcfg);
+        if (!wk && allow_compile) return fail(kHipError, err);
+        if (wk && !wk->elim_win) wk = nullptr;
+    }
+    const size_t work_bytes = (generic && !wk) ? (size_t)stripes * e_max * bytes : 0;
     Workspace *w = nullptr;
     if (int rc = workspace(d, st, (size_t)stripes * plan_stride, work_bytes, &w)) return rc;
     const uint8_t *G = nullptr;
@@ -296,7 +323,7 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
     pa.m = m;
     pa.e_max = e_max;
     pa.stripes = stripes;
-    pa.want_w = generic ? 1 : 0;
+    pa.want_w = (generic && !wk) ? 1 : 0;
     LH_HIP(launch_plan(pa, st));
     if (k <= 1) return kOk;
 
@@ -328,6 +355,38 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         int n = stripes;
         void *args[] = {(void *)&d_blocks, &s1, (void *)&plan, &s2, (void *)&zero, &n};
         LH_HIP(hipModuleLaunchKernel(jk->decode, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr));
+        return kOk;
+    }
+    if (wk) {
+        const uint8_t *zero = nullptr;
+        if (int rc = zero_page(d, (size_t)bytes, &zero)) return rc;
+        const long long ws_stride = (long long)m * bytes;
+        {
+            std::lock_guard<std::mutex> g(d->mu);
+            LH_HIP(w->wide.reserve((size_t)stripes * ws_stride));
+        }
+        const long long blocks = (long long)stripes * (wcfg.sub / (64 * wcfg.W));
+        const unsigned threads = 64u * (unsigned)((m + wcfg.rows_per_wave - 1) / wcfg.rows_per_wave);
+        long long s1 = stride, s2 = plan_stride, s3 = ws_stride;
+        const uint8_t *plan = w->plan.ptr;
+        uint8_t *ws = w->wide.ptr;
+        int n = stripes;
+        void *args[] = {(void *)&d_blocks, &s1, (void *)&plan, &s2, (void *)&zero, (void *)&ws, &s3, &n};
+        LH_HIP(hipModuleLaunchKernel(wk->elim_win, (unsigned)blocks, 1, 1, threads, 1, 1, 0, st, args, nullptr));
+        WideArgs wa{};
+        wa.ws = w->wide.ptr;
+        wa.ws_stride = ws_stride;
+        wa.blocks = d_blocks;
+        wa.blocks_stride = stride;
+        wa.plan = w->plan.ptr;
+        wa.plan_stride = plan_stride;
+        wa.k = k;
+        wa.m = m;
+        wa.e_max = e_max;
+        wa.bytes = bytes;
+        wa.sub = bytes / 8;
+        wa.stripes = stripes;
+        LH_HIP(launch_apply_wide(wa, st));
         return kOk;
     }
     // Generic: recovered originals into the workspace, then into their slots.
@@ -372,6 +431,107 @@ static bool is_device_pointer(const void *p) {
         return false;
     }
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+// ----------------------------------------------------------- host-batch pipeline
+// Stripes that start and end in host memory (packet buffers, files): chunks of stripes
+// rotate over three streams, so chunk c + 1's host-to-device copy overlaps chunk c's
+// kernels and chunk c - 1's device-to-host copy.  Host buffers should be pinned
+// (hipHostMalloc / hipHostRegister) for the copies to be asynchronous.
+static int pipe_streams(Device *d) {
+    for (auto &s : d->pipe_stream)
+        if (!s) LH_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    return kOk;
+}
+
+static int auto_chunk(long long stripe_bytes, int stripes, int chunk) {
+    if (chunk > 0) return chunk < stripes ? chunk : stripes;
+    long long c = (64ll << 20) / (stripe_bytes > 0 ? stripe_bytes : 1);  // ~64 MiB per chunk
+    if (c < 1) c = 1;
+    return (int)(c < stripes ? c : stripes);
+}
+
+static int host_encode_batch(int k, int m, int bytes, int stripes, const uint8_t *h_data, long long data_stride,
+                             uint8_t *h_rec, long long rec_stride, int chunk) {
+    if (k < 1 || m < 1 || bytes <= 0 || stripes < 0) return fail(kInvalid, "invalid k, m, block_bytes or stripes");
+    if (data_stride < (long long)k * bytes || rec_stride < (long long)m * bytes)
+        return fail(kInvalid, "stripe strides smaller than the stripe");
+    if (stripes == 0) return kOk;
+    Device *d = nullptr;
+    if (int rc = current_device(&d)) return rc;
+    std::lock_guard<std::mutex> g(d->pipe_mu);
+    if (int rc = pipe_streams(d)) return rc;
+    const long long in_sz = (long long)k * bytes, out_sz = (long long)m * bytes;
+    chunk = auto_chunk(in_sz + out_sz, stripes, chunk);
+    for (int i = 0; i < 3; ++i) {
+        LH_HIP(d->pipe_blocks[i].reserve((size_t)chunk * in_sz));
+        LH_HIP(d->pipe_out[i].reserve((size_t)chunk * out_sz));
+    }
+    int rc_all = kOk;
+    for (int s0 = 0, c = 0; s0 < stripes; s0 += chunk, ++c) {
+        const int n = stripes - s0 < chunk ? stripes - s0 : chunk;
+        const int i = c % 3;
+        hipStream_t st = d->pipe_stream[i];
+        LH_HIP(hipMemcpy2DAsync(d->pipe_blocks[i].ptr, in_sz, h_data + (long long)s0 * data_stride, data_stride, in_sz,
+                                n, hipMemcpyHostToDevice, st));
+        const int rc = encode_batch(k, m, bytes, n, d->pipe_blocks[i].ptr, in_sz, d->pipe_out[i].ptr, out_sz, st, true);
+        if (rc != kOk && rc != kInvalid) return rc;
+        if (rc == kInvalid) rc_all = kInvalid;
+        const long long copy = rc == kOk ? out_sz : (long long)bytes;  // only block 0 on invalid params
+        LH_HIP(hipMemcpy2DAsync(h_rec + (long long)s0 * rec_stride, rec_stride, d->pipe_out[i].ptr, out_sz, copy, n,
+                                hipMemcpyDeviceToHost, st));
+    }
+    for (auto s : d->pipe_stream) LH_HIP(hipStreamSynchronize(s));
+    return rc_all == kOk ? kOk : fail(kInvalid, "k + m > 256 or block_bytes % 8 != 0");
+}
+
+static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_blocks, long long stride,
+                             uint8_t *h_rows, int8_t *h_status, int chunk) {
+    if (k < 1 || m < 1 || bytes <= 0 || stripes < 0) return fail(kInvalid, "invalid k, m, block_bytes or stripes");
+    if (stride < (long long)k * bytes) return fail(kInvalid, "stripe stride smaller than the stripe");
+    if (stripes == 0) return kOk;
+    Device *d = nullptr;
+    if (int rc = current_device(&d)) return rc;
+    std::lock_guard<std::mutex> g(d->pipe_mu);
+    if (int rc = pipe_streams(d)) return rc;
+    const long long sz = (long long)k * bytes;
+    chunk = auto_chunk(sz, stripes, chunk);
+    for (int i = 0; i < 3; ++i) {
+        LH_HIP(d->pipe_blocks[i].reserve((size_t)chunk * sz));
+        LH_HIP(d->pipe_rows[i].reserve((size_t)chunk * k));
+        LH_HIP(d->pipe_status[i].reserve((size_t)chunk));
+    }
+    // Only the recovery slots (and, for m == 1, the slot the XOR lands in) change: copy
+    // those back, not the whole stripe.  Slots are read from the caller's rows first.
+    std::vector<std::vector<int>> changed((size_t)stripes);
+    for (int s = 0; s < stripes; ++s) {
+        const uint8_t *r = h_rows + (long long)s * k;
+        int out = 0, any = 0;
+        for (int i = 0; i < k; ++i)
+            if (r[i] >= k) { changed[s].push_back(i); out = i; any = 1; }
+        if (m == 1 && k > 1) { changed[s].clear(); changed[s].push_back(any ? out : 0); }
+        if (k <= 1) changed[s].clear();
+    }
+    for (int s0 = 0, c = 0; s0 < stripes; s0 += chunk, ++c) {
+        const int n = stripes - s0 < chunk ? stripes - s0 : chunk;
+        const int i = c % 3;
+        hipStream_t st = d->pipe_stream[i];
+        LH_HIP(hipMemcpy2DAsync(d->pipe_blocks[i].ptr, sz, h_blocks + (long long)s0 * stride, stride, sz, n,
+                                hipMemcpyHostToDevice, st));
+        LH_HIP(hipMemcpyAsync(d->pipe_rows[i].ptr, h_rows + (long long)s0 * k, (size_t)n * k, hipMemcpyHostToDevice, st));
+        const int rc = decode_batch(k, m, bytes, n, d->pipe_blocks[i].ptr, sz, d->pipe_rows[i].ptr,
+                                    (int8_t *)d->pipe_status[i].ptr, st, true);
+        if (rc != kOk) return rc;
+        for (int s = s0; s < s0 + n; ++s)
+            for (int slot : changed[s])
+                LH_HIP(hipMemcpyAsync(h_blocks + (long long)s * stride + (long long)slot * bytes,
+                                      d->pipe_blocks[i].ptr + (long long)(s - s0) * sz + (long long)slot * bytes, bytes,
+                                      hipMemcpyDeviceToHost, st));
+        LH_HIP(hipMemcpyAsync(h_rows + (long long)s0 * k, d->pipe_rows[i].ptr, (size_t)n * k, hipMemcpyDeviceToHost, st));
+        if (h_status) LH_HIP(hipMemcpyAsync(h_status + s0, d->pipe_status[i].ptr, n, hipMemcpyDeviceToHost, st));
+    }
+    for (auto s : d->pipe_stream) LH_HIP(hipStreamSynchronize(s));
+    return kOk;
 }
 
 static int dropin_encode(int k, int m, const unsigned char *data_ptrs[], void *recovery, int bytes) {
@@ -513,6 +673,20 @@ LH_API int cauchy_256_decode_batch(int k, int m, int block_bytes, int stripes, v
                             (int8_t *)d_status, (hipStream_t)stream, true);
 }
 
+LH_API int cauchy_256_encode_host_batch(int k, int m, int block_bytes, int stripes, const void *h_data,
+                                        long long data_stride, void *h_recovery, long long recovery_stride,
+                                        int chunk_stripes) {
+    return lh::host_encode_batch(k, m, block_bytes, stripes, (const uint8_t *)h_data, data_stride,
+                                 (uint8_t *)h_recovery, recovery_stride, chunk_stripes);
+}
+
+LH_API int cauchy_256_decode_host_batch(int k, int m, int block_bytes, int stripes, void *h_blocks,
+                                        long long stripe_stride, unsigned char *h_rows, signed char *h_status,
+                                        int chunk_stripes) {
+    return lh::host_decode_batch(k, m, block_bytes, stripes, (uint8_t *)h_blocks, stripe_stride, h_rows,
+                                 (int8_t *)h_status, chunk_stripes);
+}
+
 LH_API int cauchy_256_batch_prepare(int k, int m, int block_bytes, int max_stripes) {
     lh::Device *d = nullptr;
     if (int rc = lh::current_device(&d)) return rc;
@@ -520,6 +694,15 @@ LH_API int cauchy_256_batch_prepare(int k, int m, int block_bytes, int max_strip
     for (int dec = 0; dec < 2; ++dec) {
         lh::JitConfig cfg;
         if (lh::jit_config_for(k, m, block_bytes, dec == 1, &cfg) && !d->jit.get(cfg, &err))
+            return lh::fail(lh::kHipError, err);
+    }
+    {
+        lh::JitConfig cfg;
+        if (!lh::jit_config_for(k, m, block_bytes, false, &cfg) && lh::jit_win_config_for(k, m, block_bytes, &cfg) &&
+            !d->jit.get(cfg, &err))
+            return lh::fail(lh::kHipError, err);
+        if (!lh::jit_config_for(k, m, block_bytes, true, &cfg) && lh::jit_win_config_for(k, m, block_bytes, &cfg, true) &&
+            !d->jit.get(cfg, &err))
             return lh::fail(lh::kHipError, err);
     }
     if (max_stripes > 0 && k > 1 && m > 1) {
@@ -538,9 +721,31 @@ LH_API int cauchy_256_batch_prepare(int k, int m, int block_bytes, int max_strip
     return 0;
 }
 
+// Compile the specialised code objects of a shape into the on-disk cache without a GPU
+// (build-time warm-up for shapes whose compilation takes long).  0 ok, -3 on failure.
+LH_API int cauchy_256_jit_precompile(int k, int m, int block_bytes) {
+    std::string err;
+    std::vector<char> code;
+    lh::JitConfig cfg;
+    for (int dec = 0; dec < 2; ++dec)
+        if (lh::jit_config_for(k, m, block_bytes, dec == 1, &cfg) && !lh::compile_code_object(cfg, &code, &err))
+            return lh::fail(lh::kHipError, err);
+    if (!lh::jit_config_for(k, m, block_bytes, false, &cfg) && lh::jit_win_config_for(k, m, block_bytes, &cfg) &&
+        !lh::compile_code_object(cfg, &code, &err))
+        return lh::fail(lh::kHipError, err);
+    if (!lh::jit_config_for(k, m, block_bytes, true, &cfg) && lh::jit_win_config_for(k, m, block_bytes, &cfg, true) &&
+        !lh::compile_code_object(cfg, &code, &err))
+        return lh::fail(lh::kHipError, err);
+    return 0;
+}
+
 LH_API int cauchy_256_batch_path(int k, int m, int block_bytes, int what) {
     lh::JitConfig cfg;
-    if (!lh::jit_config_for(k, m, block_bytes, what == 1, &cfg)) return 0;
+    if (!lh::jit_config_for(k, m, block_bytes, what == 1, &cfg)) {
+        if (what == 0) return lh::jit_win_config_for(k, m, block_bytes, &cfg) ? 3 : 0;
+        const int e_max = k < m ? k : m;
+        return (e_max <= 64 && lh::jit_win_config_for(k, m, block_bytes, &cfg, true)) ? 4 : 0;
+    }
     // Decode: 2 when the plan is computed inside the specialised kernel (jit_codec.hip,
     // LH_FUSED: e_max <= 4, one stripe per <= 64 lanes, k <= 64).
     const int e_max = k < m ? k : m;

@@ -2,7 +2,11 @@
 #include "jit.hpp"
 
 #include <hip/hiprtc.h>
+#include <dlfcn.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <sstream>
@@ -81,8 +85,196 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     return true;
 }
 
+bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
+    if (const char *env = std::getenv("LONGHAIR_AMD_PATH")) {
+        if (std::string(env) == "generic") return false;
+    }
+    if (k < 2 || m < 2 || k + m > 256 || bytes % 8 != 0 || bytes <= 0) return false;
+    const int sub = bytes / 8, W = 4;
+    if (sub % (64 * W) != 0) return false;
+    cfg->k = k;
+    cfg->m = m;
+    cfg->bytes = bytes;
+    cfg->sub = sub;
+    cfg->W = W;
+    cfg->nch = sub / W;
+    cfg->spw = 0;
+    cfg->wps = (cfg->nch + 63) / 64;
+    cfg->win = decode ? 2 : 1;
+    cfg->rows_per_wave = 8;
+    if (const char *r = std::getenv("LONGHAIR_AMD_WIN_ROWS")) cfg->rows_per_wave = std::atoi(r);
+    if ((m + cfg->rows_per_wave - 1) / cfg->rows_per_wave > 16) return false;  // <= 1024 threads
+    cfg->defines.clear();
+    if (const char *d = std::getenv("LONGHAIR_AMD_JIT_DEFINES")) cfg->defines = d;
+    return true;
+}
+
+// Straight-line source of the 4-bit-windowed network for row group `g` (win modules):
+// per data column, the nibble-table entries the group's rows need are built once from
+// their lowest-bit predecessor, then every output sub-row XORs at most two entries.
+static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vector<uint8_t> &G, int g) {
+    const int R = c.rows_per_wave, k = c.k, m = c.m, PF = 3;
+    const int r0 = g * R, r1 = std::min(m, r0 + R);
+    const bool elim = c.win == 2;  // decode phase A: slot-mapped columns + recovery rows
+    auto col = [&](int x) {
+        std::ostringstream e;
+        if (elim) e << "lh_col(pl, " << x << ", base, zero)";
+        else e << "(base + " << (long long)x * c.bytes << "LL)";
+        return e.str();
+    };
+    os << "__device__ __forceinline__ void lh_wg" << g << "(const unsigned char *__restrict__ base, "
+       << (elim ? "const unsigned char *__restrict__ zero, const unsigned char *__restrict__ pl, " : "")
+       << "unsigned char *__restrict__ o) {\n";
+    for (int r = r0; r < r1; ++r)
+        for (int y = 0; y < 8; ++y) os << "  unsigned int a" << (r - r0) << "_" << y << " = 0;\n";
+    for (int q = 0; q < PF && q < k; ++q) {
+        os << "  const unsigned char *c" << q << " = " << col(q) << ";\n";
+        for (int b = 0; b < 8; ++b)
+            os << "  unsigned int d" << q << "_" << b << " = lh_ld(c" << q << " + " << b * c.sub << ");\n";
+    }
+    for (int x = 0; x < k; ++x) {
+        const int slot = x % PF;
+        os << "  {\n";
+        if (x + PF < k) {
+            os << "    const unsigned char *cn = " << col(x + PF) << ";\n";
+            for (int b = 0; b < 8; ++b)
+                os << "    const unsigned int n" << b << " = lh_ld(cn + " << b * c.sub << ");\n";
+        }
+        // Which nibble-table entries (lo: sub-blocks 0..3, hi: 4..7) this group needs.
+        bool need[2][16] = {};
+        for (int r = r0; r < r1; ++r) {
+            const uint64_t bm = bitmatrix(G[(size_t)r * k + x]);
+            for (int y = 0; y < 8; ++y) {
+                const int s = (int)((bm >> (8 * y)) & 0xFF);
+                need[0][s & 15] = need[1][s >> 4] = true;
+            }
+        }
+        for (int h = 0; h < 2; ++h) {
+            // close under "drop the lowest bit" so every entry has its predecessor
+            for (int n = 15; n >= 1; --n)
+                if (need[h][n]) need[h][n & (n - 1)] = true;
+            for (int n = 1; n < 16; ++n) {
+                if (!need[h][n]) continue;
+                const int low = __builtin_ctz(n), pre = n & (n - 1);
+                os << "    const unsigned int t" << h << "_" << n << " = ";
+                if (pre) os << "t" << h << "_" << pre << " ^ ";
+                os << "d" << slot << "_" << (4 * h + low) << ";\n";
+            }
+        }
+        for (int r = r0; r < r1; ++r) {
+            const uint64_t bm = bitmatrix(G[(size_t)r * k + x]);
+            for (int y = 0; y < 8; ++y) {
+                const int s = (int)((bm >> (8 * y)) & 0xFF), lo = s & 15, hi = s >> 4;
+                if (!lo && !hi) continue;
+                os << "    a" << (r - r0) << "_" << y << " ^= ";
+                if (lo) os << "t0_" << lo << (hi ? " ^ " : "");
+                if (hi) os << "t1_" << hi;
+                os << ";\n";
+            }
+        }
+        os << "    LH_PIN" << (r1 - r0) << ";\n";
+        if (x + PF < k)
+            for (int b = 0; b < 8; ++b) os << "    d" << slot << "_" << b << " = n" << b << ";\n";
+        os << "  }\n";
+    }
+    if (elim)  // V_r = R_r + sum_x ...: XOR the recovery row r (zero page if absent)
+        for (int r = r0; r < r1; ++r) {
+            os << "  {\n    const unsigned char *rp = lh_rec(pl, " << r << ", base, zero);\n";
+            for (int y = 0; y < 8; ++y)
+                os << "    a" << (r - r0) << "_" << y << " ^= lh_ld(rp + " << y * c.sub << ");\n";
+            os << "  }\n";
+        }
+    for (int r = r0; r < r1; ++r)
+        for (int y = 0; y < 8; ++y)
+            os << "  lh_st(o + " << (long long)r * c.bytes + y * c.sub << "LL, a" << (r - r0) << "_" << y << ");\n";
+    os << "}\n";
+}
+
+static std::string win_source_for(const JitConfig &c) {
+    std::ostringstream os;
+    const std::vector<uint8_t> G = generator_matrix(c.k, c.m);
+    const int R = c.rows_per_wave, NG = (c.m + R - 1) / R, CPS = c.sub / (64 * c.W);
+    os << "// longhair_amd windowed encode, k=" << c.k << " m=" << c.m << " bytes=" << c.bytes << "\n"
+       << "#ifndef LH_NT\n#define LH_NT 1\n#endif\n"
+       << "__device__ __forceinline__ unsigned int lh_ld(const unsigned char *p) {\n"
+       << "#if LH_NT\n  return __builtin_nontemporal_load((const unsigned int *)p);\n#else\n"
+       << "  unsigned int w; __builtin_memcpy(&w, p, 4); return w;\n#endif\n}\n"
+       << "__device__ __forceinline__ void lh_st(unsigned char *p, unsigned int v) {\n"
+       << "#if LH_NT\n  __builtin_nontemporal_store(v, (unsigned int *)p);\n#else\n"
+       << "  __builtin_memcpy(p, &v, 4);\n#endif\n}\n";
+    // LH_PINn: keep the accumulators in registers between columns (no re-association).
+    for (int n = 1; n <= R; ++n) {
+        os << "#define LH_PIN" << n << " do {";
+        for (int r = 0; r < n; ++r)
+            for (int y = 0; y < 8; ++y) os << " asm volatile(\"\" : \"+v\"(a" << r << "_" << y << "));";
+        os << " } while (0)\n";
+    }
+    if (c.win != 2)
+        for (int g = 0; g < NG; ++g) emit_win_group(os, c, G, g);
+    if (c.win == 2) {
+        // Decode phase A over a plan record (kernels.hpp PlanView): slot of original x at
+        // [16 + e_max + x], slot of recovery row r at [16 + e_max + k + r], 0xFF = absent.
+        const int e_max = std::min(c.k, c.m);
+        os << "__device__ __forceinline__ const unsigned char *lh_col(const unsigned char *pl, int x, "
+              "const unsigned char *base, const unsigned char *zero) {\n"
+           << "  const unsigned int s = pl[" << 16 + e_max << " + x];\n"
+           << "  return s == 0xFFu ? zero : base + (long long)s * " << c.bytes << ";\n}\n"
+           << "__device__ __forceinline__ const unsigned char *lh_rec(const unsigned char *pl, int r, "
+              "const unsigned char *base, const unsigned char *zero) {\n"
+           << "  const unsigned int s = pl[" << 16 + e_max + c.k << " + r];\n"
+           << "  return s == 0xFFu ? zero : base + (long long)s * " << c.bytes << ";\n}\n";
+        for (int g = 0; g < NG; ++g) emit_win_group(os, c, G, g);
+        os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
+           << "lh_jit_elim_win(const unsigned char *__restrict__ blocks, long long stride,\n"
+           << "                const unsigned char *__restrict__ plan, long long plan_stride,\n"
+           << "                const unsigned char *__restrict__ zero_page, unsigned char *__restrict__ ws,\n"
+           << "                long long ws_stride, int stripes) {\n"
+           << "  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
+           << "  const long long stripe = blockIdx.x / " << CPS << ";\n"
+           << "  if (stripe >= stripes) return;\n"
+           << "  const unsigned char *pl = plan + stripe * plan_stride;\n"
+           << "  if (pl[0] == 0) return;\n"
+           << "  const int p = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << " + (int)(threadIdx.x & 63) * "
+           << c.W << ";\n"
+           << "  const unsigned char *b = blocks + stripe * stride + p;\n"
+           << "  const unsigned char *z = zero_page + p;\n"
+           << "  unsigned char *o = ws + stripe * ws_stride + p;\n";
+        for (int g = 0; g < NG; ++g)
+            os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << "(b, z, pl, o);\n";
+        os << "}\n";
+        return os.str();
+    }
+    os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
+       << "lh_jit_encode_win(const unsigned char *__restrict__ in, long long in_stride,\n"
+       << "                  unsigned char *__restrict__ out, long long out_stride, int stripes) {\n"
+       << "  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
+       << "  const long long stripe = blockIdx.x / " << CPS << ";\n"
+       << "  if (stripe >= stripes) return;\n"
+       << "  const int p = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << " + (int)(threadIdx.x & 63) * "
+       << c.W << ";\n"
+       << "  const unsigned char *b = in + stripe * in_stride + p;\n"
+       << "  unsigned char *o = out + stripe * out_stride + p;\n";
+    for (int g = 0; g < NG; ++g) os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << "(b, o);\n";
+    os << "}\n";
+    return os.str();
+}
+
 std::string jit_source_for(const JitConfig &c) {
     std::ostringstream os;
+    if (c.win) {
+        std::string tok;
+        for (char ch : c.defines + " ") {  // tuning knobs as for the regular modules
+            if (ch == ' ' || ch == ',') {
+                const size_t eq = tok.find('=');
+                if (!tok.empty()) os << "#define " << (eq == std::string::npos ? tok : tok.substr(0, eq) + " " + tok.substr(eq + 1)) << "\n";
+                tok.clear();
+            } else {
+                tok += ch;
+            }
+        }
+        os << win_source_for(c);
+        return os.str();
+    }
     // Tuning knobs "NAME=VALUE" separated by spaces or commas.
     {
         std::string tok;
@@ -125,24 +317,73 @@ std::string jit_source_for(const JitConfig &c) {
 
 const JitKernels *JitCache::peek(const JitConfig &cfg) {
     std::lock_guard<std::mutex> g(mu_);
-    auto it = cache_.find(Key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines));
+    auto it = cache_.find(Key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines, cfg.win));
     return it == cache_.end() ? nullptr : &it->second;
 }
 
-const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err) {
-    std::lock_guard<std::mutex> g(mu_);
-    const Key key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines);
-    auto it = cache_.find(key);
-    if (it != cache_.end()) return &it->second;
+// ------------------------------------------------------------ code-object cache
+// Compiled code objects are kept on disk, keyed by a hash of the generated source and
+// the compile options, so a shape is compiled once per machine (the large-m windowed
+// modules take about a minute).  Directory: $LONGHAIR_AMD_CACHE_DIR, else jit_cache/
+// next to liblonghair_amd.so (it travels with the repository), else ~/.cache/longhair_amd.
+static const char *kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
 
+static uint64_t fnv1a(const std::string &s, uint64_t h = 1469598103934665603ull) {
+    for (unsigned char ch : s) h = (h ^ ch) * 1099511628211ull;
+    return h;
+}
+
+static std::string cache_dir() {
+    if (const char *d = std::getenv("LONGHAIR_AMD_CACHE_DIR")) return d;
+    Dl_info info;
+    if (dladdr((void *)&fnv1a, &info) && info.dli_fname) {
+        std::string p = info.dli_fname;
+        const size_t slash = p.rfind('/');
+        if (slash != std::string::npos) {
+            std::string d = p.substr(0, slash) + "/jit_cache";
+            mkdir(d.c_str(), 0755);
+            if (access(d.c_str(), W_OK) == 0) return d;
+        }
+    }
+    if (const char *home = std::getenv("HOME")) {
+        std::string d = std::string(home) + "/.cache";
+        mkdir(d.c_str(), 0755);
+        d += "/longhair_amd";
+        mkdir(d.c_str(), 0755);
+        return d;
+    }
+    return "";
+}
+
+static std::string cache_path(const std::string &src) {
+    std::string key = src;
+    for (const char *o : kOpts) key += std::string("\n") + o;
+    char name[64];
+    snprintf(name, sizeof(name), "/lh_%016llx.co", (unsigned long long)fnv1a(key));
+    const std::string d = cache_dir();
+    return d.empty() ? "" : d + name;
+}
+
+bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::string *err) {
     const std::string src = jit_source_for(cfg);
+    const std::string path = cache_path(src);
+    if (!path.empty()) {
+        if (FILE *f = fopen(path.c_str(), "rb")) {
+            fseek(f, 0, SEEK_END);
+            const long n = ftell(f);
+            fseek(f, 0, SEEK_SET);
+            code->resize(n > 0 ? (size_t)n : 0);
+            const bool ok = n > 0 && fread(code->data(), 1, (size_t)n, f) == (size_t)n;
+            fclose(f);
+            if (ok) return true;
+        }
+    }
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "lh_jit_codec.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
         *err = "hiprtcCreateProgram failed";
-        return nullptr;
+        return false;
     }
-    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-    const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof(kOpts) / sizeof(kOpts[0])), kOpts);
     if (rc != HIPRTC_SUCCESS) {
         size_t n = 0;
         hiprtcGetProgramLogSize(prog, &n);
@@ -150,29 +391,57 @@ const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err) {
         hiprtcGetProgramLog(prog, &log[0]);
         *err = "hiprtc compile failed: " + log;
         hiprtcDestroyProgram(&prog);
-        return nullptr;
+        return false;
     }
     size_t code_size = 0;
     hiprtcGetCodeSize(prog, &code_size);
-    std::vector<char> code(code_size);
-    hiprtcGetCode(prog, code.data());
+    code->resize(code_size);
+    hiprtcGetCode(prog, code->data());
     hiprtcDestroyProgram(&prog);
+    if (!path.empty()) {  // write-then-rename so concurrent processes never read a torn file
+        const std::string tmp = path + ".tmp." + std::to_string((long long)getpid());
+        if (FILE *f = fopen(tmp.c_str(), "wb")) {
+            const bool ok = fwrite(code->data(), 1, code->size(), f) == code->size();
+            fclose(f);
+            if (ok) rename(tmp.c_str(), path.c_str());
+            else unlink(tmp.c_str());
+        }
+    }
+    return true;
+}
+
+const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err) {
+    std::lock_guard<std::mutex> g(mu_);
+    const Key key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines, cfg.win);
+    auto it = cache_.find(key);
+    if (it != cache_.end()) return &it->second;
+
+    std::vector<char> code;
+    if (!compile_code_object(cfg, &code, err)) return nullptr;
 
     JitKernels kern;
     kern.cfg = cfg;
-    if (hipModuleLoadData(&kern.module, code.data()) != hipSuccess ||
-        hipModuleGetFunction(&kern.encode, kern.module, "lh_jit_encode") != hipSuccess ||
-        hipModuleGetFunction(&kern.decode, kern.module, "lh_jit_decode") != hipSuccess) {
-        *err = "hipModuleLoadData/GetFunction failed for the specialised kernels";
+    if (hipModuleLoadData(&kern.module, code.data()) != hipSuccess) {
+        *err = "hipModuleLoadData failed for the specialised kernels";
         return nullptr;
     }
-    if (hipModuleGetFunction(&kern.encode_dma, kern.module, "lh_jit_encode_dma") != hipSuccess) {
-        (void)hipGetLastError();
-        kern.encode_dma = nullptr;
-    }
-    if (hipModuleGetFunction(&kern.decode_fused, kern.module, "lh_jit_decode_fused") != hipSuccess) {
-        (void)hipGetLastError();
-        kern.decode_fused = nullptr;
+    auto fn = [&](const char *name) -> hipFunction_t {
+        hipFunction_t f = nullptr;
+        if (hipModuleGetFunction(&f, kern.module, name) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        return f;
+    };
+    kern.encode = fn("lh_jit_encode");
+    kern.decode = fn("lh_jit_decode");
+    kern.encode_dma = fn("lh_jit_encode_dma");
+    kern.decode_fused = fn("lh_jit_decode_fused");
+    kern.encode_win = fn("lh_jit_encode_win");
+    kern.elim_win = fn("lh_jit_elim_win");
+    if (!kern.encode && !kern.encode_win && !kern.elim_win) {
+        *err = "specialised module has no encode kernel";
+        return nullptr;
     }
     auto res = cache_.emplace(key, kern);
     return &res.first->second;

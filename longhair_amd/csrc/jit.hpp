@@ -19,6 +19,8 @@ struct JitConfig {
     int spw;   // stripes per wave (nch <= 64) or 0
     int wps;   // waves per stripe (nch > 64) or 0
     std::string defines;  // extra -D style tuning knobs (LONGHAIR_AMD_JIT_DEFINES)
+    int win = 0;          // 1: windowed encode module, 2: windowed decode phase-A module
+    int rows_per_wave = 8;
     int lanes_per_launch_unit() const { return 64; }
 };
 
@@ -28,6 +30,8 @@ struct JitKernels {
     hipFunction_t decode = nullptr;
     hipFunction_t encode_dma = nullptr;    // present when compiled with LH_DMA=1
     hipFunction_t decode_fused = nullptr;  // plan computed in-kernel (e_max <= 4)
+    hipFunction_t encode_win = nullptr;    // windowed large-m encode (win modules)
+    hipFunction_t elim_win = nullptr;      // windowed decode phase A (win == 2 modules)
     JitConfig cfg{};
 };
 
@@ -35,6 +39,9 @@ struct JitKernels {
 // is served by the generic kernel (too many recovery rows for the register budget, or
 // a network too large for the instruction cache).
 bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg);
+
+// Windowed large-m encode configuration (m too large for the register-resident network).
+bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode = false);
 
 // Number of ones in the expanded generator (= XORs of the straight-line network).
 long long generator_ones(int k, int m);
@@ -48,11 +55,15 @@ public:
     const JitKernels *peek(const JitConfig &cfg);
 
 private:
-    using Key = std::tuple<int, int, int, int, std::string>;
+    using Key = std::tuple<int, int, int, int, std::string, int>;
     std::mutex mu_;
     std::map<Key, JitKernels> cache_;
 };
 
 std::string jit_source_for(const JitConfig &cfg);
+
+// Compile (or fetch from the on-disk cache) the code object of a configuration.  Needs
+// no GPU, so build steps can pre-populate the cache.
+bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::string *err);
 
 }  // namespace lh

@@ -335,7 +335,7 @@ __global__ void __launch_bounds__(64) lh_plan_kernel(lh::PlanArgs a) {
         const int i = q / e, j = q % e;
         pv.set_coef(i, rcv_row[j], aug[i * w2 + e + j]);
     }
-    for (int q = lane; q < e * k; q += 64) {
+    for (int q = lane; a.want_w && q < e * k; q += 64) {
         const int i = q / k, slot = q % k;
         const int r = rows[slot];
         uint8_t v = 0;
@@ -504,6 +504,68 @@ __global__ void __launch_bounds__(256) lh_plan_small_kernel(lh::PlanArgs a) {
     for (int i = 0; i < EM; ++i) if (i < e) rws[rslot[i]] = (uint8_t)er[i];
 }
 
+// ------------------------------------------------------- wide decode, phase B
+// Large-m decode, second half: D_{E_i} = sum_r B(coef[i][r]) V_r, where V (m rows per
+// stripe, written by the windowed phase-A kernel lh_jit_elim_win) already holds
+// R_r + sum_{x present} B(G[r][x]) D_x.  One workgroup per (stripe, 256-byte column
+// chunk); wave g owns outputs [8g, 8g + 8).  Coefficients are uniform per workgroup, so
+// every coefficient bit is a scalar branch: only set bits cost XORs (8 per set bit and
+// output).  V_r is expanded once per row into its B(2^t) ladder.
+__global__ void __launch_bounds__(512) lh_apply_wide_kernel(lh::WideArgs a) {
+    constexpr int W = 4, RO = 8;
+    const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int cps = a.sub / (64 * W);
+    const long long s = blockIdx.x / cps;
+    if (s >= a.stripes) return;
+    const int p = (int)(blockIdx.x % cps) * 64 * W + lane * W;
+    const lh::PlanView pv(a.plan + s * a.plan_stride, a.k, a.m, a.e_max);
+    const int e = pv.e();
+    const int i0 = g * RO;
+    if (i0 >= e) return;
+    const uint8_t *coef = pv.coef_ptr();
+    const uint8_t *v = a.ws + s * a.ws_stride + p;
+    uint32_t acc[RO][8];
+#pragma unroll
+    for (int i = 0; i < RO; ++i)
+#pragma unroll
+        for (int y = 0; y < 8; ++y) acc[i][y] = 0;
+    for (int r = 0; r < a.m; ++r) {
+        // Skip rows no output of this wave uses (absent recovery rows).
+        uint32_t any = 0;
+#pragma unroll
+        for (int i = 0; i < RO; ++i) any |= (i0 + i < e) ? coef[(i0 + i) * a.m + r] : 0u;
+        any = __builtin_amdgcn_readfirstlane(any);
+        if (!any) continue;
+        uint32_t lad[8][8];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) __builtin_memcpy(&lad[0][b], v + (long long)r * a.bytes + b * a.sub, 4);
+#pragma unroll
+        for (int t = 1; t < 8; ++t) {
+#pragma unroll
+            for (int y = 0; y < 7; ++y) lad[t][y] = lad[t - 1][y + 1];
+            lad[t][7] = lad[t - 1][0] ^ lad[t - 1][1] ^ lad[t - 1][2] ^ lad[t - 1][7];
+        }
+#pragma unroll
+        for (int i = 0; i < RO; ++i) {
+            const uint32_t c = __builtin_amdgcn_readfirstlane((i0 + i < e) ? coef[(i0 + i) * a.m + r] : 0u);
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                if ((c >> t) & 1u)
+#pragma unroll
+                    for (int y = 0; y < 8; ++y) acc[i][y] ^= lad[t][y];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < RO; ++i) {
+        if (i0 + i < e) {
+            uint8_t *dst = a.blocks + s * a.blocks_stride + (long long)pv.out_slot(i0 + i) * a.bytes + p;
+#pragma unroll
+            for (int y = 0; y < 8; ++y) __builtin_memcpy(dst + y * a.sub, &acc[i][y], 4);
+        }
+    }
+}
+
 // ------------------------------------------------------------------ host launchers
 namespace lh {
 
@@ -528,6 +590,13 @@ hipError_t launch_xor_reduce(const XorArgs &a, hipStream_t st) {
 hipError_t launch_scatter(const ScatterArgs &a, hipStream_t st) {
     const long long lanes = (long long)a.stripes * a.e_max * ((a.bytes + 15) / 16);
     hipLaunchKernelGGL(lh_scatter_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_apply_wide(const WideArgs &a, hipStream_t st) {
+    const long long blocks = (long long)a.stripes * (a.sub / 256);
+    const int waves = (a.e_max + 7) / 8;
+    hipLaunchKernelGGL(lh_apply_wide_kernel, dim3((unsigned)blocks), dim3(64 * waves), 0, st, a);
     return hipGetLastError();
 }
 

@@ -53,7 +53,9 @@ def test_specialisation_policy():
     assert longhair_amd.batch_path(29, 4, 1296) == "jit"
     assert longhair_amd.batch_path(29, 4, 1296, decode=True) == "jit-fused"
     assert longhair_amd.batch_path(29, 8, 1296, decode=True) == "jit"
-    assert longhair_amd.batch_path(128, 32, 8192) == "generic"
+    assert longhair_amd.batch_path(128, 32, 8192) == "jit-win"
+    assert longhair_amd.batch_path(128, 32, 8192, decode=True) == "jit-wide"
+    assert longhair_amd.batch_path(128, 32, 1000) == "generic"
 
 
 def test_no_silent_cpu_path():

@@ -216,3 +216,36 @@ def test_baseline_scale_roundtrip(lh):
     for s in [0, 1, 2, 4095, 30000, stripes - 1]:
         rc, exp = oracle.encode(k, m, data[s].cpu().numpy(), nbytes)
         assert rec[s].cpu().numpy().tobytes() == exp.tobytes()
+
+
+# ------------------------------------------------------------- host-batch pipeline
+
+
+@pytest.mark.parametrize("k,m,nbytes,stripes,chunk", [(29, 4, 1296, 1000, 96), (17, 6, 520, 77, 0),
+                                                      (29, 1, 1296, 50, 8), (128, 32, 8192, 5, 2)])
+def test_host_batch_pipeline(lh, oracle, k, m, nbytes, stripes, chunk):
+    import torch
+    data = lhutil.fill(k * 3 + m, stripes * k * nbytes).reshape(stripes, k, nbytes)
+    pinned = torch.from_numpy(data).pin_memory()
+    rec = lh.encode_host_batch(pinned.numpy(), m, chunk_stripes=chunk)
+    blocks = np.zeros_like(data)
+    rows = np.zeros((stripes, k), dtype=np.uint8)
+    slots, rws = _decode_scenarios(k, m, nbytes, stripes, seed=k + m)
+    for s in range(stripes):
+        rc, exp = oracle.encode(k, m, data[s], nbytes)
+        assert rec[s].tobytes() == exp.tobytes(), s
+        for i, (kind, x) in enumerate(slots[s]):
+            blocks[s, i] = data[s, x] if kind == "d" else rec[s, x]
+        rows[s] = rws[s]
+    exp_blocks, exp_rows = blocks.copy(), rows.copy()
+    for s in range(stripes):
+        bufs = [exp_blocks[s, i].copy() for i in range(k)]
+        rc, r = oracle.decode(k, m, bufs, list(exp_rows[s]), nbytes)
+        exp_blocks[s] = np.stack(bufs)
+        exp_rows[s] = r
+    pb = torch.from_numpy(blocks).pin_memory().numpy()
+    pr = torch.from_numpy(rows).pin_memory().numpy()
+    status = lh.decode_host_batch(pb, pr, m, chunk_stripes=chunk)
+    assert (status == 0).all()
+    assert np.array_equal(pr, exp_rows)
+    assert np.array_equal(pb, exp_blocks)

@@ -24,10 +24,10 @@ def per_kernel(path, counter):
 def main():
     out_dir, cfg = sys.argv[1], sys.argv[2]
     import bench
-    k, m, nbytes, stripes = bench.CONFIGS[cfg]
+    k, m, nbytes, stripes, erasures = bench.CONFIGS[cfg]
     f = per_kernel(os.path.join(out_dir, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     w = per_kernel(os.path.join(out_dir, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
-    e = min(k, m)
+    e = min(k, m)  # decode bytes for e = min(k, m); random-erasure configs write fewer blocks
     alg = {"encode": (k + m) * nbytes * stripes, "decode": (k + e) * nbytes * stripes}
     res = {"config": cfg, "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) of "
                                     f"tools/prof_kernels.py {cfg}",
@@ -42,8 +42,8 @@ def main():
             if any(wd in name for wd in words):
                 return name, v
         return None, None
-    for role, words in (("encode", ["lh_jit_encode", "lh_apply_generic"]),
-                        ("decode", ["lh_jit_decode_fused", "lh_jit_decode", "lh_apply_generic"])):
+    for role, words in (("encode", ["lh_jit_encode_win", "lh_jit_encode", "lh_apply_generic"]),
+                        ("decode", ["lh_jit_decode_fused", "lh_jit_decode", "lh_jit_elim_win", "lh_apply_generic"])):
         name, v = pick(words)
         if v:
             res[role] = dict(v, kernel=name, ratio_to_algorithmic=v["hbm_bytes_per_launch"] / alg[role])

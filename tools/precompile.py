@@ -1,0 +1,28 @@
+#!/usr/bin/env python3
+"""Pre-populate the on-disk code-object cache (longhair_amd/jit_cache/) for the BASELINE
+shapes, without a GPU, so the first GPU run does not pay the hiprtc compile (the large-m
+windowed modules take minutes).  Usage: python tools/precompile.py [k m bytes]..."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import longhair_amd as lh  # noqa: E402
+
+DEFAULT = [(29, 4, 1296), (128, 32, 8192), (200, 56, 65536)]
+
+
+def main():
+    args = [int(a) for a in sys.argv[1:]]
+    shapes = [tuple(args[i:i + 3]) for i in range(0, len(args), 3)] or DEFAULT
+    for k, m, b in shapes:
+        t0 = time.time()
+        rc = lh.lib().cauchy_256_jit_precompile(k, m, b)
+        print(f"k={k} m={m} bytes={b}: rc={rc} {time.time() - t0:.1f} s "
+              f"{lh.lib().cauchy_256_last_error().decode()}", flush=True)
+        if rc != 0:
+            sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

@@ -32,7 +32,7 @@ def main():
     k, m, nbytes, stripes = (int(a) for a in sys.argv[1:5]) if len(sys.argv) >= 5 else (29, 4, 1296, 65536)
     torch.cuda.set_device(0)
     assert lh.cauchy_256_init() == 0
-    X, D, rows0 = bench.make_workload(k, m, nbytes, stripes, seed=7)
+    X, D, rows0, _ = bench.make_workload(k, m, nbytes, stripes, seed=7)
     e = min(k, m)
     rec_view = D[:, k - e:]
     rows = rows0.clone()
