@@ -43,7 +43,8 @@ int cauchy_256_decode_batch(int k, int m, int block_bytes, int stripes,
  * in host memory, pipelined in chunks of `chunk_stripes` (0 = about 64 MiB) over three
  * streams so the PCIe copies overlap the kernels.  Host buffers should be pinned
  * (hipHostMalloc / hipHostRegister).  Synchronous: returns when the results are in
- * host memory.  Decode copies back only the slots that change and the rows. */
+ * host memory.  Decode returns every slot of each stripe (PCIe is full duplex) and the
+ * rewritten rows. */
 int cauchy_256_encode_host_batch(int k, int m, int block_bytes, int stripes,
                                  const void *h_data, long long data_stride,
                                  void *h_recovery, long long recovery_stride, int chunk_stripes);

@@ -501,17 +501,9 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
         LH_HIP(d->pipe_rows[i].reserve((size_t)chunk * k));
         LH_HIP(d->pipe_status[i].reserve((size_t)chunk));
     }
-    // Only the recovery slots (and, for m == 1, the slot the XOR lands in) change: copy
-    // those back, not the whole stripe.  Slots are read from the caller's rows first.
-    std::vector<std::vector<int>> changed((size_t)stripes);
-    for (int s = 0; s < stripes; ++s) {
-        const uint8_t *r = h_rows + (long long)s * k;
-        int out = 0, any = 0;
-        for (int i = 0; i < k; ++i)
-            if (r[i] >= k) { changed[s].push_back(i); out = i; any = 1; }
-        if (m == 1 && k > 1) { changed[s].clear(); changed[s].push_back(any ? out : 0); }
-        if (k <= 1) changed[s].clear();
-    }
+    // The whole chunk goes back with one 2-D copy: PCIe is full duplex, so returning
+    // k blocks per stripe costs no more wall time than sending them, while per-slot
+    // copies of small blocks are dominated by per-call overhead.
     for (int s0 = 0, c = 0; s0 < stripes; s0 += chunk, ++c) {
         const int n = stripes - s0 < chunk ? stripes - s0 : chunk;
         const int i = c % 3;
@@ -522,11 +514,8 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
         const int rc = decode_batch(k, m, bytes, n, d->pipe_blocks[i].ptr, sz, d->pipe_rows[i].ptr,
                                     (int8_t *)d->pipe_status[i].ptr, st, true);
         if (rc != kOk) return rc;
-        for (int s = s0; s < s0 + n; ++s)
-            for (int slot : changed[s])
-                LH_HIP(hipMemcpyAsync(h_blocks + (long long)s * stride + (long long)slot * bytes,
-                                      d->pipe_blocks[i].ptr + (long long)(s - s0) * sz + (long long)slot * bytes, bytes,
-                                      hipMemcpyDeviceToHost, st));
+        LH_HIP(hipMemcpy2DAsync(h_blocks + (long long)s0 * stride, stride, d->pipe_blocks[i].ptr, sz, sz, n,
+                                hipMemcpyDeviceToHost, st));
         LH_HIP(hipMemcpyAsync(h_rows + (long long)s0 * k, d->pipe_rows[i].ptr, (size_t)n * k, hipMemcpyDeviceToHost, st));
         if (h_status) LH_HIP(hipMemcpyAsync(h_status + s0, d->pipe_status[i].ptr, n, hipMemcpyDeviceToHost, st));
     }

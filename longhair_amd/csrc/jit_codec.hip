@@ -962,7 +962,10 @@ __device__ __forceinline__ void lh_fused_solve::operator()(lh_plan_regs &pr) con
         for (int i = 0; i < LH_EMAX; ++i) if (i < nr) grow[rs[i]] = (unsigned char)er[i];
 }
 
-extern "C" __global__ void __launch_bounds__(256)
+#ifndef LH_DEC_LB
+#define LH_DEC_LB 1  // min waves per SIMD the register allocator must allow (tools/tune.py)
+#endif
+extern "C" __global__ void __launch_bounds__(256, LH_DEC_LB)
 lh_jit_decode_fused(unsigned char *__restrict__ blocks, long long stripe_stride, unsigned char *__restrict__ rows,
                     signed char *__restrict__ status, const unsigned char *__restrict__ zero_page,
                     const unsigned char *__restrict__ gf_exp, const short *__restrict__ gf_log, int stripes) {

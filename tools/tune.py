@@ -19,11 +19,9 @@ import longhair_amd as lh  # noqa: E402
 
 VARIANTS = [
     ("base", {}),
-    ("fused_pfd1", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF_DEC=1"}),
-    ("fused_pfd3", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF_DEC=3"}),
-    ("nofused_pfd2", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1"}),
-    ("nofused_pfd3", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1", "LONGHAIR_AMD_JIT_DEFINES": "LH_PF_DEC=3"}),
-    ("nofused_pfd1", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1", "LONGHAIR_AMD_JIT_DEFINES": "LH_PF_DEC=1"}),
+    ("declb3", {"LONGHAIR_AMD_JIT_DEFINES": "LH_DEC_LB=3"}),
+    ("nofused", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1"}),
+    ("nofused_pfd2", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1", "LONGHAIR_AMD_JIT_DEFINES": "LH_PF_DEC=2"}),
 ]
 KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID", "LONGHAIR_AMD_NO_FUSED_PLAN"]
 
