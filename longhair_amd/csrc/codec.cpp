@@ -73,7 +73,7 @@ struct HostPinned {
 
 // Per-stream scratch (decode plans and the generic path's output workspace).
 struct Workspace {
-    DevBuf plan, work, wide;
+    DevBuf plan, work;
 };
 
 // Per-device state.
@@ -297,13 +297,14 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         LH_HIP(hipModuleLaunchKernel(jk->decode_fused, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr));
         return kOk;
     }
-    // Large m: windowed phase A into a V workspace, then the wide phase B (sub % 256 == 0).
+    // Large m (<= 64): the fused windowed decode (phase A into LDS, phase B from LDS) after
+    // the planner; sub % (64 W) == 0.
     JitConfig wcfg;
     const JitKernels *wk = nullptr;
-    if (generic && e_max <= 64 && jit_win_config_for(k, m, bytes, &wcfg, true)) {
+    if (generic && jit_win_config_for(k, m, bytes, &wcfg, true)) {
         wk = allow_compile ? d->jit.get(wcfg, &err) : d->jit.peek(wcfg);
         if (!wk && allow_compile) return fail(kHipError, err);
-        if (wk && !wk->elim_win) wk = nullptr;
+        if (wk && !wk->decode_wide) wk = nullptr;
     }
     const size_t work_bytes = (generic && !wk) ? (size_t)stripes * e_max * bytes : 0;
     Workspace *w = nullptr;
@@ -360,33 +361,14 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
     if (wk) {
         const uint8_t *zero = nullptr;
         if (int rc = zero_page(d, (size_t)bytes, &zero)) return rc;
-        const long long ws_stride = (long long)m * bytes;
-        {
-            std::lock_guard<std::mutex> g(d->mu);
-            LH_HIP(w->wide.reserve((size_t)stripes * ws_stride));
-        }
         const long long blocks = (long long)stripes * (wcfg.sub / (64 * wcfg.W));
+        if (blocks > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
         const unsigned threads = 64u * (unsigned)((m + wcfg.rows_per_wave - 1) / wcfg.rows_per_wave);
-        long long s1 = stride, s2 = plan_stride, s3 = ws_stride;
+        long long s1 = stride, s2 = plan_stride;
         const uint8_t *plan = w->plan.ptr;
-        uint8_t *ws = w->wide.ptr;
         int n = stripes;
-        void *args[] = {(void *)&d_blocks, &s1, (void *)&plan, &s2, (void *)&zero, (void *)&ws, &s3, &n};
-        LH_HIP(hipModuleLaunchKernel(wk->elim_win, (unsigned)blocks, 1, 1, threads, 1, 1, 0, st, args, nullptr));
-        WideArgs wa{};
-        wa.ws = w->wide.ptr;
-        wa.ws_stride = ws_stride;
-        wa.blocks = d_blocks;
-        wa.blocks_stride = stride;
-        wa.plan = w->plan.ptr;
-        wa.plan_stride = plan_stride;
-        wa.k = k;
-        wa.m = m;
-        wa.e_max = e_max;
-        wa.bytes = bytes;
-        wa.sub = bytes / 8;
-        wa.stripes = stripes;
-        LH_HIP(launch_apply_wide(wa, st));
+        void *args[] = {(void *)&d_blocks, &s1, (void *)&plan, &s2, (void *)&zero, &n};
+        LH_HIP(hipModuleLaunchKernel(wk->decode_wide, (unsigned)blocks, 1, 1, threads, 1, 1, 0, st, args, nullptr));
         return kOk;
     }
     // Generic: recovered originals into the workspace, then into their slots.
@@ -732,8 +714,7 @@ LH_API int cauchy_256_batch_path(int k, int m, int block_bytes, int what) {
     lh::JitConfig cfg;
     if (!lh::jit_config_for(k, m, block_bytes, what == 1, &cfg)) {
         if (what == 0) return lh::jit_win_config_for(k, m, block_bytes, &cfg) ? 3 : 0;
-        const int e_max = k < m ? k : m;
-        return (e_max <= 64 && lh::jit_win_config_for(k, m, block_bytes, &cfg, true)) ? 4 : 0;
+        return lh::jit_win_config_for(k, m, block_bytes, &cfg, true) ? 4 : 0;
     }
     // Decode: 2 when the plan is computed inside the specialised kernel (jit_codec.hip,
     // LH_FUSED: e_max <= 4, one stripe per <= 64 lanes, k <= 64).

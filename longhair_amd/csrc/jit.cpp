@@ -104,6 +104,7 @@ bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
     cfg->rows_per_wave = 8;
     if (const char *r = std::getenv("LONGHAIR_AMD_WIN_ROWS")) cfg->rows_per_wave = std::atoi(r);
     if ((m + cfg->rows_per_wave - 1) / cfg->rows_per_wave > 16) return false;  // <= 1024 threads
+    if (decode && m > 64) return false;  // the fused decode keeps m x 2 KiB of V in LDS
     cfg->defines.clear();
     if (const char *d = std::getenv("LONGHAIR_AMD_JIT_DEFINES")) cfg->defines = d;
     return true;
@@ -112,19 +113,22 @@ bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
 // Straight-line source of the 4-bit-windowed network for row group `g` (win modules):
 // per data column, the nibble-table entries the group's rows need are built once from
 // their lowest-bit predecessor, then every output sub-row XORs at most two entries.
+// Encode modules store the rows to the recovery blocks; decode modules (c.win == 2)
+// read the columns through the stripe's slot map and leave V in the LDS tile `lv`.
 static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vector<uint8_t> &G, int g) {
     const int R = c.rows_per_wave, k = c.k, m = c.m, PF = 3;
     const int r0 = g * R, r1 = std::min(m, r0 + R);
     const bool elim = c.win == 2;  // decode phase A: slot-mapped columns + recovery rows
     auto col = [&](int x) {
         std::ostringstream e;
-        if (elim) e << "lh_col(pl, " << x << ", base, zero)";
+        if (elim) e << "lh_slot(slv, " << x << ", base, zero)";
         else e << "(base + " << (long long)x * c.bytes << "LL)";
         return e.str();
     };
     os << "__device__ __forceinline__ void lh_wg" << g << "(const unsigned char *__restrict__ base, "
-       << (elim ? "const unsigned char *__restrict__ zero, const unsigned char *__restrict__ pl, " : "")
-       << "unsigned char *__restrict__ o) {\n";
+       << (elim ? "const unsigned char *__restrict__ zero, const unsigned int (&slv)[LH_NQ], unsigned int *__restrict__ lv"
+                : "unsigned char *__restrict__ o")
+       << ") {\n";
     for (int r = r0; r < r1; ++r)
         for (int y = 0; y < 8; ++y) os << "  unsigned int a" << (r - r0) << "_" << y << " = 0;\n";
     for (int q = 0; q < PF && q < k; ++q) {
@@ -177,24 +181,109 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
             for (int b = 0; b < 8; ++b) os << "    d" << slot << "_" << b << " = n" << b << ";\n";
         os << "  }\n";
     }
-    if (elim)  // V_r = R_r + sum_x ...: XOR the recovery row r (zero page if absent)
+    if (elim) {  // V_r = R_r + sum_x ...: XOR the recovery row r (zero page if absent)
         for (int r = r0; r < r1; ++r) {
-            os << "  {\n    const unsigned char *rp = lh_rec(pl, " << r << ", base, zero);\n";
+            os << "  {\n    const unsigned char *rp = lh_slot(slv, " << k + r << ", base, zero);\n";
             for (int y = 0; y < 8; ++y)
                 os << "    a" << (r - r0) << "_" << y << " ^= lh_ld(rp + " << y * c.sub << ");\n";
             os << "  }\n";
         }
-    for (int r = r0; r < r1; ++r)
-        for (int y = 0; y < 8; ++y)
-            os << "  lh_st(o + " << (long long)r * c.bytes + y * c.sub << "LL, a" << (r - r0) << "_" << y << ");\n";
+        for (int r = r0; r < r1; ++r)
+            for (int y = 0; y < 8; ++y)
+                os << "  lv[" << (r * 8 + y) * 64 << " + (threadIdx.x & 63)] = a" << (r - r0) << "_" << y << ";\n";
+    } else {
+        for (int r = r0; r < r1; ++r)
+            for (int y = 0; y < 8; ++y)
+                os << "  lh_st(o + " << (long long)r * c.bytes + y * c.sub << "LL, a" << (r - r0) << "_" << y << ");\n";
+    }
     os << "}\n";
+}
+
+// Fused large-m decode (m <= 64, one workgroup per (stripe, 64 * W-byte column chunk)):
+// phase A (V_r = R_r + sum_{x present} B(G[r][x]) D_x, windowed network above, slot maps
+// from the stripe's plan held in VGPR lanes and read with v_readlane) into an LDS tile,
+// then phase B: wave g recovers D_{E_i} = sum_r B(coef[i][r]) V_r for i in [8g, 8g + 8)
+// from LDS.  Coefficients are workgroup-uniform, so each coefficient bit is a scalar
+// branch; V_r is doubled in place (B(2) in bit-sliced form: (v1..v7, v0^v1^v2^v7)).
+static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::vector<uint8_t> &G) {
+    const int R = c.rows_per_wave, NG = (c.m + R - 1) / R, CPS = c.sub / (64 * c.W);
+    const int e_max = std::min(c.k, c.m), km = c.k + c.m;
+    const int coef_off = 16 + e_max + c.k + c.m;  // kernels.hpp PlanView
+    os << "#define LH_NQ " << (km + 63) / 64 << "\n"
+       << "__device__ __forceinline__ const unsigned char *lh_slot(const unsigned int (&slv)[LH_NQ], const int i,\n"
+       << "    const unsigned char *base, const unsigned char *zero) {\n"
+       << "  const unsigned int s = (unsigned int)__builtin_amdgcn_readlane((int)slv[i / 64], i % 64);\n"
+       << "  return s == 0xFFu ? zero : base + (long long)s * " << c.bytes << ";\n}\n";
+    for (int g = 0; g < NG; ++g) emit_win_group(os, c, G, g);
+    os << "__device__ __forceinline__ void lh_phase_b(const int g, const int e, const int lane,\n"
+       << "    const unsigned int *__restrict__ lv, const unsigned char *__restrict__ cf,\n"
+       << "    const unsigned char *__restrict__ used, const int nu, const unsigned char *__restrict__ pl,\n"
+       << "    unsigned char *__restrict__ base) {\n"
+       << "  const int i0 = g * 8;\n"
+       << "  if (i0 >= e) return;\n"
+       << "  unsigned int acc[8][8];\n"
+       << "#pragma unroll\n  for (int i = 0; i < 8; ++i)\n#pragma unroll\n    for (int y = 0; y < 8; ++y) acc[i][y] = 0;\n"
+       << "  for (int j = 0; j < nu; ++j) {\n"
+       << "    const int r = __builtin_amdgcn_readfirstlane(used[j]);\n"
+       << "    unsigned int v[8], cs[8];\n"
+       << "#pragma unroll\n    for (int y = 0; y < 8; ++y) v[y] = lv[(r * 8 + y) * 64 + lane];\n"
+       << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n"
+       << "      cs[i] = __builtin_amdgcn_readfirstlane(i0 + i < e ? (unsigned int)cf[(i0 + i) * " << c.m << " + r] : 0u);\n"
+       << "#pragma unroll\n    for (int t = 0; t < 8; ++t) {\n"
+       << "#pragma unroll\n      for (int i = 0; i < 8; ++i)\n"
+       << "        if ((cs[i] >> t) & 1u)\n"
+       << "#pragma unroll\n          for (int y = 0; y < 8; ++y) acc[i][y] ^= v[y];\n"
+       << "      if (t < 7) {\n"
+       << "        const unsigned int t7 = v[0] ^ v[1] ^ v[2] ^ v[7];\n"
+       << "#pragma unroll\n        for (int y = 0; y < 7; ++y) v[y] = v[y + 1];\n"
+       << "        v[7] = t7;\n      }\n    }\n  }\n"
+       << "#pragma unroll\n  for (int i = 0; i < 8; ++i)\n"
+       << "    if (i0 + i < e) {\n"
+       << "      unsigned char *dst = base + (long long)pl[16 + i0 + i] * " << c.bytes << ";\n"
+       << "#pragma unroll\n      for (int y = 0; y < 8; ++y) lh_st(dst + y * " << c.sub << ", acc[i][y]);\n"
+       << "    }\n}\n";
+    os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
+       << "lh_jit_decode_wide(unsigned char *__restrict__ blocks, long long stride,\n"
+       << "                   const unsigned char *__restrict__ plan, long long plan_stride,\n"
+       << "                   const unsigned char *__restrict__ zero_page, int stripes) {\n"
+       << "  __shared__ unsigned int lv[" << c.m * 8 * 64 << "];\n"
+       << "  __shared__ unsigned char cf[" << e_max * c.m << "];\n"
+       << "  __shared__ unsigned char used[" << c.m << "];\n"
+       << "  __shared__ int n_used;\n"
+       << "  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
+       << "  const int lane = threadIdx.x & 63;\n"
+       << "  const long long stripe = blockIdx.x / " << CPS << ";\n"
+       << "  if (stripe >= stripes) return;\n"
+       << "  const unsigned char *pl = plan + stripe * plan_stride;\n"
+       << "  const int e = pl[0];\n"
+       << "  if (e == 0) return;\n"
+       << "  for (int q = threadIdx.x; q < e * " << c.m << "; q += blockDim.x) cf[q] = pl[" << coef_off << " + q];\n"
+       << "  unsigned int slv[LH_NQ];\n"
+       << "#pragma unroll\n  for (int q = 0; q < LH_NQ; ++q) {\n"
+       << "    const int i = q * 64 + lane;\n"
+       << "    slv[q] = i < " << km << " ? (unsigned int)pl[" << 16 + e_max << " + i] : 0xFFu;\n"
+       << "  }\n"
+       << "  if (g == 0) {  // recovery rows present in the stripe = the coefficient columns in use\n"
+       << "    const bool u = lane < " << c.m << " && pl[" << 16 + e_max + c.k << " + lane] != 0xFFu;\n"
+       << "    const unsigned long long bal = __ballot(u);\n"
+       << "    if (u) used[__builtin_popcountll(bal & ((1ull << lane) - 1))] = (unsigned char)lane;\n"
+       << "    if (lane == 0) n_used = (int)__builtin_popcountll(bal);\n"
+       << "  }\n"
+       << "  const int p = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << " + lane * " << c.W << ";\n"
+       << "  unsigned char *b = blocks + stripe * stride + p;\n"
+       << "  const unsigned char *z = zero_page + p;\n";
+    for (int g = 0; g < NG; ++g) os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << "(b, z, slv, lv);\n";
+    os << "  __syncthreads();\n"
+       << "  lh_phase_b(g, e, lane, lv, cf, used, n_used, pl, b);\n"
+       << "}\n";
 }
 
 static std::string win_source_for(const JitConfig &c) {
     std::ostringstream os;
     const std::vector<uint8_t> G = generator_matrix(c.k, c.m);
     const int R = c.rows_per_wave, NG = (c.m + R - 1) / R, CPS = c.sub / (64 * c.W);
-    os << "// longhair_amd windowed encode, k=" << c.k << " m=" << c.m << " bytes=" << c.bytes << "\n"
+    os << "// longhair_amd windowed " << (c.win == 2 ? "decode" : "encode") << ", k=" << c.k << " m=" << c.m
+       << " bytes=" << c.bytes << "\n"
        << "#ifndef LH_NT\n#define LH_NT 1\n#endif\n"
        << "__device__ __forceinline__ unsigned int lh_ld(const unsigned char *p) {\n"
        << "#if LH_NT\n  return __builtin_nontemporal_load((const unsigned int *)p);\n#else\n"
@@ -209,41 +298,11 @@ static std::string win_source_for(const JitConfig &c) {
             for (int y = 0; y < 8; ++y) os << " asm volatile(\"\" : \"+v\"(a" << r << "_" << y << "));";
         os << " } while (0)\n";
     }
-    if (c.win != 2)
-        for (int g = 0; g < NG; ++g) emit_win_group(os, c, G, g);
     if (c.win == 2) {
-        // Decode phase A over a plan record (kernels.hpp PlanView): slot of original x at
-        // [16 + e_max + x], slot of recovery row r at [16 + e_max + k + r], 0xFF = absent.
-        const int e_max = std::min(c.k, c.m);
-        os << "__device__ __forceinline__ const unsigned char *lh_col(const unsigned char *pl, int x, "
-              "const unsigned char *base, const unsigned char *zero) {\n"
-           << "  const unsigned int s = pl[" << 16 + e_max << " + x];\n"
-           << "  return s == 0xFFu ? zero : base + (long long)s * " << c.bytes << ";\n}\n"
-           << "__device__ __forceinline__ const unsigned char *lh_rec(const unsigned char *pl, int r, "
-              "const unsigned char *base, const unsigned char *zero) {\n"
-           << "  const unsigned int s = pl[" << 16 + e_max + c.k << " + r];\n"
-           << "  return s == 0xFFu ? zero : base + (long long)s * " << c.bytes << ";\n}\n";
-        for (int g = 0; g < NG; ++g) emit_win_group(os, c, G, g);
-        os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
-           << "lh_jit_elim_win(const unsigned char *__restrict__ blocks, long long stride,\n"
-           << "                const unsigned char *__restrict__ plan, long long plan_stride,\n"
-           << "                const unsigned char *__restrict__ zero_page, unsigned char *__restrict__ ws,\n"
-           << "                long long ws_stride, int stripes) {\n"
-           << "  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
-           << "  const long long stripe = blockIdx.x / " << CPS << ";\n"
-           << "  if (stripe >= stripes) return;\n"
-           << "  const unsigned char *pl = plan + stripe * plan_stride;\n"
-           << "  if (pl[0] == 0) return;\n"
-           << "  const int p = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << " + (int)(threadIdx.x & 63) * "
-           << c.W << ";\n"
-           << "  const unsigned char *b = blocks + stripe * stride + p;\n"
-           << "  const unsigned char *z = zero_page + p;\n"
-           << "  unsigned char *o = ws + stripe * ws_stride + p;\n";
-        for (int g = 0; g < NG; ++g)
-            os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << "(b, z, pl, o);\n";
-        os << "}\n";
+        emit_wide_decode(os, c, G);
         return os.str();
     }
+    for (int g = 0; g < NG; ++g) emit_win_group(os, c, G, g);
     os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
        << "lh_jit_encode_win(const unsigned char *__restrict__ in, long long in_stride,\n"
        << "                  unsigned char *__restrict__ out, long long out_stride, int stripes) {\n"
@@ -438,8 +497,8 @@ const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err) {
     kern.encode_dma = fn("lh_jit_encode_dma");
     kern.decode_fused = fn("lh_jit_decode_fused");
     kern.encode_win = fn("lh_jit_encode_win");
-    kern.elim_win = fn("lh_jit_elim_win");
-    if (!kern.encode && !kern.encode_win && !kern.elim_win) {
+    kern.decode_wide = fn("lh_jit_decode_wide");
+    if (!kern.encode && !kern.encode_win && !kern.decode_wide) {
         *err = "specialised module has no encode kernel";
         return nullptr;
     }

@@ -31,7 +31,7 @@ struct JitKernels {
     hipFunction_t encode_dma = nullptr;    // present when compiled with LH_DMA=1
     hipFunction_t decode_fused = nullptr;  // plan computed in-kernel (e_max <= 4)
     hipFunction_t encode_win = nullptr;    // windowed large-m encode (win modules)
-    hipFunction_t elim_win = nullptr;      // windowed decode phase A (win == 2 modules)
+    hipFunction_t decode_wide = nullptr;   // fused windowed decode (win == 2 modules, m <= 64)
     JitConfig cfg{};
 };
 

@@ -191,166 +191,173 @@ __global__ void __launch_bounds__(256) lh_scatter_kernel(lh::ScatterArgs a) {
 }
 
 // -------------------------------------------------------------------- decode plan
-// One 64-lane wave per stripe.  LDS: GF tables + the e x 2e augmented matrix.
+// One 64-lane wave per stripe, every step lane-parallel.
+//  * Classification (reference sort_blocks, cauchy_256.cpp:538-570): a row -> slot map in
+//    LDS; recovery slots (array order) and missing originals (ascending) are compacted
+//    with wave ballots and prefix popcounts.
+//  * e x e GF(256) inverse by Gauss-Jordan without row swaps: lane i owns rows i and
+//    i + 64 of [A | I], stored column-major in LDS so a wave's same-column accesses hit
+//    consecutive bytes; the pivot of column c is the lowest unused row with a non-zero
+//    entry (one ballot).  [A | I] reduces to [P | M] with row p_c of the permutation P
+//    holding the 1 of column c, so A^-1[c][:] = M[p_c][:].
+// LDS: GF tables, maps, and 2 e_max x RC bytes (RC = 64 or 128 rows).
 __global__ void __launch_bounds__(64) lh_plan_kernel(lh::PlanArgs a) {
     const int s = blockIdx.x;
     const int lane = threadIdx.x;
     const int k = a.k, m = a.m, e_max = a.e_max;
+    const int RC = e_max > 64 ? 128 : 64;  // row capacity of the augmented matrix
     __shared__ uint8_t gexp[512];
     __shared__ int16_t glog[256];
     __shared__ uint8_t rows[256];
-    __shared__ uint8_t rcv_slot[256], rcv_row[256], erasure[256], orig_slot_of[256];
-    __shared__ int sh_e, sh_status;
-    extern __shared__ uint8_t aug[];  // e_max x (2 * e_max)
+    __shared__ uint8_t slot_of[256];  // row -> slot, 0xFF absent
+    __shared__ uint8_t rcv_slot[256], rcv_row[256], erasure[256];
+    __shared__ uint8_t piv_row[128];  // p_c per column
+    __shared__ int16_t plog[256];     // normalised pivot row in log form, -1 = zero
+    extern __shared__ uint8_t aug[];  // element (i, j) at aug[j * RC + i], j < 2 e_max
 
     for (int i = lane; i < 256; i += 64) {
         gexp[i] = a.gf_exp[i];
         gexp[i + 256] = a.gf_exp[i + 256];
         glog[i] = a.gf_log[i];
+        slot_of[i] = 0xFF;
     }
     uint8_t *rws = a.rows + (long long)s * k;
     for (int i = lane; i < k; i += 64) rows[i] = rws[i];
     __syncthreads();
 
-    auto gmul = [&](uint8_t x, uint8_t y) -> uint8_t {
-        return (x && y) ? gexp[glog[x] + glog[y]] : (uint8_t)0;
-    };
-
     uint8_t *rec = a.plan + (long long)s * a.plan_stride;
     lh::PlanView pv(rec, k, m, e_max);
 
-    if (lane == 0) {
-        // Classification in array order (reference sort_blocks).  Rows outside the code
-        // or repeated make the stripe invalid (undefined behaviour in the reference).
-        uint8_t seen[256];
-        for (int i = 0; i < 256; ++i) seen[i] = 0;
-        int status = 0, n_rcv = 0;
-        for (int i = 0; i < 256; ++i) orig_slot_of[i] = 0xFF;
-        for (int i = 0; i < k; ++i) {
-            const int r = rows[i];
-            if (r >= k + m || seen[r]) status = -1;
-            else seen[r] = 1;
-            if (r < k) orig_slot_of[r] = (uint8_t)i;
-            else if (n_rcv < 256) { rcv_slot[n_rcv] = (uint8_t)i; rcv_row[n_rcv] = (uint8_t)(r - k); ++n_rcv; }
-        }
-        int e = 0;
-        if (status == 0) {
-            if (k <= 1) {
-                rows[0] = 0;  // cauchy_256.cpp:1252-1256
-            } else if (m == 1) {
-                // cauchy_decode_m1 (:487-535): the recovery block (or blocks[0] when none is
-                // present) becomes the XOR of all k blocks and takes the first missing row.
-                int out = 0;
-                for (int i = 0; i < k; ++i) if (rows[i] >= k) out = i;
-                int miss = -1;
-                for (int i = 0; i < k; ++i) if (!seen[i]) { miss = i; break; }
-                if (miss >= 0) rows[out] = (uint8_t)miss;
-                rcv_slot[0] = (uint8_t)out;
-                e = 1;
-            } else {
-                for (int i = 0, j = 0; i < 256 && j < n_rcv; ++i)
-                    if (!seen[i]) erasure[j++] = (uint8_t)i;
-                e = n_rcv;
-            }
-        }
-        sh_e = e;
-        sh_status = status;
+    // Row -> slot map.  A row outside the code or a repeated row invalidates the stripe
+    // (undefined behaviour in the reference).
+    bool bad = false;
+    for (int i = lane; i < k; i += 64) {
+        const int r = rows[i];
+        if (r >= k + m) bad = true;
+        else slot_of[r] = (uint8_t)i;
     }
     __syncthreads();
-    const int e = sh_e;
+    for (int i = lane; i < k; i += 64) {
+        const int r = rows[i];
+        if (r < k + m && slot_of[r] != i) bad = true;
+    }
+    const int status = __ballot(bad) ? -1 : 0;
+    const unsigned long long below = (1ull << lane) - 1;
+    int n_rcv = 0, n_miss = 0;
+    for (int i0 = 0; i0 < k; i0 += 64) {
+        const int i = i0 + lane;
+        const bool isrcv = i < k && rows[i] >= k;
+        const bool miss = i < k && slot_of[i] == 0xFF;
+        const unsigned long long br = __ballot(isrcv), bm = __ballot(miss);
+        if (isrcv) {
+            const int q = n_rcv + __builtin_popcountll(br & below);
+            rcv_slot[q] = (uint8_t)i;
+            rcv_row[q] = (uint8_t)(rows[i] - k);
+        }
+        if (miss) erasure[n_miss + __builtin_popcountll(bm & below)] = (uint8_t)i;
+        n_rcv += __builtin_popcountll(br);
+        n_miss += __builtin_popcountll(bm);
+    }
+    __syncthreads();
+    const int e = (status != 0 || k <= 1) ? 0 : (m == 1 ? 1 : n_rcv);
     if (lane == 0) {
         rec[0] = (uint8_t)e;
-        rec[1] = (uint8_t)(int8_t)sh_status;
-        if (a.status) a.status[s] = (int8_t)sh_status;
+        rec[1] = (uint8_t)(int8_t)status;
+        if (a.status) a.status[s] = (int8_t)status;
     }
-    if (sh_status != 0) {
-        if (lane == 0) rec[0] = 0;
+    if (status != 0) return;
+    if (k <= 1) {  // cauchy_256.cpp:1252-1256
+        if (lane == 0 && k == 1) rws[0] = 0;
         return;
     }
-    if (m == 1 || k <= 1) {
-        if (lane == 0 && e) pv.set_out_slot(0, rcv_slot[0]);
-        for (int i = lane; i < k; i += 64) rws[i] = rows[i];
+    if (m == 1) {
+        // cauchy_decode_m1 (:487-535): the last recovery slot (or slot 0 when none is
+        // present) becomes the XOR of all k blocks and takes the first missing row.
+        if (lane == 0) {
+            const int out = n_rcv ? rcv_slot[n_rcv - 1] : 0;
+            pv.set_out_slot(0, (uint8_t)out);
+            if (n_miss) rws[out] = erasure[0];
+        }
         return;
     }
     if (e == 0) return;
 
-    // Augmented [A | I] with A[i][j] = G[r_i][E_j] (r_i = recovery row of the i-th
-    // recovery slot, E_j = j-th missing original).
+    // [A | I]: A[i][j] = G[r_i][E_j] (r_i = recovery row of the i-th recovery slot,
+    // E_j = j-th missing original).
     const int w2 = 2 * e;
-    for (int q = lane; q < e * w2; q += 64) {
-        const int i = q / w2, j = q % w2;
-        uint8_t v;
-        if (j < e) v = a.G[rcv_row[i] * k + erasure[j]];
-        else v = (j - e == i) ? 1 : 0;
-        aug[i * w2 + j] = v;
+    for (int q = lane; q < w2 * RC; q += 64) {
+        const int j = q / RC, i = q - j * RC;
+        uint8_t v = 0;
+        if (i < e) v = (j < e) ? a.G[rcv_row[i] * k + erasure[j]] : (uint8_t)(j - e == i);
+        aug[q] = v;
     }
     __syncthreads();
-    // Gauss-Jordan over GF(256).
-    for (int col = 0; col < e; ++col) {
-        __shared__ int piv;
-        if (lane == 0) {
-            int p = -1;
-            for (int r = col; r < e; ++r) if (aug[r * w2 + col]) { p = r; break; }
-            piv = p;
-        }
-        __syncthreads();
-        const int p = piv;
-        if (p < 0) {  // singular: cannot happen for distinct valid rows (Cauchy MDS)
+    bool used0 = false, used1 = false;  // rows lane and lane + 64 are pivots already
+    const int r1 = lane + 64;
+    for (int c = 0; c < e; ++c) {
+        const bool c0 = lane < e && !used0 && aug[c * RC + lane] != 0;
+        const bool c1 = RC > 64 && r1 < e && !used1 && aug[c * RC + r1] != 0;
+        const unsigned long long b0 = __ballot(c0), b1 = __ballot(c1);
+        if (!b0 && !b1) {  // singular: impossible for distinct valid rows (Cauchy MDS)
             if (lane == 0) { rec[0] = 0; rec[1] = 0xFF; if (a.status) a.status[s] = -1; }
             return;
         }
-        if (p != col) {
-            for (int j = lane; j < w2; j += 64) {
-                const uint8_t t0 = aug[col * w2 + j];
-                aug[col * w2 + j] = aug[p * w2 + j];
-                aug[p * w2 + j] = t0;
+        const int p = b0 ? __builtin_ctzll(b0) : 64 + __builtin_ctzll(b1);
+        if (p == lane) used0 = true;
+        if (p == r1) used1 = true;
+        const int linv = 255 - glog[aug[c * RC + p]];
+        __syncthreads();
+        // Normalise the pivot row (its columns < c are zero: earlier pivots cleared them).
+        for (int j = c + lane; j < w2; j += 64) {
+            const uint32_t v = aug[j * RC + p];
+            const uint32_t nv = v ? gexp[glog[v] + linv] : 0u;
+            aug[j * RC + p] = (uint8_t)nv;
+            plog[j] = nv ? glog[nv] : (int16_t)-1;
+        }
+        if (lane == 0) piv_row[c] = (uint8_t)p;
+        __syncthreads();
+        // Clear column c from every other row.
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int i = lane + 64 * h;
+            if (i >= e || i == p || (h == 1 && RC == 64)) continue;
+            const uint32_t f = aug[c * RC + i];
+            if (!f) continue;
+            const int lf = glog[f];
+            for (int j = c; j < w2; ++j) {
+                const int pl = plog[j];
+                if (pl >= 0) aug[j * RC + i] ^= gexp[lf + pl];
             }
         }
         __syncthreads();
-        const uint8_t pinv = gexp[255 - glog[aug[col * w2 + col]]];
-        __syncthreads();
-        for (int j = lane; j < w2; j += 64) aug[col * w2 + j] = gmul(aug[col * w2 + j], pinv);
-        __syncthreads();
-        for (int q = lane; q < e * w2; q += 64) {
-            const int r = q / w2, j = q % w2;
-            if (r == col) continue;
-            const uint8_t f = aug[r * w2 + col];
-            if (j == col) continue;  // column `col` cleared below, after every row used f
-            aug[r * w2 + j] ^= gmul(f, aug[col * w2 + j]);
-        }
-        __syncthreads();
-        for (int r = lane; r < e; r += 64) if (r != col) aug[r * w2 + col] = 0;
-        __syncthreads();
     }
-    // Ainv[i][j] = aug[i][e + j].  Emit: out slots, src/rec slot maps, coef (e x m over
+    // A^-1[c][j] = aug[e + j][p_c].  Emit: out slots, src/rec slot maps, coef (e x m over
     // recovery rows) and W (e x k over slots).
     for (int i = lane; i < e; i += 64) pv.set_out_slot(i, rcv_slot[i]);
-    for (int x = lane; x < k; x += 64) pv.set_src_slot(x, orig_slot_of[x]);
-    for (int r = lane; r < m; r += 64) pv.set_rec_slot(r, 0xFF);
-    __syncthreads();
-    for (int j = lane; j < e; j += 64) pv.set_rec_slot(rcv_row[j], rcv_slot[j]);
+    for (int x = lane; x < k; x += 64) pv.set_src_slot(x, slot_of[x]);
+    for (int r = lane; r < m; r += 64) pv.set_rec_slot(r, slot_of[k + r]);
     for (int q = lane; q < e * m; q += 64) pv.set_coef(q / m, q % m, 0);
     __syncthreads();
     for (int q = lane; q < e * e; q += 64) {
         const int i = q / e, j = q % e;
-        pv.set_coef(i, rcv_row[j], aug[i * w2 + e + j]);
+        pv.set_coef(i, rcv_row[j], aug[(e + j) * RC + piv_row[i]]);
     }
     for (int q = lane; a.want_w && q < e * k; q += 64) {
         const int i = q / k, slot = q % k;
         const int r = rows[slot];
-        uint8_t v = 0;
+        uint32_t v = 0;
         if (r >= k) {
-            for (int j = 0; j < e; ++j) if (rcv_slot[j] == slot) v = aug[i * w2 + e + j];
+            for (int j = 0; j < e; ++j) if (rcv_slot[j] == slot) v = aug[(e + j) * RC + piv_row[i]];
         } else {
-            for (int j = 0; j < e; ++j) v ^= gmul(aug[i * w2 + e + j], a.G[rcv_row[j] * k + r]);
+            for (int j = 0; j < e; ++j) {
+                const uint32_t x = aug[(e + j) * RC + piv_row[i]], y = a.G[rcv_row[j] * k + r];
+                if (x && y) v ^= gexp[glog[x] + glog[y]];
+            }
         }
-        pv.set_w(i, slot, v);
+        pv.set_w(i, slot, (uint8_t)v);
     }
-    __syncthreads();
     // Recovery slot i takes erased row E_i (reference generate_bitmatrix, :786).
-    for (int i = lane; i < e; i += 64) rows[rcv_slot[i]] = erasure[i];
-    __syncthreads();
-    for (int i = lane; i < k; i += 64) rws[i] = rows[i];
+    for (int i = lane; i < e; i += 64) rws[rcv_slot[i]] = erasure[i];
 }
 
 // ------------------------------------------------------- decode plan, small e_max
@@ -504,68 +511,6 @@ __global__ void __launch_bounds__(256) lh_plan_small_kernel(lh::PlanArgs a) {
     for (int i = 0; i < EM; ++i) if (i < e) rws[rslot[i]] = (uint8_t)er[i];
 }
 
-// ------------------------------------------------------- wide decode, phase B
-// Large-m decode, second half: D_{E_i} = sum_r B(coef[i][r]) V_r, where V (m rows per
-// stripe, written by the windowed phase-A kernel lh_jit_elim_win) already holds
-// R_r + sum_{x present} B(G[r][x]) D_x.  One workgroup per (stripe, 256-byte column
-// chunk); wave g owns outputs [8g, 8g + 8).  Coefficients are uniform per workgroup, so
-// every coefficient bit is a scalar branch: only set bits cost XORs (8 per set bit and
-// output).  V_r is expanded once per row into its B(2^t) ladder.
-__global__ void __launch_bounds__(512) lh_apply_wide_kernel(lh::WideArgs a) {
-    constexpr int W = 4, RO = 8;
-    const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int cps = a.sub / (64 * W);
-    const long long s = blockIdx.x / cps;
-    if (s >= a.stripes) return;
-    const int p = (int)(blockIdx.x % cps) * 64 * W + lane * W;
-    const lh::PlanView pv(a.plan + s * a.plan_stride, a.k, a.m, a.e_max);
-    const int e = pv.e();
-    const int i0 = g * RO;
-    if (i0 >= e) return;
-    const uint8_t *coef = pv.coef_ptr();
-    const uint8_t *v = a.ws + s * a.ws_stride + p;
-    uint32_t acc[RO][8];
-#pragma unroll
-    for (int i = 0; i < RO; ++i)
-#pragma unroll
-        for (int y = 0; y < 8; ++y) acc[i][y] = 0;
-    for (int r = 0; r < a.m; ++r) {
-        // Skip rows no output of this wave uses (absent recovery rows).
-        uint32_t any = 0;
-#pragma unroll
-        for (int i = 0; i < RO; ++i) any |= (i0 + i < e) ? coef[(i0 + i) * a.m + r] : 0u;
-        any = __builtin_amdgcn_readfirstlane(any);
-        if (!any) continue;
-        uint32_t lad[8][8];
-#pragma unroll
-        for (int b = 0; b < 8; ++b) __builtin_memcpy(&lad[0][b], v + (long long)r * a.bytes + b * a.sub, 4);
-#pragma unroll
-        for (int t = 1; t < 8; ++t) {
-#pragma unroll
-            for (int y = 0; y < 7; ++y) lad[t][y] = lad[t - 1][y + 1];
-            lad[t][7] = lad[t - 1][0] ^ lad[t - 1][1] ^ lad[t - 1][2] ^ lad[t - 1][7];
-        }
-#pragma unroll
-        for (int i = 0; i < RO; ++i) {
-            const uint32_t c = __builtin_amdgcn_readfirstlane((i0 + i < e) ? coef[(i0 + i) * a.m + r] : 0u);
-#pragma unroll
-            for (int t = 0; t < 8; ++t)
-                if ((c >> t) & 1u)
-#pragma unroll
-                    for (int y = 0; y < 8; ++y) acc[i][y] ^= lad[t][y];
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < RO; ++i) {
-        if (i0 + i < e) {
-            uint8_t *dst = a.blocks + s * a.blocks_stride + (long long)pv.out_slot(i0 + i) * a.bytes + p;
-#pragma unroll
-            for (int y = 0; y < 8; ++y) __builtin_memcpy(dst + y * a.sub, &acc[i][y], 4);
-        }
-    }
-}
-
 // ------------------------------------------------------------------ host launchers
 namespace lh {
 
@@ -593,13 +538,6 @@ hipError_t launch_scatter(const ScatterArgs &a, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_apply_wide(const WideArgs &a, hipStream_t st) {
-    const long long blocks = (long long)a.stripes * (a.sub / 256);
-    const int waves = (a.e_max + 7) / 8;
-    hipLaunchKernelGGL(lh_apply_wide_kernel, dim3((unsigned)blocks), dim3(64 * waves), 0, st, a);
-    return hipGetLastError();
-}
-
 hipError_t launch_plan(const PlanArgs &a, hipStream_t st) {
     if (a.k > 1 && a.m > 1 && a.e_max <= 8) {
         const unsigned blocks = (unsigned)((a.stripes + 255) / 256);
@@ -607,7 +545,7 @@ hipError_t launch_plan(const PlanArgs &a, hipStream_t st) {
         else hipLaunchKernelGGL(lh_plan_small_kernel<8>, dim3(blocks), dim3(256), 0, st, a);
         return hipGetLastError();
     }
-    const size_t lds = (size_t)a.e_max * 2 * a.e_max;
+    const size_t lds = (size_t)2 * a.e_max * (a.e_max > 64 ? 128 : 64);
     hipLaunchKernelGGL(lh_plan_kernel, dim3((unsigned)a.stripes), dim3(64), lds, st, a);
     return hipGetLastError();
 }

@@ -87,18 +87,7 @@ struct PlanArgs {
     int want_w;                   // emit the single-pass coefficients (generic path)
 };
 
-struct WideArgs {
-    const uint8_t *ws;            // V rows: stripe s, row r at ws + s*ws_stride + r*bytes
-    long long ws_stride;
-    uint8_t *blocks;              // decode slots (outputs go to the plan's out slots)
-    long long blocks_stride;
-    const uint8_t *plan;
-    long long plan_stride;
-    int k, m, e_max, bytes, sub, stripes;
-};
-
 hipError_t launch_apply_generic(const ApplyArgs &a, int W, hipStream_t st);
-hipError_t launch_apply_wide(const WideArgs &a, hipStream_t st);  // sub % 256 == 0, e_max <= 64
 hipError_t launch_xor_reduce(const XorArgs &a, hipStream_t st);
 hipError_t launch_scatter(const ScatterArgs &a, hipStream_t st);
 hipError_t launch_plan(const PlanArgs &a, hipStream_t st);
