@@ -483,21 +483,44 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
         LH_HIP(d->pipe_rows[i].reserve((size_t)chunk * k));
         LH_HIP(d->pipe_status[i].reserve((size_t)chunk));
     }
-    // The whole chunk goes back with one 2-D copy: PCIe is full duplex, so returning
-    // k blocks per stripe costs no more wall time than sending them, while per-slot
-    // copies of small blocks are dominated by per-call overhead.
+    // Only the slots decode can write travel back: the recovery slots (for m == 1 the
+    // last one, or slot 0 when there is none: cauchy_decode_m1's quirk).  One 2-D copy per
+    // chunk covers the range [lo, hi] of such slots over the chunk's stripes (per-slot
+    // copies of small blocks would be dominated by per-call overhead).
     for (int s0 = 0, c = 0; s0 < stripes; s0 += chunk, ++c) {
         const int n = stripes - s0 < chunk ? stripes - s0 : chunk;
         const int i = c % 3;
         hipStream_t st = d->pipe_stream[i];
+        int lo = k, hi = -1;
+        if (k > 1) {
+            for (int s = s0; s < s0 + n; ++s) {
+                const uint8_t *r = h_rows + (long long)s * k;
+                int last = -1;
+                for (int x = 0; x < k; ++x) {
+                    if (r[x] < k) continue;
+                    if (m > 1 || last < 0) lo = x < lo ? x : lo;
+                    last = x;
+                }
+                if (m == 1) {
+                    const int out = last < 0 ? 0 : last;
+                    lo = out < lo ? out : lo;
+                    hi = out > hi ? out : hi;
+                } else if (last > hi) {
+                    hi = last;
+                }
+            }
+        }
         LH_HIP(hipMemcpy2DAsync(d->pipe_blocks[i].ptr, sz, h_blocks + (long long)s0 * stride, stride, sz, n,
                                 hipMemcpyHostToDevice, st));
         LH_HIP(hipMemcpyAsync(d->pipe_rows[i].ptr, h_rows + (long long)s0 * k, (size_t)n * k, hipMemcpyHostToDevice, st));
         const int rc = decode_batch(k, m, bytes, n, d->pipe_blocks[i].ptr, sz, d->pipe_rows[i].ptr,
                                     (int8_t *)d->pipe_status[i].ptr, st, true);
         if (rc != kOk) return rc;
-        LH_HIP(hipMemcpy2DAsync(h_blocks + (long long)s0 * stride, stride, d->pipe_blocks[i].ptr, sz, sz, n,
-                                hipMemcpyDeviceToHost, st));
+        if (hi >= lo) {
+            const long long off = (long long)lo * bytes, w = (long long)(hi - lo + 1) * bytes;
+            LH_HIP(hipMemcpy2DAsync(h_blocks + (long long)s0 * stride + off, stride, d->pipe_blocks[i].ptr + off, sz, w,
+                                    n, hipMemcpyDeviceToHost, st));
+        }
         LH_HIP(hipMemcpyAsync(h_rows + (long long)s0 * k, d->pipe_rows[i].ptr, (size_t)n * k, hipMemcpyDeviceToHost, st));
         if (h_status) LH_HIP(hipMemcpyAsync(h_status + s0, d->pipe_status[i].ptr, n, hipMemcpyDeviceToHost, st));
     }

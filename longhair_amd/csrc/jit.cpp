@@ -170,10 +170,12 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
             for (int y = 0; y < 8; ++y) {
                 const int s = (int)((bm >> (8 * y)) & 0xFF), lo = s & 15, hi = s >> 4;
                 if (!lo && !hi) continue;
-                os << "    a" << (r - r0) << "_" << y << " ^= ";
-                if (lo) os << "t0_" << lo << (hi ? " ^ " : "");
-                if (hi) os << "t1_" << hi;
-                os << ";\n";
+                const std::string a = "a" + std::to_string(r - r0) + "_" + std::to_string(y);
+                if (lo && hi)  // XOR3 in one v_bitop3_b32 (hipcc does not fuse XOR chains)
+                    os << "    " << a << " = __builtin_amdgcn_bitop3_b32(" << a << ", t0_" << lo << ", t1_" << hi
+                       << ", 0x96);\n";
+                else
+                    os << "    " << a << " ^= " << (lo ? "t0_" + std::to_string(lo) : "t1_" + std::to_string(hi)) << ";\n";
             }
         }
         os << "    LH_PIN" << (r1 - r0) << ";\n";
@@ -234,7 +236,7 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
        << "        if ((cs[i] >> t) & 1u)\n"
        << "#pragma unroll\n          for (int y = 0; y < 8; ++y) acc[i][y] ^= v[y];\n"
        << "      if (t < 7) {\n"
-       << "        const unsigned int t7 = v[0] ^ v[1] ^ v[2] ^ v[7];\n"
+       << "        const unsigned int t7 = __builtin_amdgcn_bitop3_b32(v[0], v[1], v[2], 0x96) ^ v[7];\n"
        << "#pragma unroll\n        for (int y = 0; y < 7; ++y) v[y] = v[y + 1];\n"
        << "        v[7] = t7;\n      }\n    }\n  }\n"
        << "#pragma unroll\n  for (int i = 0; i < 8; ++i)\n"

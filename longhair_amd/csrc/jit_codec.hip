@@ -38,12 +38,6 @@ static constexpr unsigned char LH_BM[LH_M][LH_K][8] = {
 
 #define LH_NW ((LH_W + 3) / 4)
 
-#ifndef LH_WIN
-#define LH_WIN 0  // large-m windowed encode (see lh_jit_encode_win)
-#endif
-#ifndef LH_WIN_ONLY
-#define LH_WIN_ONLY LH_WIN  // a windowed module carries only the windowed encode
-#endif
 
 struct lh_word {
     unsigned int v[LH_NW];
@@ -94,16 +88,50 @@ __device__ __forceinline__ void lh_xor(lh_word &a, const lh_word &b) {
     for (int i = 0; i < LH_NW; ++i) a.v[i] ^= b.v[i];
 }
 
+// gfx950 v_bitop3_b32: any 3-input boolean function in one VALU op.  The LUT index is
+// (src0 << 2) | (src1 << 1) | src2: 0x96 = src0 ^ src1 ^ src2, 0x78 = src0 ^ (src1 & src2).
+// hipcc does not fuse XOR chains on its own (it emits one v_xor_b32 per term).
+__device__ __forceinline__ unsigned int lh_x3(unsigned int a, unsigned int b, unsigned int c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ unsigned int lh_xand(unsigned int a, unsigned int b, unsigned int c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x78);
+}
+__device__ __forceinline__ void lh_xor2(lh_word &a, const lh_word &b, const lh_word &c) {
+#pragma unroll
+    for (int i = 0; i < LH_NW; ++i) a.v[i] = lh_x3(a.v[i], b.v[i], c.v[i]);
+}
+
+// a ^= sum of d[b] over the set bits b of S, the terms taken two at a time (XOR3).
+template <unsigned S, int B = 0, int P = -1>
+struct lh_net {
+    __device__ __forceinline__ static void run(lh_word &a, const lh_word (&d)[8]) {
+        if constexpr (B == 8) {
+            if constexpr (P >= 0) lh_xor(a, d[P]);
+        } else if constexpr (((S >> B) & 1u) == 0) {
+            lh_net<S, B + 1, P>::run(a, d);
+        } else if constexpr (P < 0) {
+            lh_net<S, B + 1, B>::run(a, d);
+        } else {
+            lh_xor2(a, d[P], d[B]);
+            lh_net<S, B + 1, -1>::run(a, d);
+        }
+    }
+};
+
 // acc[r][y] ^= sum_x B(G[r][x]) d_x, one column x at a time, all constants.
+template <int X, int I = 0>
+struct lh_col_net {
+    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], const lh_word (&d)[8]) {
+        if constexpr (I < LH_M * 8) {
+            lh_net<LH_BM[I / 8][X][I % 8]>::run(acc[I / 8][I % 8], d);
+            lh_col_net<X, I + 1>::run(acc, d);
+        }
+    }
+};
 template <int X>
 __device__ __forceinline__ void lh_column(lh_word (&acc)[LH_M][8], const lh_word (&d)[8]) {
-#pragma unroll
-    for (int r = 0; r < LH_M; ++r)
-#pragma unroll
-        for (int y = 0; y < 8; ++y)
-#pragma unroll
-            for (int b = 0; b < 8; ++b)
-                if ((LH_BM[r][X][y] >> b) & 1) lh_xor(acc[r][y], d[b]);
+    lh_col_net<X>::run(acc, d);
 }
 
 struct lh_lane {
@@ -216,9 +244,12 @@ __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned ch
         for (int y = 0; y < 8; ++y) lh_store(o + (long long)r * LH_BYTES + y * LH_SUB, acc[r][y]);
 }
 
-#if !LH_WIN_ONLY
+#if 1
 // recovery[s][r] = sum_x B(G[r][x]) data[s][x]   (cauchy_256_encode for m > 1, valid k, m)
-extern "C" __global__ void __launch_bounds__(256)
+#ifndef LH_ENC_LB
+#define LH_ENC_LB 1  // min waves per SIMD the register allocator must allow (tools/tune.py)
+#endif
+extern "C" __global__ void __launch_bounds__(256, LH_ENC_LB)
 lh_jit_encode(const unsigned char *__restrict__ in, long long in_stride,
               unsigned char *__restrict__ out, long long out_stride, int stripes) {
     LH_WAVE_LOOP(stripes) { lh_encode_wave(lh_w, in, in_stride, out, out_stride, stripes); }
@@ -458,154 +489,6 @@ lh_jit_encode_dma(const unsigned char *__restrict__ in, long long in_stride,
 }
 #endif  // LH_DMA
 
-// ------------------------------------------------------- large-m windowed encode
-// LH_WIN = 1 (host picks it for m > 12 and sub % (64 * W) == 0): one workgroup of LH_NG
-// waves codes 64 * W bytes of every sub-block of one stripe; wave g owns output rows
-// [g * LH_R, g * LH_R + LH_R) and holds only those accumulators.  Per data column the
-// network is 4-bit windowed (the reference's win_encode idea, cauchy_256.cpp:1414-1493,
-// done at compile time): every output sub-row is T_lo[s & 15] ^ T_hi[s >> 4] of two
-// nibble tables over sub-blocks 0..3 and 4..7, whose entries are built once per column
-// from their lowest-bit predecessor and shared by all rows (the compiler's value
-// numbering merges repeated entries).  All waves of the group read the same input bytes;
-// the CU's L1 serves the repeats.
-
-#if LH_WIN
-#ifndef LH_R
-#define LH_R 8
-#endif
-#define LH_NG ((LH_M + LH_R - 1) / LH_R)
-#define LH_CPS (LH_SUB / (64 * LH_W))  // workgroups per stripe
-
-template <int N>
-__device__ __forceinline__ lh_word lh_tab(const lh_word (&d)[8], int base_b) {
-    // XOR of d[base_b + b] over the set bits b of the nibble N.
-    if (N == 0) {
-        lh_word z;
-#pragma unroll
-        for (int i = 0; i < LH_NW; ++i) z.v[i] = 0;
-        return z;
-    }
-    lh_word t = lh_tab<(N & (N - 1))>(d, base_b);
-    lh_xor(t, d[base_b + __builtin_ctz(N == 0 ? 1 : N)]);
-    return t;
-}
-template <>
-__device__ __forceinline__ lh_word lh_tab<0>(const lh_word (&)[8], int) {
-    lh_word z;
-#pragma unroll
-    for (int i = 0; i < LH_NW; ++i) z.v[i] = 0;
-    return z;
-}
-
-template <int S>
-__device__ __forceinline__ void lh_win_apply(lh_word &acc, const lh_word (&d)[8]) {
-    constexpr int LO = S & 15, HI = S >> 4;
-    if (LO) lh_xor(acc, lh_tab<LO>(d, 0));
-    if (HI) lh_xor(acc, lh_tab<HI>(d, 4));
-}
-
-template <int G, int X, int RR>
-struct lh_win_rows {
-    __device__ __forceinline__ static void run(lh_word (&acc)[LH_R][8], const lh_word (&d)[8]) {
-        constexpr int R = G * LH_R + RR;
-        if (R < LH_M) {
-            constexpr int RC = R < LH_M ? R : 0;
-            lh_win_apply<LH_BM[RC][X][0]>(acc[RR][0], d);
-            lh_win_apply<LH_BM[RC][X][1]>(acc[RR][1], d);
-            lh_win_apply<LH_BM[RC][X][2]>(acc[RR][2], d);
-            lh_win_apply<LH_BM[RC][X][3]>(acc[RR][3], d);
-            lh_win_apply<LH_BM[RC][X][4]>(acc[RR][4], d);
-            lh_win_apply<LH_BM[RC][X][5]>(acc[RR][5], d);
-            lh_win_apply<LH_BM[RC][X][6]>(acc[RR][6], d);
-            lh_win_apply<LH_BM[RC][X][7]>(acc[RR][7], d);
-        }
-        lh_win_rows<G, X, RR + 1>::run(acc, d);
-    }
-};
-template <int G, int X>
-struct lh_win_rows<G, X, LH_R> {
-    __device__ __forceinline__ static void run(lh_word (&)[LH_R][8], const lh_word (&)[8]) {}
-};
-
-__device__ __forceinline__ void lh_opaque_r(lh_word (&acc)[LH_R][8]) {
-#pragma unroll
-    for (int r = 0; r < LH_R; ++r)
-#pragma unroll
-        for (int y = 0; y < 8; ++y)
-#pragma unroll
-            for (int i = 0; i < LH_NW; ++i) asm volatile("" : "+v"(acc[r][y].v[i]));
-}
-
-template <int G, int X>
-struct lh_win_cols {
-    __device__ __forceinline__ static void run(lh_word (&acc)[LH_R][8], lh_word (&ring)[LH_PF][8],
-                                               const unsigned char *base) {
-        if (X + LH_PF < LH_K) {
-            lh_word nxt[8];
-#pragma unroll
-            for (int b = 0; b < 8; ++b) nxt[b] = lh_load(base + (long long)(X + LH_PF) * LH_BYTES + b * LH_SUB);
-            lh_win_rows<G, X, 0>::run(acc, ring[X % LH_PF]);
-            lh_opaque_r(acc);
-#pragma unroll
-            for (int b = 0; b < 8; ++b) ring[X % LH_PF][b] = nxt[b];
-        } else {
-            lh_win_rows<G, X, 0>::run(acc, ring[X % LH_PF]);
-            lh_opaque_r(acc);
-        }
-        lh_win_cols<G, X + 1>::run(acc, ring, base);
-    }
-};
-template <int G>
-struct lh_win_cols<G, LH_K> {
-    __device__ __forceinline__ static void run(lh_word (&)[LH_R][8], lh_word (&)[LH_PF][8], const unsigned char *) {}
-};
-
-template <int G>
-__device__ __forceinline__ void lh_win_group(const unsigned char *base, unsigned char *o) {
-    lh_word acc[LH_R][8];
-#pragma unroll
-    for (int r = 0; r < LH_R; ++r)
-#pragma unroll
-        for (int y = 0; y < 8; ++y)
-#pragma unroll
-            for (int i = 0; i < LH_NW; ++i) acc[r][y].v[i] = 0;
-    lh_word ring[LH_PF][8];
-#pragma unroll
-    for (int q = 0; q < LH_PF; ++q)
-#pragma unroll
-        for (int b = 0; b < 8; ++b) ring[q][b] = lh_load(base + (long long)q * LH_BYTES + b * LH_SUB);
-    lh_win_cols<G, 0>::run(acc, ring, base);
-#pragma unroll
-    for (int rr = 0; rr < LH_R; ++rr)
-        if (G * LH_R + rr < LH_M)
-#pragma unroll
-            for (int y = 0; y < 8; ++y) lh_store(o + (long long)(G * LH_R + rr) * LH_BYTES + y * LH_SUB, acc[rr][y]);
-}
-
-template <int G>
-struct lh_win_dispatch {
-    __device__ __forceinline__ static void run(int g, const unsigned char *base, unsigned char *o) {
-        if (g == G) lh_win_group<G>(base, o);
-        else lh_win_dispatch<G + 1>::run(g, base, o);
-    }
-};
-template <>
-struct lh_win_dispatch<LH_NG> {
-    __device__ __forceinline__ static void run(int, const unsigned char *, unsigned char *) {}
-};
-
-extern "C" __global__ void __launch_bounds__(64 * LH_NG)
-lh_jit_encode_win(const unsigned char *__restrict__ in, long long in_stride,
-                  unsigned char *__restrict__ out, long long out_stride, int stripes) {
-    const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const long long stripe = blockIdx.x / LH_CPS;
-    if (stripe >= stripes) return;
-    const int p = (int)(blockIdx.x % LH_CPS) * 64 * LH_W + lane * LH_W;
-    lh_win_dispatch<0>::run(g, in + stripe * in_stride + p, out + stripe * out_stride + p);
-}
-#endif  // LH_WIN
-
 // ------------------------------------------------------------------------ decode
 // Plan record layout: kernels.hpp PlanView (e at [0], out_slot at [16], then src_slot[k],
 // rec_slot[m], coef[e_max][m]).  e_max = min(k, m) for m > 1.
@@ -754,7 +637,7 @@ __device__ __forceinline__ void lh_decode_body(const lh_lane &l, unsigned char *
                 if (t != 7) {  // o = B(2) o
                     lh_word t7;
 #pragma unroll
-                    for (int q = 0; q < LH_NW; ++q) t7.v[q] = o[0].v[q] ^ o[1].v[q] ^ o[2].v[q] ^ o[7].v[q];
+                    for (int q = 0; q < LH_NW; ++q) t7.v[q] = lh_x3(o[0].v[q], o[1].v[q], o[2].v[q]) ^ o[7].v[q];
 #pragma unroll
                     for (int y = 0; y < 7; ++y) o[y] = o[y + 1];
                     o[7] = t7;
@@ -768,7 +651,7 @@ __device__ __forceinline__ void lh_decode_body(const lh_lane &l, unsigned char *
 #pragma unroll
                     for (int y = 0; y < 8; ++y)
 #pragma unroll
-                        for (int q = 0; q < LH_NW; ++q) o[y].v[q] ^= v[r][y].v[q] & mask;
+                        for (int q = 0; q < LH_NW; ++q) o[y].v[q] = lh_xand(o[y].v[q], v[r][y].v[q], mask);
                 }
 #pragma unroll
                 for (int y = 0; y < 8; ++y)
@@ -799,7 +682,7 @@ __device__ __forceinline__ void lh_decode_wave(long long wave, unsigned char *__
     lh_decode_body(l, blocks, stripe_stride, pr, zero_page, lh_no_prep());
 }
 
-#if !LH_WIN_ONLY
+#if 1
 extern "C" __global__ void __launch_bounds__(256)
 lh_jit_decode(unsigned char *__restrict__ blocks, long long stripe_stride,
               const unsigned char *__restrict__ plan, long long plan_stride,
@@ -815,7 +698,7 @@ lh_jit_decode(unsigned char *__restrict__ blocks, long long stripe_stride,
 // GF(256) log/exp tables in LDS.  Semantics follow lh_plan_small_kernel (kernels.hip):
 // reference sort_blocks (cauchy_256.cpp:538-570) and generate_bitmatrix's row
 // assignment (:786); duplicate / out-of-range rows mark the stripe invalid, untouched.
-#if LH_EMAX <= 4 && LH_NCH <= 64 && LH_K <= 64 && !LH_WIN_ONLY
+#if LH_EMAX <= 4 && LH_NCH <= 64 && LH_K <= 64
 #define LH_FUSED 1
 static constexpr unsigned char LH_GRAW[LH_M][LH_K] = LH_G_INIT;
 #define LH_P4(n) (((n) + 3) / 4 * 4)

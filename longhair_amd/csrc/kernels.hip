@@ -285,11 +285,19 @@ __global__ void __launch_bounds__(64) lh_plan_kernel(lh::PlanArgs a) {
     // [A | I]: A[i][j] = G[r_i][E_j] (r_i = recovery row of the i-th recovery slot,
     // E_j = j-th missing original).
     const int w2 = 2 * e;
-    for (int q = lane; q < w2 * RC; q += 64) {
-        const int j = q / RC, i = q - j * RC;
-        uint8_t v = 0;
-        if (i < e) v = (j < e) ? a.G[rcv_row[i] * k + erasure[j]] : (uint8_t)(j - e == i);
-        aug[q] = v;
+    for (int h = 0; h < RC / 64; ++h) {
+        const int i = lane + 64 * h;
+        if (i >= e) continue;
+        const uint8_t *grow = a.G + rcv_row[i] * k;
+        for (int j0 = 0; j0 < e; j0 += 8) {  // 8 independent gathers in flight
+            uint8_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = (j0 + u < e) ? grow[erasure[j0 + u]] : (uint8_t)0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (j0 + u < e) aug[(j0 + u) * RC + i] = v[u];
+        }
+        for (int j = 0; j < e; ++j) aug[(e + j) * RC + i] = (uint8_t)(j == i);
     }
     __syncthreads();
     bool used0 = false, used1 = false;  // rows lane and lane + 64 are pivots already
@@ -324,9 +332,16 @@ __global__ void __launch_bounds__(64) lh_plan_kernel(lh::PlanArgs a) {
             const uint32_t f = aug[c * RC + i];
             if (!f) continue;
             const int lf = glog[f];
-            for (int j = c; j < w2; ++j) {
-                const int pl = plog[j];
-                if (pl >= 0) aug[j * RC + i] ^= gexp[lf + pl];
+            for (int j0 = c; j0 < w2; j0 += 8) {  // 8 independent updates per step (LDS latency)
+                int pl[8];
+                uint32_t av[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) pl[u] = (j0 + u < w2) ? plog[j0 + u] : -1;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) av[u] = (pl[u] >= 0) ? aug[(j0 + u) * RC + i] : 0u;
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (pl[u] >= 0) aug[(j0 + u) * RC + i] = (uint8_t)(av[u] ^ gexp[lf + pl[u]]);
             }
         }
         __syncthreads();
