@@ -103,6 +103,8 @@ bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
     cfg->win = decode ? 2 : 1;
     cfg->rows_per_wave = 8;
     if (const char *r = std::getenv("LONGHAIR_AMD_WIN_ROWS")) cfg->rows_per_wave = std::atoi(r);
+    cfg->win_pf = 3;
+    if (const char *f = std::getenv("LONGHAIR_AMD_WIN_PF")) cfg->win_pf = std::max(1, std::atoi(f));
     if ((m + cfg->rows_per_wave - 1) / cfg->rows_per_wave > 16) return false;  // <= 1024 threads
     if (decode && m > 64) return false;  // the fused decode keeps m x 2 KiB of V in LDS
     cfg->defines.clear();
@@ -116,7 +118,7 @@ bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
 // Encode modules store the rows to the recovery blocks; decode modules (c.win == 2)
 // read the columns through the stripe's slot map and leave V in the LDS tile `lv`.
 static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vector<uint8_t> &G, int g) {
-    const int R = c.rows_per_wave, k = c.k, m = c.m, PF = 3;
+    const int R = c.rows_per_wave, k = c.k, m = c.m, PF = c.win_pf;
     const int r0 = g * R, r1 = std::min(m, r0 + R);
     const bool elim = c.win == 2;  // decode phase A: slot-mapped columns + recovery rows
     auto col = [&](int x) {
@@ -378,7 +380,7 @@ std::string jit_source_for(const JitConfig &c) {
 
 const JitKernels *JitCache::peek(const JitConfig &cfg) {
     std::lock_guard<std::mutex> g(mu_);
-    auto it = cache_.find(Key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines, cfg.win));
+    auto it = cache_.find(Key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines, cfg.win * 100000 + cfg.rows_per_wave * 100 + cfg.win_pf));
     return it == cache_.end() ? nullptr : &it->second;
 }
 
@@ -473,7 +475,7 @@ bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::str
 
 const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err) {
     std::lock_guard<std::mutex> g(mu_);
-    const Key key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines, cfg.win);
+    const Key key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines, cfg.win * 100000 + cfg.rows_per_wave * 100 + cfg.win_pf);
     auto it = cache_.find(key);
     if (it != cache_.end()) return &it->second;
 

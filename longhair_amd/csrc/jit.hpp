@@ -21,6 +21,7 @@ struct JitConfig {
     std::string defines;  // extra -D style tuning knobs (LONGHAIR_AMD_JIT_DEFINES)
     int win = 0;          // 1: windowed encode module, 2: windowed decode phase-A module
     int rows_per_wave = 8;
+    int win_pf = 3;       // windowed modules: columns in flight ahead of the one combined
     int lanes_per_launch_unit() const { return 64; }
 };
 

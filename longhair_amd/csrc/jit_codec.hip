@@ -217,6 +217,72 @@ struct lh_unroll_encode<LH_K> {
     __device__ __forceinline__ static void run(lh_word (&)[LH_M][8], lh_word (&)[LH_PF][8], const unsigned char *) {}
 };
 
+// LH_PAIR = 1: columns combined two at a time, so the odd terms left by one column's
+// XOR3 pairing pair up with the next column's (row 0 of the generator is all ones: its
+// eight single terms per column halve).  Needs LH_PF >= 2.
+#ifndef LH_PAIR
+#define LH_PAIR 0
+#endif
+template <unsigned S0, unsigned S1, int B = 0, int P = -1>
+struct lh_net2 {
+    __device__ __forceinline__ static void run(lh_word &a, const lh_word (&d0)[8], const lh_word (&d1)[8]) {
+        constexpr unsigned S = S0 | (S1 << 8);
+        if constexpr (B == 16) {
+            if constexpr (P >= 0) lh_xor(a, P < 8 ? d0[P & 7] : d1[P & 7]);
+        } else if constexpr (((S >> B) & 1u) == 0) {
+            lh_net2<S0, S1, B + 1, P>::run(a, d0, d1);
+        } else if constexpr (P < 0) {
+            lh_net2<S0, S1, B + 1, B>::run(a, d0, d1);
+        } else {
+            lh_xor2(a, P < 8 ? d0[P & 7] : d1[P & 7], B < 8 ? d0[B & 7] : d1[B & 7]);
+            lh_net2<S0, S1, B + 1, -1>::run(a, d0, d1);
+        }
+    }
+};
+template <int X, int I = 0>
+struct lh_col_net2 {
+    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], const lh_word (&d0)[8], const lh_word (&d1)[8]) {
+        if constexpr (I < LH_M * 8) {
+            lh_net2<LH_BM[I / 8][X][I % 8], LH_BM[I / 8][X + 1][I % 8]>::run(acc[I / 8][I % 8], d0, d1);
+            lh_col_net2<X, I + 1>::run(acc, d0, d1);
+        }
+    }
+};
+template <int X>
+struct lh_unroll_encode2 {
+    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], lh_word (&ring)[LH_PF][8],
+                                               const unsigned char *base) {
+        if constexpr (X + 1 >= LH_K) {
+            lh_unroll_encode<X>::run(acc, ring, base);  // odd column count: last one alone
+        } else {
+            lh_word n0[8], n1[8];
+            if constexpr (X + LH_PF < LH_K) {
+#pragma unroll
+                for (int b = 0; b < 8; ++b) n0[b] = lh_load(base + (long long)(X + LH_PF) * LH_BYTES + b * LH_SUB);
+            }
+            if constexpr (X + 1 + LH_PF < LH_K) {
+#pragma unroll
+                for (int b = 0; b < 8; ++b) n1[b] = lh_load(base + (long long)(X + 1 + LH_PF) * LH_BYTES + b * LH_SUB);
+            }
+            lh_col_net2<X>::run(acc, ring[X % LH_PF], ring[(X + 1) % LH_PF]);
+            lh_opaque(acc);
+            if constexpr (X + LH_PF < LH_K) {
+#pragma unroll
+                for (int b = 0; b < 8; ++b) ring[X % LH_PF][b] = n0[b];
+            }
+            if constexpr (X + 1 + LH_PF < LH_K) {
+#pragma unroll
+                for (int b = 0; b < 8; ++b) ring[(X + 1) % LH_PF][b] = n1[b];
+            }
+            lh_unroll_encode2<X + 2>::run(acc, ring, base);
+        }
+    }
+};
+template <>
+struct lh_unroll_encode2<LH_K> {
+    __device__ __forceinline__ static void run(lh_word (&)[LH_M][8], lh_word (&)[LH_PF][8], const unsigned char *) {}
+};
+
 __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned char *__restrict__ in,
                                                long long in_stride, unsigned char *__restrict__ out,
                                                long long out_stride, int stripes) {
@@ -236,7 +302,11 @@ __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned ch
         if (q < LH_K)
 #pragma unroll
             for (int b = 0; b < 8; ++b) ring[q][b] = lh_load(base + (long long)q * LH_BYTES + b * LH_SUB);
+#if LH_PAIR && LH_PF >= 2
+    lh_unroll_encode2<0>::run(acc, ring, base);
+#else
     lh_unroll_encode<0>::run(acc, ring, base);
+#endif
     unsigned char *o = out + l.stripe * out_stride + l.p;
 #pragma unroll
     for (int r = 0; r < LH_M; ++r)
@@ -531,6 +601,9 @@ __device__ __forceinline__ const unsigned char *lh_slot_ptr(unsigned int slot, c
 #ifndef LH_PF_DEC
 #define LH_PF_DEC 1  // decode prefetch depth (tools/tune.py, fused plan: 1 > 2 > 3)
 #endif
+#ifndef LH_PREP_FIRST
+#define LH_PREP_FIRST 0  // fused decode: solve the plan before (1) or while (0) the first columns load
+#endif
 
 template <int X>
 __device__ __forceinline__ const unsigned char *lh_dcol_src(const unsigned int (&srcw)[LH_NSRC],
@@ -607,6 +680,9 @@ __device__ __forceinline__ void lh_decode_body(const lh_lane &l, unsigned char *
 #pragma unroll
             for (int i = 0; i < LH_NW; ++i) v[r][y].v[i] = 0;
     {
+#if LH_PREP_FIRST
+        prep(pr);  // solve before the first loads: the ring is not live across the solve
+#endif
         lh_word ring[LH_PF_DEC][8];
 #pragma unroll
         for (int q = 0; q < LH_PF_DEC; ++q) {
@@ -617,7 +693,9 @@ __device__ __forceinline__ void lh_decode_body(const lh_lane &l, unsigned char *
 #pragma unroll
             for (int b = 0; b < 8; ++b) ring[q][b] = lh_load(src + b * LH_SUB);
         }
+#if !LH_PREP_FIRST
         prep(pr);
+#endif
         lh_unroll_decode<0>::run(v, ring, base, zero, pr.srcw, pr.recw);
     }
     const int e = pr.e;

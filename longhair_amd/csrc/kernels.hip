@@ -289,13 +289,12 @@ __global__ void __launch_bounds__(64) lh_plan_kernel(lh::PlanArgs a) {
         const int i = lane + 64 * h;
         if (i >= e) continue;
         const uint8_t *grow = a.G + rcv_row[i] * k;
-        for (int j0 = 0; j0 < e; j0 += 8) {  // 8 independent gathers in flight
+        for (int j0 = 0; j0 < e; j0 += 8) {  // 8 independent gathers in flight, no branches
             uint8_t v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = (j0 + u < e) ? grow[erasure[j0 + u]] : (uint8_t)0;
+            for (int u = 0; u < 8; ++u) v[u] = grow[erasure[min(j0 + u, e - 1)]];
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (j0 + u < e) aug[(j0 + u) * RC + i] = v[u];
+            for (int u = 0; u < 8; ++u) aug[min(j0 + u, e - 1) * RC + i] = v[u];  // clamped: same value
         }
         for (int j = 0; j < e; ++j) aug[(e + j) * RC + i] = (uint8_t)(j == i);
     }
@@ -332,16 +331,22 @@ __global__ void __launch_bounds__(64) lh_plan_kernel(lh::PlanArgs a) {
             const uint32_t f = aug[c * RC + i];
             if (!f) continue;
             const int lf = glog[f];
-            for (int j0 = c; j0 < w2; j0 += 8) {  // 8 independent updates per step (LDS latency)
+            // 8 independent updates per step and no branches, so the LDS latencies overlap
+            // (indices past the row are clamped to its last column: same value rewritten).
+            for (int j0 = c; j0 < w2; j0 += 8) {
                 int pl[8];
-                uint32_t av[8];
+                uint32_t av[8], gv[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) pl[u] = (j0 + u < w2) ? plog[j0 + u] : -1;
+                for (int u = 0; u < 8; ++u) {
+                    const int j = min(j0 + u, w2 - 1);
+                    pl[u] = plog[j];
+                    av[u] = aug[j * RC + i];
+                }
 #pragma unroll
-                for (int u = 0; u < 8; ++u) av[u] = (pl[u] >= 0) ? aug[(j0 + u) * RC + i] : 0u;
+                for (int u = 0; u < 8; ++u) gv[u] = gexp[lf + max(pl[u], 0)];
 #pragma unroll
                 for (int u = 0; u < 8; ++u)
-                    if (pl[u] >= 0) aug[(j0 + u) * RC + i] = (uint8_t)(av[u] ^ gexp[lf + pl[u]]);
+                    aug[min(j0 + u, w2 - 1) * RC + i] = (uint8_t)(av[u] ^ (pl[u] >= 0 ? gv[u] : 0u));
             }
         }
         __syncthreads();

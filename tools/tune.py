@@ -19,11 +19,9 @@ import longhair_amd as lh  # noqa: E402
 
 VARIANTS = [
     ("base", {}),
-    ("enclb4", {"LONGHAIR_AMD_JIT_DEFINES": "LH_ENC_LB=4"}),
-    ("enclb4pf2", {"LONGHAIR_AMD_JIT_DEFINES": "LH_ENC_LB=4,LH_PF=2"}),
-    ("declb3", {"LONGHAIR_AMD_JIT_DEFINES": "LH_DEC_LB=3"}),
-    ("nofused", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1"}),
-    ("nofused_pfd2", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1", "LONGHAIR_AMD_JIT_DEFINES": "LH_PF_DEC=2"}),
+    ("prepfirst", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PREP_FIRST=1"}),
+    ("nf_pf2_lb3", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1", "LONGHAIR_AMD_JIT_DEFINES": "LH_PREP_FIRST=1,LH_PF_DEC=2,LH_DEC_LB=3"}),
+    ("nf_pf3", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1", "LONGHAIR_AMD_JIT_DEFINES": "LH_PREP_FIRST=1,LH_PF_DEC=3"}),
 ]
 KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID", "LONGHAIR_AMD_NO_FUSED_PLAN"]
 
