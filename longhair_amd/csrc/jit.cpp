@@ -101,10 +101,15 @@ bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
     cfg->spw = 0;
     cfg->wps = (cfg->nch + 63) / 64;
     cfg->win = decode ? 2 : 1;
-    cfg->rows_per_wave = 8;
+    // Rows per wave: 16 for encode (half the redundant column loads and nibble tables of
+    // 8: k128/m32 encode 4.21 -> 3.00 ms); 8 for the fused decode, whose V tile in LDS
+    // (m x 2 KiB per workgroup) caps the workgroups per CU, so it needs more waves each.
+    cfg->rows_per_wave = decode ? 8 : 16;
     if (const char *r = std::getenv("LONGHAIR_AMD_WIN_ROWS")) cfg->rows_per_wave = std::atoi(r);
     cfg->win_pf = 3;
     if (const char *f = std::getenv("LONGHAIR_AMD_WIN_PF")) cfg->win_pf = std::max(1, std::atoi(f));
+    cfg->win_lds = 1;
+    if (const char *l = std::getenv("LONGHAIR_AMD_WIN_LDS")) cfg->win_lds = std::atoi(l) ? 1 : 0;
     if ((m + cfg->rows_per_wave - 1) / cfg->rows_per_wave > 16) return false;  // <= 1024 threads
     if (decode && m > 64) return false;  // the fused decode keeps m x 2 KiB of V in LDS
     cfg->defines.clear();
@@ -127,21 +132,62 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
         else e << "(base + " << (long long)x * c.bytes << "LL)";
         return e.str();
     };
+    // LDS staging (c.win_lds): the workgroup's 8 x 256-byte column tile is fetched once by
+    // LDS-DMA (global_load_lds_dwordx4, 16 B per lane; waves 0 and 1 each move one 1-KiB
+    // half, or wave 0 both when the group has one wave) into a ring of D = PF + 1 tiles,
+    // PF columns ahead; per column every wave waits for its own DMA (counted vmcnt), meets
+    // the others at s_barrier, issues the DMA of column x + PF into the tile of column
+    // x - 1 (read by every wave before the barrier) and reads its 8 dwords from LDS.  Each
+    // column crosses HBM once per workgroup, at 16 B per lane, instead of once per wave at
+    // 4 B per lane (a 4-byte-lane stream reads at 4.1 TB/s against 6.3 for 16-byte lanes).
+    const bool lds = c.win_lds != 0;
+    const int NG = (m + R - 1) / R, D = PF + 1;
+    const int ndma = NG == 1 ? 2 : (g < 2 ? 1 : 0);  // DMA instructions per column, this wave
     os << "__device__ __forceinline__ void lh_wg" << g << "(const unsigned char *__restrict__ base, "
        << (elim ? "const unsigned char *__restrict__ zero, const unsigned int (&slv)[LH_NQ], unsigned int *__restrict__ lv"
                 : "unsigned char *__restrict__ o")
+       << (lds ? ", const unsigned char *__restrict__ sb, const unsigned char *__restrict__ zb" : "")
        << ") {\n";
     for (int r = r0; r < r1; ++r)
         for (int y = 0; y < 8; ++y) os << "  unsigned int a" << (r - r0) << "_" << y << " = 0;\n";
-    for (int q = 0; q < PF && q < k; ++q) {
-        os << "  const unsigned char *c" << q << " = " << col(q) << ";\n";
-        for (int b = 0; b < 8; ++b)
-            os << "  unsigned int d" << q << "_" << b << " = lh_ld(c" << q << " + " << b * c.sub << ");\n";
+    auto dcol = [&](int x) {  // uniform base of column x for the DMA (stripe + chunk, or zero page)
+        std::ostringstream e;
+        if (elim) e << "lh_slot(slv, " << x << ", sb, zb)";
+        else e << "(sb + " << (long long)x * c.bytes << "LL)";
+        return e.str();
+    };
+    auto dma = [&](int x, const char *ind) {
+        for (int h = 0; h < 2; ++h) {
+            if (!(NG == 1 || g == h)) continue;
+            os << ind << "lh_dma(" << dcol(x) << " + dof" << h << ", tile" << x % D << " + " << h * 1024 << ");\n";
+        }
+    };
+    if (lds) {
+        os << "  const int lane = threadIdx.x & 63;\n";
+        for (int h = 0; h < 2; ++h)
+            if (NG == 1 || g == h)
+                os << "  const unsigned int dof" << h << " = ((" << 64 * h << " + lane) >> 4) * " << c.sub
+                   << "u + ((lane & 15) << 4);\n";
+        for (int q = 0; q < PF && q < k; ++q) dma(q, "  ");
+    } else {
+        for (int q = 0; q < PF && q < k; ++q) {
+            os << "  const unsigned char *c" << q << " = " << col(q) << ";\n";
+            for (int b = 0; b < 8; ++b)
+                os << "  unsigned int d" << q << "_" << b << " = lh_ld(c" << q << " + " << b * c.sub << ");\n";
+        }
     }
     for (int x = 0; x < k; ++x) {
-        const int slot = x % PF;
+        const int slot = lds ? 0 : x % PF;
         os << "  {\n";
-        if (x + PF < k) {
+        if (lds) {
+            const int ahead = std::min(PF - 1, k - 1 - x);  // this wave's DMAs issued after column x
+            if (ndma) os << "    lh_wait_vm(" << ndma * ahead << ");\n";
+            os << "    __builtin_amdgcn_s_barrier();\n";
+            if (x + PF < k) dma(x + PF, "    ");
+            for (int b = 0; b < 8; ++b)
+                os << "    const unsigned int d0_" << b << " = ((const unsigned int *)(tile" << x % D << " + " << b * 256
+                   << "))[lane];\n";
+        } else if (x + PF < k) {
             os << "    const unsigned char *cn = " << col(x + PF) << ";\n";
             for (int b = 0; b < 8; ++b)
                 os << "    const unsigned int n" << b << " = lh_ld(cn + " << b * c.sub << ");\n";
@@ -181,7 +227,7 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
             }
         }
         os << "    LH_PIN" << (r1 - r0) << ";\n";
-        if (x + PF < k)
+        if (!lds && x + PF < k)
             for (int b = 0; b < 8; ++b) os << "    d" << slot << "_" << b << " = n" << b << ";\n";
         os << "  }\n";
     }
@@ -219,33 +265,43 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
        << "  const unsigned int s = (unsigned int)__builtin_amdgcn_readlane((int)slv[i / 64], i % 64);\n"
        << "  return s == 0xFFu ? zero : base + (long long)s * " << c.bytes << ";\n}\n";
     for (int g = 0; g < NG; ++g) emit_win_group(os, c, G, g);
+    // Phase B: coefficients are workgroup-uniform, so each coefficient bit is a scalar
+    // branch and only set bits cost XORs; V_r is doubled in place (B(2) in bit-sliced
+    // form: (v1..v7, v0^v1^v2^v7)).  (A nibble-windowed variant -- a 16-way uniform switch
+    // per output and nibble with XOR3-paired cases -- measured 1.2-1.3x slower.)
+    os << "#ifndef LH_PB_MASK  // masks: k128/m32 decode 7.0 ms against 6.5 ms with branches\n#define LH_PB_MASK 0\n#endif\n";
     os << "__device__ __forceinline__ void lh_phase_b(const int g, const int e, const int lane,\n"
        << "    const unsigned int *__restrict__ lv, const unsigned char *__restrict__ cf,\n"
        << "    const unsigned char *__restrict__ used, const int nu, const unsigned char *__restrict__ pl,\n"
        << "    unsigned char *__restrict__ base) {\n"
-       << "  const int i0 = g * 8;\n"
-       << "  if (i0 >= e) return;\n"
-       << "  unsigned int acc[8][8];\n"
-       << "#pragma unroll\n  for (int i = 0; i < 8; ++i)\n#pragma unroll\n    for (int y = 0; y < 8; ++y) acc[i][y] = 0;\n"
-       << "  for (int j = 0; j < nu; ++j) {\n"
-       << "    const int r = __builtin_amdgcn_readfirstlane(used[j]);\n"
-       << "    unsigned int v[8], cs[8];\n"
-       << "#pragma unroll\n    for (int y = 0; y < 8; ++y) v[y] = lv[(r * 8 + y) * 64 + lane];\n"
-       << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n"
-       << "      cs[i] = __builtin_amdgcn_readfirstlane(i0 + i < e ? (unsigned int)cf[(i0 + i) * " << c.m << " + r] : 0u);\n"
-       << "#pragma unroll\n    for (int t = 0; t < 8; ++t) {\n"
+       << "  for (int i0 = g * 8; i0 < e; i0 += " << 8 * NG << ") {  // outputs [i0, i0 + 8) of this wave\n"
+       << "    unsigned int acc[8][8];\n"
+       << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n#pragma unroll\n      for (int y = 0; y < 8; ++y) acc[i][y] = 0;\n"
+       << "    for (int j = 0; j < nu; ++j) {\n"
+       << "      const int r = __builtin_amdgcn_readfirstlane(used[j]);\n"
+       << "      unsigned int v[8], cs[8];\n"
+       << "#pragma unroll\n      for (int y = 0; y < 8; ++y) v[y] = lv[(r * 8 + y) * 64 + lane];\n"
        << "#pragma unroll\n      for (int i = 0; i < 8; ++i)\n"
-       << "        if ((cs[i] >> t) & 1u)\n"
-       << "#pragma unroll\n          for (int y = 0; y < 8; ++y) acc[i][y] ^= v[y];\n"
-       << "      if (t < 7) {\n"
-       << "        const unsigned int t7 = __builtin_amdgcn_bitop3_b32(v[0], v[1], v[2], 0x96) ^ v[7];\n"
-       << "#pragma unroll\n        for (int y = 0; y < 7; ++y) v[y] = v[y + 1];\n"
-       << "        v[7] = t7;\n      }\n    }\n  }\n"
-       << "#pragma unroll\n  for (int i = 0; i < 8; ++i)\n"
-       << "    if (i0 + i < e) {\n"
-       << "      unsigned char *dst = base + (long long)pl[16 + i0 + i] * " << c.bytes << ";\n"
-       << "#pragma unroll\n      for (int y = 0; y < 8; ++y) lh_st(dst + y * " << c.sub << ", acc[i][y]);\n"
-       << "    }\n}\n";
+       << "        cs[i] = __builtin_amdgcn_readfirstlane(i0 + i < e ? (unsigned int)cf[(i0 + i) * " << c.m
+       << " + r] : 0u);\n"
+       << "#pragma unroll\n      for (int t = 0; t < 8; ++t) {\n"
+       << "#pragma unroll\n        for (int i = 0; i < 8; ++i) {\n"
+       << "#if LH_PB_MASK  // uniform 0 / ~0 mask per (output, bit): one v_bitop3 a ^ (v & m) per sub-row\n"
+       << "          const unsigned int msk = 0u - ((cs[i] >> t) & 1u);\n"
+       << "#pragma unroll\n          for (int y = 0; y < 8; ++y) acc[i][y] = __builtin_amdgcn_bitop3_b32(acc[i][y], v[y], msk, 0x78);\n"
+       << "#else  // scalar branch per (output, bit): only set bits cost XORs\n"
+       << "          if ((cs[i] >> t) & 1u)\n"
+       << "#pragma unroll\n            for (int y = 0; y < 8; ++y) acc[i][y] ^= v[y];\n"
+       << "#endif\n        }\n"
+       << "        if (t < 7) {\n"
+       << "          const unsigned int t7 = __builtin_amdgcn_bitop3_b32(v[0], v[1], v[2], 0x96) ^ v[7];\n"
+       << "#pragma unroll\n          for (int y = 0; y < 7; ++y) v[y] = v[y + 1];\n"
+       << "          v[7] = t7;\n        }\n      }\n    }\n"
+       << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n"
+       << "      if (i0 + i < e) {\n"
+       << "        unsigned char *dst = base + (long long)pl[16 + i0 + i] * " << c.bytes << ";\n"
+       << "#pragma unroll\n        for (int y = 0; y < 8; ++y) lh_st(dst + y * " << c.sub << ", acc[i][y]);\n"
+       << "      }\n  }\n}\n";
     os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
        << "lh_jit_decode_wide(unsigned char *__restrict__ blocks, long long stride,\n"
        << "                   const unsigned char *__restrict__ plan, long long plan_stride,\n"
@@ -276,7 +332,14 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
        << "  const int p = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << " + lane * " << c.W << ";\n"
        << "  unsigned char *b = blocks + stripe * stride + p;\n"
        << "  const unsigned char *z = zero_page + p;\n";
-    for (int g = 0; g < NG; ++g) os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << "(b, z, slv, lv);\n";
+    const char *dargs = "(b, z, slv, lv)";
+    if (c.win_lds) {
+        os << "  const int chunk = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << ";\n"
+           << "  const unsigned char *sb = blocks + stripe * stride + chunk;\n"
+           << "  const unsigned char *zb = zero_page + chunk;\n";
+        dargs = "(b, z, slv, lv, sb, zb)";
+    }
+    for (int g = 0; g < NG; ++g) os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << dargs << ";\n";
     os << "  __syncthreads();\n"
        << "  lh_phase_b(g, e, lane, lv, cf, used, n_used, pl, b);\n"
        << "}\n";
@@ -294,7 +357,17 @@ static std::string win_source_for(const JitConfig &c) {
        << "  unsigned int w; __builtin_memcpy(&w, p, 4); return w;\n#endif\n}\n"
        << "__device__ __forceinline__ void lh_st(unsigned char *p, unsigned int v) {\n"
        << "#if LH_NT\n  __builtin_nontemporal_store(v, (unsigned int *)p);\n#else\n"
-       << "  __builtin_memcpy(p, &v, 4);\n#endif\n}\n";
+       << "  __builtin_memcpy(p, &v, 4);\n#endif\n}\n"
+       << "__device__ __forceinline__ void lh_dma(const unsigned char *src, unsigned char *lds) {  // 16 B per lane\n"
+       << "  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)src,\n"
+       << "                                   (__attribute__((address_space(3))) void *)lds, 16, 0, LH_NT ? 2 : 0);\n}\n"
+       << "// s_waitcnt vmcnt(N) with expcnt / lgkmcnt untouched (gfx9 encoding)\n"
+       << "#define lh_wait_vm(N) __builtin_amdgcn_s_waitcnt(((N) & 15) | (((N) >> 4) << 14) | (7 << 4) | (15 << 8))\n";
+    // One __shared__ object per LDS ring slot: the compiler's LDS-DMA wait tracking tells
+    // distinct objects apart, so reading tile x % D does not wait for the DMA into another.
+    if (c.win_lds)
+        for (int q = 0; q <= c.win_pf; ++q)
+            os << "__shared__ __attribute__((aligned(16))) unsigned char tile" << q << "[2048];\n";
     // LH_PINn: keep the accumulators in registers between columns (no re-association).
     for (int n = 1; n <= R; ++n) {
         os << "#define LH_PIN" << n << " do {";
@@ -317,7 +390,13 @@ static std::string win_source_for(const JitConfig &c) {
        << c.W << ";\n"
        << "  const unsigned char *b = in + stripe * in_stride + p;\n"
        << "  unsigned char *o = out + stripe * out_stride + p;\n";
-    for (int g = 0; g < NG; ++g) os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << "(b, o);\n";
+    const char *eargs = "(b, o)";
+    if (c.win_lds) {
+        os << "  const unsigned char *sb = in + stripe * in_stride + (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W
+           << ";\n";
+        eargs = "(b, o, sb, nullptr)";
+    }
+    for (int g = 0; g < NG; ++g) os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << eargs << ";\n";
     os << "}\n";
     return os.str();
 }
@@ -380,7 +459,7 @@ std::string jit_source_for(const JitConfig &c) {
 
 const JitKernels *JitCache::peek(const JitConfig &cfg) {
     std::lock_guard<std::mutex> g(mu_);
-    auto it = cache_.find(Key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines, cfg.win * 100000 + cfg.rows_per_wave * 100 + cfg.win_pf));
+    auto it = cache_.find(Key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines, cfg.win * 100000 + cfg.win_lds * 10000 + cfg.rows_per_wave * 100 + cfg.win_pf));
     return it == cache_.end() ? nullptr : &it->second;
 }
 
@@ -475,7 +554,7 @@ bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::str
 
 const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err) {
     std::lock_guard<std::mutex> g(mu_);
-    const Key key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines, cfg.win * 100000 + cfg.rows_per_wave * 100 + cfg.win_pf);
+    const Key key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines, cfg.win * 100000 + cfg.win_lds * 10000 + cfg.rows_per_wave * 100 + cfg.win_pf);
     auto it = cache_.find(key);
     if (it != cache_.end()) return &it->second;
 

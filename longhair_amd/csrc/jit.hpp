@@ -22,6 +22,7 @@ struct JitConfig {
     int win = 0;          // 1: windowed encode module, 2: windowed decode phase-A module
     int rows_per_wave = 8;
     int win_pf = 3;       // windowed modules: columns in flight ahead of the one combined
+    int win_lds = 1;      // windowed modules: stage column tiles in LDS by LDS-DMA (0: per-wave loads)
     int lanes_per_launch_unit() const { return 64; }
 };
 

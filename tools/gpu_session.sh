@@ -23,5 +23,12 @@ for cfg in k29m4 ${CONFIGS:-k128m32 k200m56}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$cfg" -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --cpu-baseline off > "$OUT/prof_$cfg.log" 2>&1 || { tail -20 "$OUT/prof_$cfg.log"; exit 1; }
   find "$OUT/prof_$cfg" -name "*kernel_stats.csv" -exec grep -E "lh_" {} \; | cut -c1-160
 done
+for cfg in k29m4 ${CONFIGS:-k128m32 k200m56}; do
+  mkdir -p "$OUT/pmc_$cfg"
+  timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_$cfg/pmc_fetch" -o run --output-format csv -- python3 tools/prof_kernels.py $cfg > "$OUT/pmc_$cfg/fetch.log" 2>&1 || { tail -20 "$OUT/pmc_$cfg/fetch.log"; exit 1; }
+  timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_$cfg/pmc_write" -o run --output-format csv -- python3 tools/prof_kernels.py $cfg > "$OUT/pmc_$cfg/write.log" 2>&1 || { tail -20 "$OUT/pmc_$cfg/write.log"; exit 1; }
+  python3 tools/pmc_summary.py "$OUT/pmc_$cfg" $cfg > "$OUT/pmc_$cfg/summary.json" || exit 1
+  grep -E '"(kernel|ratio_to_algorithmic)"' "$OUT/pmc_$cfg/summary.json"
+done
 timeout -k 10 600 python tools/pcie_bench.py k29m4 k200m56 > "$OUT/pcie.json" 2> "$OUT/pcie.err" || { tail -20 "$OUT/pcie.err"; exit 1; }
 cat "$OUT/pcie.json"

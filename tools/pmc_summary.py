@@ -43,7 +43,7 @@ def main():
                 return name, v
         return None, None
     for role, words in (("encode", ["lh_jit_encode_win", "lh_jit_encode", "lh_apply_generic"]),
-                        ("decode", ["lh_jit_decode_fused", "lh_jit_decode", "lh_jit_elim_win", "lh_apply_generic"])):
+                        ("decode", ["lh_jit_decode_fused", "lh_jit_decode_wide", "lh_jit_decode", "lh_apply_generic"])):
         name, v = pick(words)
         if v:
             res[role] = dict(v, kernel=name, ratio_to_algorithmic=v["hbm_bytes_per_launch"] / alg[role])

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Pre-populate the on-disk code-object cache (longhair_amd/jit_cache/) for the BASELINE
 shapes, without a GPU, so the first GPU run does not pay the hiprtc compile (the large-m
-windowed modules take minutes).  Usage: python tools/precompile.py [k m bytes]..."""
+windowed modules take minutes).  Usage: python tools/precompile.py [--all | k m bytes ...]"""
 import os
 import sys
 import time
@@ -10,11 +10,18 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import longhair_amd as lh  # noqa: E402
 
 DEFAULT = [(29, 4, 1296), (128, 32, 8192), (200, 56, 65536)]
+# Further shapes the GPU parity tests run through the specialised path (tests/test_gpu_parity.py).
+TESTS = [(29, 2, 1296), (29, 3, 1296), (29, 8, 1296), (4, 2, 16), (10, 6, 8), (17, 6, 520), (64, 5, 4096),
+         (3, 250, 24), (250, 3, 24), (2, 2, 8), (29, 4, 1304), (9, 7, 72), (29, 2, 16), (10, 8, 24),
+         (128, 32, 1024), (5, 3, 8)]
 
 
 def main():
-    args = [int(a) for a in sys.argv[1:]]
-    shapes = [tuple(args[i:i + 3]) for i in range(0, len(args), 3)] or DEFAULT
+    if sys.argv[1:] == ["--all"]:
+        shapes = DEFAULT + TESTS
+    else:
+        args = [int(a) for a in sys.argv[1:]]
+        shapes = [tuple(args[i:i + 3]) for i in range(0, len(args), 3)] or DEFAULT
     for k, m, b in shapes:
         t0 = time.time()
         rc = lh.lib().cauchy_256_jit_precompile(k, m, b)

@@ -23,11 +23,20 @@ VARIANTS = [
     ("nf_pf2_lb3", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1", "LONGHAIR_AMD_JIT_DEFINES": "LH_PREP_FIRST=1,LH_PF_DEC=2,LH_DEC_LB=3"}),
     ("nf_pf3", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1", "LONGHAIR_AMD_JIT_DEFINES": "LH_PREP_FIRST=1,LH_PF_DEC=3"}),
 ]
-KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID", "LONGHAIR_AMD_NO_FUSED_PLAN"]
+KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID", "LONGHAIR_AMD_NO_FUSED_PLAN",
+         "LONGHAIR_AMD_WIN_ROWS", "LONGHAIR_AMD_WIN_PF", "LONGHAIR_AMD_WIN_LDS"]
+# Large-m (windowed) variants: rows per wave and columns in flight.
+VARIANTS_WIN = [
+    ("base", {}),
+    ("pb_branch", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PB_MASK=0"}),
+]
 
 
 def main():
+    global VARIANTS
     k, m, nbytes, stripes = (int(a) for a in sys.argv[1:5]) if len(sys.argv) >= 5 else (29, 4, 1296, 65536)
+    if m > 12:
+        VARIANTS = VARIANTS_WIN
     torch.cuda.set_device(0)
     assert lh.cauchy_256_init() == 0
     X, D, rows0, _ = bench.make_workload(k, m, nbytes, stripes, seed=7)
@@ -36,7 +45,7 @@ def main():
     rows = rows0.clone()
     ref_rec = None
     results = {name: ([], []) for name, _ in VARIANTS}
-    reps = 10
+    reps = 3 if m > 12 else 10
     for rnd in range(3):
         for name, env in VARIANTS:
             for key in KNOBS:

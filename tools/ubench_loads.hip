@@ -18,6 +18,22 @@ __global__ void stream_read(const u32x4* __restrict__ in, u32x4* __restrict__ ou
   out[t] = acc;
 }
 
+// FETCH_SIZE calibration: the same aligned stream read with 4- and 8-byte lanes.
+__global__ void stream_read4(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, size_t n) {
+  size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * blockDim.x;
+  uint32_t acc = 0;
+  for (size_t i = t; i < n; i += stride) acc ^= in[i];
+  out[t] = acc;
+}
+__global__ void stream_read8(const u32x2* __restrict__ in, u32x2* __restrict__ out, size_t n) {
+  size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * blockDim.x;
+  u32x2 acc = {0, 0};
+  for (size_t i = t; i < n; i += stride) acc ^= in[i];
+  out[t] = acc;
+}
+
 template <int W> struct Word;
 template <> struct Word<2> { typedef uint16_t T; };
 template <> struct Word<4> { typedef uint32_t T; };
@@ -87,6 +103,8 @@ int main() {
     char nm[64]; snprintf(nm, 64, "stream dwordx4 grid=%d", grid);
     timeit(nm, (double)in_bytes, [&] { stream_read<<<grid, 256>>>((const u32x4*)din, (u32x4*)dout, n16); });
   }
+  timeit("stream dword grid=2048", (double)in_bytes, [&] { stream_read4<<<2048, 256>>>((const uint32_t*)din, (uint32_t*)dout, in_bytes / 4); });
+  timeit("stream dwordx2 grid=2048", (double)in_bytes, [&] { stream_read8<<<2048, 256>>>((const u32x2*)din, (u32x2*)dout, in_bytes / 8); });
 #define PAT(W) { int nch = (bytes/8 + W - 1)/W; long thr = (long)stripes * nch; int grid = (int)((thr + 255)/256); \
     timeit("pattern W=" #W, (double)in_bytes, [&]{ stripe_pattern<W><<<grid,256>>>(din, dout, stripes, k, bytes); }); }
   PAT(2) PAT(4) PAT(8) PAT(16)
