@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--config", default="k29m4", choices=sorted(CONFIGS))
     ap.add_argument("--stripes", type=int, default=0, help="override stripes per GPU")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU work for the baseline")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU work (thread-seconds) for the baseline")
     return ap.parse_args()
 
 

@@ -270,27 +270,44 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
     // form: (v1..v7, v0^v1^v2^v7)).  (A nibble-windowed variant -- a 16-way uniform switch
     // per output and nibble with XOR3-paired cases -- measured 1.2-1.3x slower.)
     os << "#ifndef LH_PB_MASK  // masks: k128/m32 decode 7.0 ms against 6.5 ms with branches\n#define LH_PB_MASK 0\n#endif\n";
+    // The coefficients of the wave's 8 outputs for used row j sit packed in lane j
+    // (cpk0: outputs 0..3, cpk1: 4..7) and come back as SGPRs through v_readlane, and the
+    // next row's V is read from LDS while the current row is applied, so no LDS round
+    // trip sits between a row's coefficient bits and their branches.
     os << "__device__ __forceinline__ void lh_phase_b(const int g, const int e, const int lane,\n"
        << "    const unsigned int *__restrict__ lv, const unsigned char *__restrict__ cf,\n"
        << "    const unsigned char *__restrict__ used, const int nu, const unsigned char *__restrict__ pl,\n"
        << "    unsigned char *__restrict__ base) {\n"
+       << "  const unsigned int ur = lane < nu ? (unsigned int)used[lane] : 0u;  // row of used slot `lane`\n"
        << "  for (int i0 = g * 8; i0 < e; i0 += " << 8 * NG << ") {  // outputs [i0, i0 + 8) of this wave\n"
+       << "    unsigned int cpk0 = 0, cpk1 = 0;\n"
+       << "    if (lane < nu) {\n"
+       << "#pragma unroll\n      for (int i = 0; i < 4; ++i) {\n"
+       << "        cpk0 |= (i0 + i < e ? (unsigned int)cf[(i0 + i) * " << c.m << " + ur] : 0u) << (8 * i);\n"
+       << "        cpk1 |= (i0 + 4 + i < e ? (unsigned int)cf[(i0 + 4 + i) * " << c.m << " + ur] : 0u) << (8 * i);\n"
+       << "      }\n    }\n"
        << "    unsigned int acc[8][8];\n"
        << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n#pragma unroll\n      for (int y = 0; y < 8; ++y) acc[i][y] = 0;\n"
+       << "    unsigned int v[8], vn[8];\n"
+       << "    {\n      const int r = __builtin_amdgcn_readlane((int)ur, 0);\n"
+       << "#pragma unroll\n      for (int y = 0; y < 8; ++y) vn[y] = lv[(r * 8 + y) * 64 + lane];\n    }\n"
        << "    for (int j = 0; j < nu; ++j) {\n"
-       << "      const int r = __builtin_amdgcn_readfirstlane(used[j]);\n"
-       << "      unsigned int v[8], cs[8];\n"
-       << "#pragma unroll\n      for (int y = 0; y < 8; ++y) v[y] = lv[(r * 8 + y) * 64 + lane];\n"
-       << "#pragma unroll\n      for (int i = 0; i < 8; ++i)\n"
-       << "        cs[i] = __builtin_amdgcn_readfirstlane(i0 + i < e ? (unsigned int)cf[(i0 + i) * " << c.m
-       << " + r] : 0u);\n"
+       << "#pragma unroll\n      for (int y = 0; y < 8; ++y) v[y] = vn[y];\n"
+       << "      if (j + 1 < nu) {  // next row's V in flight\n"
+       << "        const int rn = __builtin_amdgcn_readlane((int)ur, j + 1);\n"
+       << "#pragma unroll\n        for (int y = 0; y < 8; ++y) vn[y] = lv[(rn * 8 + y) * 64 + lane];\n"
+       << "      }\n"
+       << "      const unsigned int c0 = (unsigned int)__builtin_amdgcn_readlane((int)cpk0, j);\n"
+       << "      const unsigned int c1 = (unsigned int)__builtin_amdgcn_readlane((int)cpk1, j);\n"
        << "#pragma unroll\n      for (int t = 0; t < 8; ++t) {\n"
        << "#pragma unroll\n        for (int i = 0; i < 8; ++i) {\n"
+       << "          const unsigned int bit = ((i < 4 ? c0 : c1) >> (8 * (i & 3) + t)) & 1u;\n"
        << "#if LH_PB_MASK  // uniform 0 / ~0 mask per (output, bit): one v_bitop3 a ^ (v & m) per sub-row\n"
-       << "          const unsigned int msk = 0u - ((cs[i] >> t) & 1u);\n"
+       << "          const unsigned int msk = 0u - bit;\n"
        << "#pragma unroll\n          for (int y = 0; y < 8; ++y) acc[i][y] = __builtin_amdgcn_bitop3_b32(acc[i][y], v[y], msk, 0x78);\n"
-       << "#else  // scalar branch per (output, bit): only set bits cost XORs\n"
-       << "          if ((cs[i] >> t) & 1u)\n"
+       << "#else  // scalar branch per (output, bit): only set bits cost XORs; the XORs stay on the\n"
+       << "       // fall-through path (a clear bit costs one taken branch, a set bit none)\n"
+       << "          if (__builtin_expect(bit, 1))\n"
        << "#pragma unroll\n            for (int y = 0; y < 8; ++y) acc[i][y] ^= v[y];\n"
        << "#endif\n        }\n"
        << "        if (t < 7) {\n"
@@ -341,7 +358,9 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
     }
     for (int g = 0; g < NG; ++g) os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << dargs << ";\n";
     os << "  __syncthreads();\n"
+       << "#ifndef LH_PB_SKIP  // timing probe only (tools/time_probe.py): phase A alone\n"
        << "  lh_phase_b(g, e, lane, lv, cf, used, n_used, pl, b);\n"
+       << "#endif\n"
        << "}\n";
 }
 

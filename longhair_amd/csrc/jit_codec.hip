@@ -69,14 +69,17 @@ __device__ __forceinline__ lh_word lh_load(const unsigned char *p) {
     return w;
 }
 
+#ifndef LH_NT_ST
+#define LH_NT_ST LH_NT  // non-temporal stores (tools/tune.py knob, independent of the loads)
+#endif
 __device__ __forceinline__ void lh_store(unsigned char *p, const lh_word &w) {
-#if LH_NT && LH_W == 16
+#if LH_NT_ST && LH_W == 16
     lh_u32x4 v = {w.v[0], w.v[1], w.v[2], w.v[3]};
     __builtin_nontemporal_store(v, (lh_u32x4 *)p);
-#elif LH_NT && LH_W == 8
+#elif LH_NT_ST && LH_W == 8
     lh_u32x2 v = {w.v[0], w.v[1]};
     __builtin_nontemporal_store(v, (lh_u32x2 *)p);
-#elif LH_NT && LH_W == 4
+#elif LH_NT_ST && LH_W == 4
     __builtin_nontemporal_store(w.v[0], (unsigned int *)p);
 #else
     __builtin_memcpy(p, &w.v[0], LH_W);

@@ -191,7 +191,7 @@ __global__ void __launch_bounds__(256) lh_scatter_kernel(lh::ScatterArgs a) {
 }
 
 // -------------------------------------------------------------------- decode plan
-// One 64-lane wave per stripe, every step lane-parallel.
+// One workgroup per stripe (1 or 4 waves), every step lane-parallel.
 //  * Classification (reference sort_blocks, cauchy_256.cpp:538-570): a row -> slot map in
 //    LDS; recovery slots (array order) and missing originals (ascending) are compacted
 //    with wave ballots and prefix popcounts.
@@ -201,9 +201,10 @@ __global__ void __launch_bounds__(256) lh_scatter_kernel(lh::ScatterArgs a) {
 //    entry (one ballot).  [A | I] reduces to [P | M] with row p_c of the permutation P
 //    holding the 1 of column c, so A^-1[c][:] = M[p_c][:].
 // LDS: GF tables, maps, and 2 e_max x RC bytes (RC = 64 or 128 rows).
-__global__ void __launch_bounds__(64) lh_plan_kernel(lh::PlanArgs a) {
+__global__ void __launch_bounds__(256) lh_plan_kernel(lh::PlanArgs a) {
     const int s = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, nth = blockDim.x;
+    const int lane = tid & 63, wv = tid >> 6, NW = nth >> 6;
     const int k = a.k, m = a.m, e_max = a.e_max;
     const int RC = e_max > 64 ? 128 : 64;  // row capacity of the augmented matrix
     __shared__ uint8_t gexp[512];
@@ -215,14 +216,14 @@ __global__ void __launch_bounds__(64) lh_plan_kernel(lh::PlanArgs a) {
     __shared__ int16_t plog[256];     // normalised pivot row in log form, -1 = zero
     extern __shared__ uint8_t aug[];  // element (i, j) at aug[j * RC + i], j < 2 e_max
 
-    for (int i = lane; i < 256; i += 64) {
+    for (int i = tid; i < 256; i += nth) {
         gexp[i] = a.gf_exp[i];
         gexp[i + 256] = a.gf_exp[i + 256];
         glog[i] = a.gf_log[i];
         slot_of[i] = 0xFF;
     }
     uint8_t *rws = a.rows + (long long)s * k;
-    for (int i = lane; i < k; i += 64) rows[i] = rws[i];
+    for (int i = tid; i < k; i += nth) rows[i] = rws[i];
     __syncthreads();
 
     uint8_t *rec = a.plan + (long long)s * a.plan_stride;
@@ -260,20 +261,20 @@ __global__ void __launch_bounds__(64) lh_plan_kernel(lh::PlanArgs a) {
     }
     __syncthreads();
     const int e = (status != 0 || k <= 1) ? 0 : (m == 1 ? 1 : n_rcv);
-    if (lane == 0) {
+    if (tid == 0) {
         rec[0] = (uint8_t)e;
         rec[1] = (uint8_t)(int8_t)status;
         if (a.status) a.status[s] = (int8_t)status;
     }
     if (status != 0) return;
     if (k <= 1) {  // cauchy_256.cpp:1252-1256
-        if (lane == 0 && k == 1) rws[0] = 0;
+        if (tid == 0 && k == 1) rws[0] = 0;
         return;
     }
     if (m == 1) {
         // cauchy_decode_m1 (:487-535): the last recovery slot (or slot 0 when none is
         // present) becomes the XOR of all k blocks and takes the first missing row.
-        if (lane == 0) {
+        if (tid == 0) {
             const int out = n_rcv ? rcv_slot[n_rcv - 1] : 0;
             pv.set_out_slot(0, (uint8_t)out);
             if (n_miss) rws[out] = erasure[0];
@@ -289,14 +290,14 @@ __global__ void __launch_bounds__(64) lh_plan_kernel(lh::PlanArgs a) {
         const int i = lane + 64 * h;
         if (i >= e) continue;
         const uint8_t *grow = a.G + rcv_row[i] * k;
-        for (int j0 = 0; j0 < e; j0 += 8) {  // 8 independent gathers in flight, no branches
+        for (int j0 = 8 * wv; j0 < e; j0 += 8 * NW) {  // 8 independent gathers in flight, no branches
             uint8_t v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) v[u] = grow[erasure[min(j0 + u, e - 1)]];
 #pragma unroll
             for (int u = 0; u < 8; ++u) aug[min(j0 + u, e - 1) * RC + i] = v[u];  // clamped: same value
         }
-        for (int j = 0; j < e; ++j) aug[(e + j) * RC + i] = (uint8_t)(j == i);
+        for (int j = wv; j < e; j += NW) aug[(e + j) * RC + i] = (uint8_t)(j == i);
     }
     __syncthreads();
     bool used0 = false, used1 = false;  // rows lane and lane + 64 are pivots already
@@ -306,34 +307,36 @@ __global__ void __launch_bounds__(64) lh_plan_kernel(lh::PlanArgs a) {
         const bool c1 = RC > 64 && r1 < e && !used1 && aug[c * RC + r1] != 0;
         const unsigned long long b0 = __ballot(c0), b1 = __ballot(c1);
         if (!b0 && !b1) {  // singular: impossible for distinct valid rows (Cauchy MDS)
-            if (lane == 0) { rec[0] = 0; rec[1] = 0xFF; if (a.status) a.status[s] = -1; }
+            if (tid == 0) { rec[0] = 0; rec[1] = 0xFF; if (a.status) a.status[s] = -1; }
             return;
         }
         const int p = b0 ? __builtin_ctzll(b0) : 64 + __builtin_ctzll(b1);
         if (p == lane) used0 = true;
         if (p == r1) used1 = true;
         const int linv = 255 - glog[aug[c * RC + p]];
+        // Factors of this thread's rows, read before any wave touches column c.
+        const uint32_t f0 = (lane < e && lane != p) ? aug[c * RC + lane] : 0u;
+        const uint32_t f1 = (RC > 64 && r1 < e && r1 != p) ? aug[c * RC + r1] : 0u;
         __syncthreads();
         // Normalise the pivot row (its columns < c are zero: earlier pivots cleared them).
-        for (int j = c + lane; j < w2; j += 64) {
+        for (int j = c + tid; j < w2; j += nth) {
             const uint32_t v = aug[j * RC + p];
             const uint32_t nv = v ? gexp[glog[v] + linv] : 0u;
             aug[j * RC + p] = (uint8_t)nv;
             plog[j] = nv ? glog[nv] : (int16_t)-1;
         }
-        if (lane == 0) piv_row[c] = (uint8_t)p;
+        if (tid == 0) piv_row[c] = (uint8_t)p;
         __syncthreads();
-        // Clear column c from every other row.
+        // Clear column c from every other row; the waves split the columns.
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int i = lane + 64 * h;
-            if (i >= e || i == p || (h == 1 && RC == 64)) continue;
-            const uint32_t f = aug[c * RC + i];
+            const uint32_t f = h ? f1 : f0;
             if (!f) continue;
             const int lf = glog[f];
             // 8 independent updates per step and no branches, so the LDS latencies overlap
             // (indices past the row are clamped to its last column: same value rewritten).
-            for (int j0 = c; j0 < w2; j0 += 8) {
+            for (int j0 = c + 8 * wv; j0 < w2; j0 += 8 * NW) {
                 int pl[8];
                 uint32_t av[8], gv[8];
 #pragma unroll
@@ -353,16 +356,16 @@ __global__ void __launch_bounds__(64) lh_plan_kernel(lh::PlanArgs a) {
     }
     // A^-1[c][j] = aug[e + j][p_c].  Emit: out slots, src/rec slot maps, coef (e x m over
     // recovery rows) and W (e x k over slots).
-    for (int i = lane; i < e; i += 64) pv.set_out_slot(i, rcv_slot[i]);
-    for (int x = lane; x < k; x += 64) pv.set_src_slot(x, slot_of[x]);
-    for (int r = lane; r < m; r += 64) pv.set_rec_slot(r, slot_of[k + r]);
-    for (int q = lane; q < e * m; q += 64) pv.set_coef(q / m, q % m, 0);
+    for (int i = tid; i < e; i += nth) pv.set_out_slot(i, rcv_slot[i]);
+    for (int x = tid; x < k; x += nth) pv.set_src_slot(x, slot_of[x]);
+    for (int r = tid; r < m; r += nth) pv.set_rec_slot(r, slot_of[k + r]);
+    for (int q = tid; q < e * m; q += nth) pv.set_coef(q / m, q % m, 0);
     __syncthreads();
-    for (int q = lane; q < e * e; q += 64) {
+    for (int q = tid; q < e * e; q += nth) {
         const int i = q / e, j = q % e;
         pv.set_coef(i, rcv_row[j], aug[(e + j) * RC + piv_row[i]]);
     }
-    for (int q = lane; a.want_w && q < e * k; q += 64) {
+    for (int q = tid; a.want_w && q < e * k; q += nth) {
         const int i = q / k, slot = q % k;
         const int r = rows[slot];
         uint32_t v = 0;
@@ -377,7 +380,7 @@ __global__ void __launch_bounds__(64) lh_plan_kernel(lh::PlanArgs a) {
         pv.set_w(i, slot, (uint8_t)v);
     }
     // Recovery slot i takes erased row E_i (reference generate_bitmatrix, :786).
-    for (int i = lane; i < e; i += 64) rws[rcv_slot[i]] = erasure[i];
+    for (int i = tid; i < e; i += nth) rws[rcv_slot[i]] = erasure[i];
 }
 
 // ------------------------------------------------------- decode plan, small e_max
@@ -565,8 +568,11 @@ hipError_t launch_plan(const PlanArgs &a, hipStream_t st) {
         else hipLaunchKernelGGL(lh_plan_small_kernel<8>, dim3(blocks), dim3(256), 0, st, a);
         return hipGetLastError();
     }
+    // Few stripes (latency-bound: one workgroup per stripe cannot fill the chip): four
+    // waves per stripe split the elimination's columns; many stripes: one wave each.
     const size_t lds = (size_t)2 * a.e_max * (a.e_max > 64 ? 128 : 64);
-    hipLaunchKernelGGL(lh_plan_kernel, dim3((unsigned)a.stripes), dim3(64), lds, st, a);
+    const unsigned threads = (a.stripes <= 4096 && a.e_max > 8) ? 256u : 64u;
+    hipLaunchKernelGGL(lh_plan_kernel, dim3((unsigned)a.stripes), dim3(threads), lds, st, a);
     return hipGetLastError();
 }
 

@@ -120,6 +120,8 @@ def _encode_batch_vs_oracle(lh, oracle, k, m, nbytes, stripes, seed):
     (29, 4, 1296, 257), (29, 2, 1296, 64), (29, 3, 1296, 64), (29, 8, 1296, 32), (4, 2, 16, 100),
     (10, 6, 8, 200), (17, 6, 520, 40), (64, 5, 4096, 8), (3, 250, 24, 6), (250, 3, 24, 6),
     (128, 32, 8192, 3), (200, 56, 65536, 1), (2, 2, 8, 1000), (29, 4, 1304, 33), (9, 7, 72, 129),
+    # windowed large-m path: one wave (16 rows) per workgroup, two waves (16 + 4), m = 6 (k = 250)
+    (100, 16, 2048, 5), (40, 20, 4096, 4), (250, 6, 2048, 3),
 ])
 def test_encode_batch_vs_oracle(lh, oracle, path, k, m, nbytes, stripes):
     _encode_batch_vs_oracle(lh, oracle, k, m, nbytes, stripes, seed=k * 7 + m + nbytes)
@@ -141,6 +143,8 @@ def _decode_scenarios(k, m, nbytes, stripes, seed, e=None):
     (17, 6, 520, 40, None), (128, 32, 8192, 3, 32), (128, 32, 1024, 8, None), (200, 56, 65536, 1, 56),
     (5, 3, 8, 200, None), (2, 2, 8, 50, 2), (29, 1, 1296, 50, None), (29, 1, 20, 50, None),
     (1, 3, 16, 10, None),
+    # fused wide decode: 2 and 3 waves per workgroup, one wave (m = 6, k = 250), random e
+    (100, 16, 2048, 12, None), (40, 20, 4096, 8, None), (250, 6, 2048, 8, None),
 ])
 def test_decode_batch_vs_oracle(lh, oracle, path, k, m, nbytes, stripes, e):
     import torch

@@ -19,9 +19,10 @@ import longhair_amd as lh  # noqa: E402
 
 VARIANTS = [
     ("base", {}),
-    ("prepfirst", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PREP_FIRST=1"}),
-    ("nf_pf2_lb3", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1", "LONGHAIR_AMD_JIT_DEFINES": "LH_PREP_FIRST=1,LH_PF_DEC=2,LH_DEC_LB=3"}),
-    ("nf_pf3", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1", "LONGHAIR_AMD_JIT_DEFINES": "LH_PREP_FIRST=1,LH_PF_DEC=3"}),
+    ("st_plain", {"LONGHAIR_AMD_JIT_DEFINES": "LH_NT_ST=0"}),
+    ("ld_plain", {"LONGHAIR_AMD_JIT_DEFINES": "LH_NT=0,LH_NT_ST=1"}),
+    ("pf4", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=4"}),
+    ("pf2", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=2"}),
 ]
 KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID", "LONGHAIR_AMD_NO_FUSED_PLAN",
          "LONGHAIR_AMD_WIN_ROWS", "LONGHAIR_AMD_WIN_PF", "LONGHAIR_AMD_WIN_LDS"]
