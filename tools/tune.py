@@ -19,10 +19,8 @@ import longhair_amd as lh  # noqa: E402
 
 VARIANTS = [
     ("base", {}),
-    ("st_plain", {"LONGHAIR_AMD_JIT_DEFINES": "LH_NT_ST=0"}),
-    ("ld_plain", {"LONGHAIR_AMD_JIT_DEFINES": "LH_NT=0,LH_NT_ST=1"}),
-    ("pf4", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=4"}),
-    ("pf2", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=2"}),
+    ("zskip0", {"LONGHAIR_AMD_JIT_DEFINES": "LH_ZSKIP=0"}),
+    ("nofused", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1"}),
 ]
 KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID", "LONGHAIR_AMD_NO_FUSED_PLAN",
          "LONGHAIR_AMD_WIN_ROWS", "LONGHAIR_AMD_WIN_PF", "LONGHAIR_AMD_WIN_LDS"]
