@@ -270,6 +270,7 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
     // form: (v1..v7, v0^v1^v2^v7)).  (A nibble-windowed variant -- a 16-way uniform switch
     // per output and nibble with XOR3-paired cases -- measured 1.2-1.3x slower.)
     os << "#ifndef LH_PB_MASK  // masks: k128/m32 decode 7.0 ms against 6.5 ms with branches\n#define LH_PB_MASK 0\n#endif\n";
+    os << "#ifndef LH_PB_PAIR  // bits in pairs, XOR3 when both set: 7.2 ms against 6.2 (k128/m32 decode)\n#define LH_PB_PAIR 0\n#endif\n";
     // The coefficients of the wave's 8 outputs for used row j sit packed in lane j
     // (cpk0: outputs 0..3, cpk1: 4..7) and come back as SGPRs through v_readlane, and the
     // next row's V is read from LDS while the current row is applied, so no LDS round
@@ -299,6 +300,26 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
        << "      }\n"
        << "      const unsigned int c0 = (unsigned int)__builtin_amdgcn_readlane((int)cpk0, j);\n"
        << "      const unsigned int c1 = (unsigned int)__builtin_amdgcn_readlane((int)cpk1, j);\n"
+       << "#if LH_PB_PAIR  // bits (2q, 2q + 1) of a coefficient together: both set -> one XOR3\n"
+       << "#pragma unroll\n      for (int q = 0; q < 4; ++q) {\n"
+       << "        unsigned int w[8];  // w = B(2) v: the ladder entry of bit 2q + 1\n"
+       << "        {\n          const unsigned int t7 = __builtin_amdgcn_bitop3_b32(v[0], v[1], v[2], 0x96) ^ v[7];\n"
+       << "#pragma unroll\n          for (int y = 0; y < 7; ++y) w[y] = v[y + 1];\n"
+       << "          w[7] = t7;\n        }\n"
+       << "#pragma unroll\n        for (int i = 0; i < 8; ++i) {\n"
+       << "          const unsigned int two = ((i < 4 ? c0 : c1) >> (8 * (i & 3) + 2 * q)) & 3u;\n"
+       << "          if (two == 3u) {\n"
+       << "#pragma unroll\n            for (int y = 0; y < 8; ++y) acc[i][y] = __builtin_amdgcn_bitop3_b32(acc[i][y], v[y], w[y], 0x96);\n"
+       << "          } else if (two == 1u) {\n"
+       << "#pragma unroll\n            for (int y = 0; y < 8; ++y) acc[i][y] ^= v[y];\n"
+       << "          } else if (two == 2u) {\n"
+       << "#pragma unroll\n            for (int y = 0; y < 8; ++y) acc[i][y] ^= w[y];\n"
+       << "          }\n        }\n"
+       << "        if (q < 3) {  // v = B(2) w: the entry of bit 2q + 2\n"
+       << "          const unsigned int t7 = __builtin_amdgcn_bitop3_b32(w[0], w[1], w[2], 0x96) ^ w[7];\n"
+       << "#pragma unroll\n          for (int y = 0; y < 7; ++y) v[y] = w[y + 1];\n"
+       << "          v[7] = t7;\n        }\n      }\n"
+       << "#else\n"
        << "#pragma unroll\n      for (int t = 0; t < 8; ++t) {\n"
        << "#pragma unroll\n        for (int i = 0; i < 8; ++i) {\n"
        << "          const unsigned int bit = ((i < 4 ? c0 : c1) >> (8 * (i & 3) + t)) & 1u;\n"
@@ -313,7 +334,9 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
        << "        if (t < 7) {\n"
        << "          const unsigned int t7 = __builtin_amdgcn_bitop3_b32(v[0], v[1], v[2], 0x96) ^ v[7];\n"
        << "#pragma unroll\n          for (int y = 0; y < 7; ++y) v[y] = v[y + 1];\n"
-       << "          v[7] = t7;\n        }\n      }\n    }\n"
+       << "          v[7] = t7;\n        }\n      }\n"
+       << "#endif\n"
+       << "    }\n"
        << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n"
        << "      if (i0 + i < e) {\n"
        << "        unsigned char *dst = base + (long long)pl[16 + i0 + i] * " << c.bytes << ";\n"
