@@ -79,6 +79,7 @@ struct Workspace {
 // Per-device state.
 struct Device {
     int id = 0;
+    int cus = 0;                         // compute units
     std::mutex mu;                       // guards maps below and the drop-in staging
     uint8_t *gf_exp = nullptr;           // 512 B
     int16_t *gf_log = nullptr;           // 256 x int16
@@ -117,6 +118,7 @@ static int current_device(Device **out) {
         LH_HIP(hipMemcpy(d->gf_exp, F.exp, 512, hipMemcpyHostToDevice));
         LH_HIP(hipMemcpy(d->gf_log, F.log, 256 * sizeof(int16_t), hipMemcpyHostToDevice));
         LH_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        LH_HIP(hipDeviceGetAttribute(&d->cus, hipDeviceAttributeMultiprocessorCount, id));
         slot = std::move(d);
     }
     *out = slot.get();
@@ -287,14 +289,22 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         // Plan computed inside the decode kernel: one launch, no plan workspace.
         const uint8_t *zero = nullptr;
         if (int rc = zero_page(d, (size_t)bytes, &zero)) return rc;
-        const long long blocks = jit_blocks(cfg, stripes);
+        long long blocks = jit_blocks(cfg, stripes);
+        hipFunction_t fn = jk->decode_fused;
+        const char *pipe = std::getenv("LONGHAIR_AMD_DEC_PIPE");
+        if (pipe && std::atoi(pipe) && jk->decode_pipe && jk->pipe_blocks_per_cu > 0 && d->cus > 0) {
+            // Persistent pipelined variant: at most one resident grid.
+            const long long resident = (long long)d->cus * jk->pipe_blocks_per_cu;
+            if (blocks > resident) blocks = resident;
+            fn = jk->decode_pipe;
+        }
         long long s1 = stride;
         const uint8_t *gexp = d->gf_exp;
         const int16_t *glog = d->gf_log;
         int n = stripes;
         void *args[] = {(void *)&d_blocks, &s1, (void *)&d_rows, (void *)&d_status, (void *)&zero,
                         (void *)&gexp, (void *)&glog, &n};
-        LH_HIP(hipModuleLaunchKernel(jk->decode_fused, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr));
+        LH_HIP(hipModuleLaunchKernel(fn, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr));
         return kOk;
     }
     // Large m (<= 64): the fused windowed decode (phase A into LDS, phase B from LDS) after

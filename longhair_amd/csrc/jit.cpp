@@ -621,6 +621,13 @@ const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err) {
     kern.decode = fn("lh_jit_decode");
     kern.encode_dma = fn("lh_jit_encode_dma");
     kern.decode_fused = fn("lh_jit_decode_fused");
+    kern.decode_pipe = fn("lh_jit_decode_pipe");
+    if (kern.decode_pipe &&
+        hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&kern.pipe_blocks_per_cu, kern.decode_pipe, 256, 0) !=
+            hipSuccess) {
+        (void)hipGetLastError();
+        kern.pipe_blocks_per_cu = 0;
+    }
     kern.encode_win = fn("lh_jit_encode_win");
     kern.decode_wide = fn("lh_jit_decode_wide");
     if (!kern.encode && !kern.encode_win && !kern.decode_wide) {

@@ -690,42 +690,41 @@ struct lh_no_prep {
 // recovery row r.  Phase B: D_{E_i} = sum_r B(coef[i][r]) V_r with the per-stripe inverse,
 // by Horner over the coefficient bits: B(c) v = B(2)(...B(2)(c_7 v)...) + c_0 v.
 // `prep` runs while the first columns are in flight (the fused kernel solves its plan there).
-template <class PREP>
-__device__ __forceinline__ void lh_decode_body(const lh_lane &l, unsigned char *__restrict__ blocks,
-                                               long long stripe_stride, lh_plan_regs &pr,
-                                               const unsigned char *__restrict__ zero_page, const PREP &prep) {
-    unsigned char *base = blocks + l.stripe * stripe_stride + l.p;
-    const unsigned char *zero = zero_page + l.p;
+// Decode pieces.  Ring issue: the first LH_PF_DEC columns of a stripe group.
+__device__ __forceinline__ void lh_dec_issue(lh_word (&ring)[LH_PF_DEC][8], const lh_plan_regs &pr,
+                                             const unsigned char *base, const unsigned char *zero) {
+#pragma unroll
+    for (int q = 0; q < LH_PF_DEC; ++q) {
+        const unsigned char *src = (q == 0) ? lh_dcol_src<0>(pr.srcw, pr.recw, base, zero)
+                                 : (q == 1) ? lh_dcol_src<1>(pr.srcw, pr.recw, base, zero)
+                                 : (q == 2) ? lh_dcol_src<2>(pr.srcw, pr.recw, base, zero)
+                                            : lh_dcol_src<3>(pr.srcw, pr.recw, base, zero);
+        lh_load_col(ring[q], src, zero);
+    }
+}
 
-    lh_word v[LH_M][8];
+// Phase A: V_r = R_r + sum_{x present} B(G[r][x]) D_x for every recovery row r, streaming
+// the ring (already issued) through all k + m columns.
+__device__ __forceinline__ void lh_dec_phase_a(lh_word (&v)[LH_M][8], lh_word (&ring)[LH_PF_DEC][8],
+                                               const lh_plan_regs &pr, const unsigned char *base,
+                                               const unsigned char *zero) {
 #pragma unroll
     for (int r = 0; r < LH_M; ++r)
 #pragma unroll
         for (int y = 0; y < 8; ++y)
 #pragma unroll
             for (int i = 0; i < LH_NW; ++i) v[r][y].v[i] = 0;
-    {
-#if LH_PREP_FIRST
-        prep(pr);  // solve before the first loads: the ring is not live across the solve
-#endif
-        lh_word ring[LH_PF_DEC][8];
-#pragma unroll
-        for (int q = 0; q < LH_PF_DEC; ++q) {
-            const unsigned char *src = (q == 0) ? lh_dcol_src<0>(pr.srcw, pr.recw, base, zero)
-                                     : (q == 1) ? lh_dcol_src<1>(pr.srcw, pr.recw, base, zero)
-                                     : (q == 2) ? lh_dcol_src<2>(pr.srcw, pr.recw, base, zero)
-                                                : lh_dcol_src<3>(pr.srcw, pr.recw, base, zero);
-            lh_load_col(ring[q], src, zero);
-        }
-#if !LH_PREP_FIRST
-        prep(pr);
-#endif
-        lh_unroll_decode<0>::run(v, ring, base, zero, pr.srcw, pr.recw);
-    }
+    lh_unroll_decode<0>::run(v, ring, base, zero, pr.srcw, pr.recw);
+}
+
+// Phase B: D_{E_i} = sum_r B(coef[i][r]) V_r with the per-stripe inverse, by Horner over
+// the coefficient bits: B(c) v = B(2)(...B(2)(c_7 v)...) + c_0 v, one v_bitop3 masked XOR
+// per (row, bit, sub-row); the recovered blocks go to the plan's output slots.
+__device__ __forceinline__ void lh_dec_phase_b(const lh_word (&v)[LH_M][8], const lh_plan_regs &pr,
+                                               unsigned char *base) {
     const int e = pr.e;
     const unsigned int(&coefw)[LH_NCOEF] = pr.coefw;
     const unsigned int(&outw)[LH_NOUT] = pr.outw;
-
 #pragma unroll
     for (int i = 0; i < LH_EMAX; ++i) {
         if (i < e) {
@@ -767,6 +766,29 @@ __device__ __forceinline__ void lh_decode_body(const lh_lane &l, unsigned char *
     }
 }
 
+// In-place erasure decode of one stripe group: ring issue, `prep` (the fused kernel
+// solves its plan there, while the first columns are in flight), phase A, phase B.
+template <class PREP>
+__device__ __forceinline__ void lh_decode_body(const lh_lane &l, unsigned char *__restrict__ blocks,
+                                               long long stripe_stride, lh_plan_regs &pr,
+                                               const unsigned char *__restrict__ zero_page, const PREP &prep) {
+    unsigned char *base = blocks + l.stripe * stripe_stride + l.p;
+    const unsigned char *zero = zero_page + l.p;
+    lh_word v[LH_M][8];
+    {
+#if LH_PREP_FIRST
+        prep(pr);  // solve before the first loads: the ring is not live across the solve
+#endif
+        lh_word ring[LH_PF_DEC][8];
+        lh_dec_issue(ring, pr, base, zero);
+#if !LH_PREP_FIRST
+        prep(pr);
+#endif
+        lh_dec_phase_a(v, ring, pr, base, zero);
+    }
+    lh_dec_phase_b(v, pr, base);
+}
+
 __device__ __forceinline__ void lh_decode_wave(long long wave, unsigned char *__restrict__ blocks,
                                                long long stripe_stride, const unsigned char *__restrict__ plan,
                                                long long plan_stride, const unsigned char *__restrict__ zero_page,
@@ -805,6 +827,18 @@ lh_jit_decode(unsigned char *__restrict__ blocks, long long stripe_stride,
 static constexpr unsigned char LH_GRAW[LH_M][LH_K] = LH_G_INIT;
 #define LH_P4(n) (((n) + 3) / 4 * 4)
 #define LH_SR (2 * LH_P4(LH_K) + LH_P4(LH_M))  // per-stripe scratch: rows | src map | rec map
+#define LH_NRW ((LH_K + LH_NCH - 1) / LH_NCH)    // Block.row bytes per lane
+
+// The lane's Block.row bytes (slots c, c + LH_NCH, ...), loaded ahead of the plan.
+__device__ __forceinline__ void lh_fused_rows(const lh_lane &l, int c, const unsigned char *__restrict__ rows,
+                                              unsigned int (&rowv)[LH_NRW]) {
+    const unsigned char *grow = rows + l.stripe * LH_K;
+#pragma unroll
+    for (int t = 0; t < LH_NRW; ++t) {
+        const int i = c + t * LH_NCH;
+        rowv[t] = (l.active && i < LH_K) ? (unsigned int)grow[i] : 0u;
+    }
+}
 
 __device__ __forceinline__ unsigned int lh_gmul(const unsigned char *gexp, const short *glog, unsigned int a,
                                                 unsigned int b) {
@@ -825,6 +859,7 @@ struct lh_fused_solve {
 // Part 1: slot maps, validity and the erasure / recovery lists.  Returns false when the
 // stripe has nothing to do (no erasure or invalid rows).
 __device__ __forceinline__ bool lh_fused_plan(const lh_lane &l, int c, int sl, unsigned char *scr,
+                                              const unsigned int (&rowv)[LH_NRW],
                                               unsigned char *__restrict__ rows, signed char *__restrict__ status,
                                               lh_fused_solve &sv, lh_plan_regs &pr) {
     unsigned char *lrows = scr;
@@ -834,8 +869,11 @@ __device__ __forceinline__ bool lh_fused_plan(const lh_lane &l, int c, int sl, u
     // Clear the maps (0xFF = absent), then every lane records the rows of its slots.
     for (int q = c; q < (LH_P4(LH_K) + LH_P4(LH_M)) / 4; q += LH_NCH) ((unsigned int *)lsrc)[q] = 0xFFFFFFFFu;
     bool bad = false;
-    for (int i = c; i < LH_K; i += LH_NCH) {
-        const unsigned int r = grow[i];
+#pragma unroll
+    for (int t = 0; t < LH_NRW; ++t) {
+        const int i = c + t * LH_NCH;
+        if (i >= LH_K) continue;
+        const unsigned int r = rowv[t];
         lrows[i] = (unsigned char)r;
         if (r < LH_K) lsrc[r] = (unsigned char)i;
         else if (r < LH_K + LH_M) lrec[r - LH_K] = (unsigned char)i;
@@ -973,8 +1011,75 @@ lh_jit_decode_fused(unsigned char *__restrict__ blocks, long long stripe_stride,
         lh_fused_solve sv;
         sv.gexp = gexp;
         sv.glog = glog;
-        if (l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rows, status, sv, pr))
+        unsigned int rowv[LH_NRW];
+        lh_fused_rows(l, c, rows, rowv);
+        if (l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr))
             lh_decode_body(l, blocks, stripe_stride, pr, zero_page, sv);
+    }
+}
+
+// Persistent, software-pipelined variant (host launches at most one resident grid): while
+// a wave runs phase B of its stripe group, the next group's plan is already derived (its
+// Block.row bytes were loaded before phase A) and its first columns are in flight.
+extern "C" __global__ void __launch_bounds__(256, LH_DEC_LB)
+lh_jit_decode_pipe(unsigned char *__restrict__ blocks, long long stripe_stride, unsigned char *__restrict__ rows,
+                   signed char *__restrict__ status, const unsigned char *__restrict__ zero_page,
+                   const unsigned char *__restrict__ gf_exp, const short *__restrict__ gf_log, int stripes) {
+    __shared__ unsigned char gexp[512];
+    __shared__ short glog[256];
+    __shared__ __attribute__((aligned(16))) unsigned char scratch[4][LH_SPW > 0 ? LH_SPW : 1][LH_SR];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        gexp[i] = gf_exp[i];
+        gexp[i + 256] = gf_exp[i + 256];
+        glog[i] = gf_log[i];
+    }
+    __syncthreads();
+    const int wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int sl = lane / LH_NCH;
+    const int c = lane - sl * LH_NCH;
+    const long long nw = lh_total_waves(stripes);
+    const long long wstride = (long long)gridDim.x * (blockDim.x >> 6);
+    long long w = (long long)blockIdx.x * (blockDim.x >> 6) + wid;
+    if (w >= nw) return;
+    lh_lane l = lh_map_lane(stripes, w);
+    unsigned int rowv[LH_NRW];
+    lh_fused_rows(l, c, rows, rowv);
+    lh_plan_regs pr;
+    lh_fused_solve sv;
+    sv.gexp = gexp;
+    sv.glog = glog;
+    bool go = l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr);
+    lh_word ring[LH_PF_DEC][8];
+    if (go) lh_dec_issue(ring, pr, blocks + l.stripe * stripe_stride + l.p, zero_page + l.p);
+    for (;;) {
+        const long long w2 = w + wstride;
+        const bool more = w2 < nw;
+        const lh_lane l2 = lh_map_lane(stripes, w2);
+        unsigned int rowv2[LH_NRW];
+        if (more) lh_fused_rows(l2, c, rows, rowv2);  // in flight during phase A
+        unsigned char *base = blocks + l.stripe * stripe_stride + l.p;
+        lh_word v[LH_M][8];
+        if (go) {
+            sv(pr);
+            lh_dec_phase_a(v, ring, pr, base, zero_page + l.p);
+        }
+        lh_plan_regs pr2;
+        lh_fused_solve sv2;
+        sv2.gexp = gexp;
+        sv2.glog = glog;
+        bool go2 = false;
+        if (more) {
+            go2 = l2.active && lh_fused_plan(l2, c, sl, &scratch[wid][sl][0], rowv2, rows, status, sv2, pr2);
+            if (go2) lh_dec_issue(ring, pr2, blocks + l2.stripe * stripe_stride + l2.p, zero_page + l2.p);
+        }
+        if (go) lh_dec_phase_b(v, pr, base);
+        if (!more) break;
+        w = w2;
+        l = l2;
+        pr = pr2;
+        sv = sv2;
+        go = go2;
     }
 }
 #endif  // LH_EMAX <= 4 && LH_NCH <= 64 && LH_K <= 64

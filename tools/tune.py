@@ -19,10 +19,11 @@ import longhair_amd as lh  # noqa: E402
 
 VARIANTS = [
     ("base", {}),
-    ("zskip0", {"LONGHAIR_AMD_JIT_DEFINES": "LH_ZSKIP=0"}),
-    ("nofused", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1"}),
+    ("pipe", {"LONGHAIR_AMD_DEC_PIPE": "1"}),
+    ("pipe_pf2", {"LONGHAIR_AMD_DEC_PIPE": "1", "LONGHAIR_AMD_JIT_DEFINES": "LH_PF_DEC=2"}),
 ]
 KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID", "LONGHAIR_AMD_NO_FUSED_PLAN",
+         "LONGHAIR_AMD_DEC_PIPE",
          "LONGHAIR_AMD_WIN_ROWS", "LONGHAIR_AMD_WIN_PF", "LONGHAIR_AMD_WIN_LDS"]
 # Large-m (windowed) variants: rows per wave and columns in flight.
 VARIANTS_WIN = [
