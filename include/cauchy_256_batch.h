@@ -43,8 +43,8 @@ int cauchy_256_decode_batch(int k, int m, int block_bytes, int stripes,
  * in host memory, pipelined in chunks of `chunk_stripes` (0 = about 64 MiB) over three
  * streams so the PCIe copies overlap the kernels.  Host buffers should be pinned
  * (hipHostMalloc / hipHostRegister).  Synchronous: returns when the results are in
- * host memory.  Decode returns every slot of each stripe (PCIe is full duplex) and the
- * rewritten rows. */
+ * host memory.  Decode copies back the slots decode can write (the recovery slots of each
+ * chunk's stripes) and the rewritten rows. */
 int cauchy_256_encode_host_batch(int k, int m, int block_bytes, int stripes,
                                  const void *h_data, long long data_stride,
                                  void *h_recovery, long long recovery_stride, int chunk_stripes);
@@ -60,14 +60,31 @@ int cauchy_256_batch_prepare(int k, int m, int block_bytes, int max_stripes);
 /* Which kernel family serves this shape: 0 = generic coefficient-driven kernels,
  * 1 = run-time specialised (JIT) network, 2 (decode only) = specialised network with the
  * erasure plan computed inside the same kernel, 3 (encode only) = run-time specialised
- * 4-bit-windowed network for large m, 4 (decode only) = windowed phase A + per-stripe
- * inverse kernel for large m.  `what` = 0 for encode, 1 for decode. */
+ * 4-bit-windowed network for large m, 4 (decode only) = per-stripe planner + fused
+ * windowed decode for large m (m <= 64).  `what` = 0 for encode, 1 for decode. */
 int cauchy_256_batch_path(int k, int m, int block_bytes, int what);
 
 /* Compile the specialised kernels of a shape into the on-disk code-object cache
  * ($LONGHAIR_AMD_CACHE_DIR, else jit_cache/ beside the library).  Needs no GPU.
  * Returns 0 or -3. */
 int cauchy_256_jit_precompile(int k, int m, int block_bytes);
+
+/* Packet framing: the reference transmits every block with its
+ * one-byte row (README.md:66-72).  A packet is [row][block_bytes bytes of the block],
+ * block_bytes + 1 bytes long, at any alignment.
+ *   frame:   the k data and m recovery blocks of stripe s become packets
+ *            d_packets + s * packet_stride + i * (block_bytes + 1), rows i = 0 .. k + m - 1.
+ *   unframe: the k packets received for stripe s (any order, any rows) at
+ *            d_packets + s * packet_stride + i * (block_bytes + 1) become decode slot i of
+ *            d_blocks and d_rows[s * k + i], ready for cauchy_256_decode_batch.
+ * Asynchronous on `stream`; 0, -1 (invalid parameters), -2 or -3. */
+int cauchy_256_frame_batch(int k, int m, int block_bytes, int stripes,
+                           const void *d_data, long long data_stride,
+                           const void *d_recovery, long long recovery_stride,
+                           void *d_packets, long long packet_stride, void *stream);
+int cauchy_256_unframe_batch(int k, int block_bytes, int stripes,
+                             const void *d_packets, long long packet_stride,
+                             void *d_blocks, long long stripe_stride, unsigned char *d_rows, void *stream);
 
 /* Last error message of the calling thread (empty string if none). */
 const char *cauchy_256_last_error(void);

@@ -149,6 +149,45 @@ def decode_host_batch(blocks, rows, m, chunk_stripes=0):
     return status
 
 
+def frame_batch(data, recovery, packets=None, stream=None):
+    """Packets of a batch (the reference sends each block with its one-byte row,
+    README.md:66-72): uint8 CUDA tensors data [S, k, B] and recovery [S, m, B] ->
+    packets [S, k + m, B + 1], packet i = [row i][block i]."""
+    import torch
+    stripes, k, nbytes = data.shape
+    m = recovery.shape[1]
+    assert data.stride(2) == 1 and data.stride(1) == nbytes and recovery.stride(2) == 1 and recovery.stride(1) == nbytes
+    if packets is None:
+        packets = torch.empty((stripes, k + m, nbytes + 1), dtype=torch.uint8, device=data.device)
+    assert packets.is_contiguous() and tuple(packets.shape) == (stripes, k + m, nbytes + 1)
+    rc = lib().cauchy_256_frame_batch(k, m, nbytes, stripes, ctypes.c_void_p(data.data_ptr()), data.stride(0),
+                                      ctypes.c_void_p(recovery.data_ptr()), recovery.stride(0),
+                                      ctypes.c_void_p(packets.data_ptr()), packets.stride(0),
+                                      ctypes.c_void_p(_stream_handle(stream)))
+    if rc != 0:
+        raise LonghairError(rc, "cauchy_256_frame_batch")
+    return packets
+
+
+def unframe_batch(packets, blocks=None, rows=None, stream=None):
+    """The k packets received per stripe (uint8 CUDA tensor [S, k, B + 1], any order)
+    -> (blocks [S, k, B], rows [S, k]), the layout decode_batch takes."""
+    import torch
+    assert packets.is_contiguous() and packets.dtype == torch.uint8
+    stripes, k, b1 = packets.shape
+    if blocks is None:
+        blocks = torch.empty((stripes, k, b1 - 1), dtype=torch.uint8, device=packets.device)
+    if rows is None:
+        rows = torch.empty((stripes, k), dtype=torch.uint8, device=packets.device)
+    assert blocks.stride(2) == 1 and blocks.stride(1) == b1 - 1 and rows.is_contiguous()
+    rc = lib().cauchy_256_unframe_batch(k, b1 - 1, stripes, ctypes.c_void_p(packets.data_ptr()), packets.stride(0),
+                                        ctypes.c_void_p(blocks.data_ptr()), blocks.stride(0),
+                                        ctypes.c_void_p(rows.data_ptr()), ctypes.c_void_p(_stream_handle(stream)))
+    if rc != 0:
+        raise LonghairError(rc, "cauchy_256_unframe_batch")
+    return blocks, rows
+
+
 def prepare(k, m, block_bytes, max_stripes=0):
     """Compile the specialised kernels / reserve workspace for a shape (synchronous)."""
     rc = lib().cauchy_256_batch_prepare(k, m, block_bytes, max_stripes)

@@ -32,6 +32,12 @@ EXPORTS = {
     "cauchy_256_batch_prepare": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "cauchy_256_batch_path": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "cauchy_256_jit_precompile": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "cauchy_256_frame_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_longlong,
+                                              ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p]),
+    "cauchy_256_unframe_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                                ctypes.c_longlong, ctypes.c_void_p, ctypes.c_longlong,
+                                                ctypes.c_void_p, ctypes.c_void_p]),
     "cauchy_256_last_error": (ctypes.c_char_p, []),
 }
 

@@ -757,6 +757,57 @@ LH_API int cauchy_256_batch_path(int k, int m, int block_bytes, int what) {
     return 1;
 }
 
+LH_API int cauchy_256_frame_batch(int k, int m, int block_bytes, int stripes, const void *d_data,
+                                  long long data_stride, const void *d_recovery, long long recovery_stride,
+                                  void *d_packets, long long packet_stride, void *stream) {
+    if (k < 1 || m < 0 || k + m > 256 || block_bytes <= 0 || stripes < 0 ||
+        data_stride < (long long)k * block_bytes || (m > 0 && recovery_stride < (long long)m * block_bytes) ||
+        packet_stride < (long long)(k + m) * (block_bytes + 1))
+        return lh::fail(lh::kInvalid, "invalid framing parameters");
+    lh::Device *d = nullptr;
+    if (int rc = lh::current_device(&d)) return rc;
+    lh::FrameArgs a{};
+    a.data = (const uint8_t *)d_data;
+    a.data_stride = data_stride;
+    a.rec = (const uint8_t *)d_recovery;
+    a.rec_stride = recovery_stride;
+    a.packets = (uint8_t *)d_packets;
+    a.packet_stride = packet_stride;
+    a.k = k;
+    a.m = m;
+    a.bytes = block_bytes;
+    a.stripes = stripes;
+    a.npk = k + m;
+    a.unframe = 0;
+    if (hipError_t e = lh::launch_frame(a, (hipStream_t)stream))
+        return lh::fail(lh::kHipError, std::string("frame: ") + hipGetErrorString(e));
+    return 0;
+}
+
+LH_API int cauchy_256_unframe_batch(int k, int block_bytes, int stripes, const void *d_packets,
+                                    long long packet_stride, void *d_blocks, long long stripe_stride,
+                                    unsigned char *d_rows, void *stream) {
+    if (k < 1 || k > 256 || block_bytes <= 0 || stripes < 0 || packet_stride < (long long)k * (block_bytes + 1) ||
+        stripe_stride < (long long)k * block_bytes)
+        return lh::fail(lh::kInvalid, "invalid framing parameters");
+    lh::Device *d = nullptr;
+    if (int rc = lh::current_device(&d)) return rc;
+    lh::FrameArgs a{};
+    a.packets = (uint8_t *)d_packets;
+    a.packet_stride = packet_stride;
+    a.blocks = (uint8_t *)d_blocks;
+    a.blocks_stride = stripe_stride;
+    a.rows = d_rows;
+    a.k = k;
+    a.bytes = block_bytes;
+    a.stripes = stripes;
+    a.npk = k;
+    a.unframe = 1;
+    if (hipError_t e = lh::launch_frame(a, (hipStream_t)stream))
+        return lh::fail(lh::kHipError, std::string("unframe: ") + hipGetErrorString(e));
+    return 0;
+}
+
 LH_API const char *cauchy_256_last_error(void) { return lh::g_last_error.c_str(); }
 
 }  // extern "C"

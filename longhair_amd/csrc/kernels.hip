@@ -534,6 +534,39 @@ __global__ void __launch_bounds__(256) lh_plan_small_kernel(lh::PlanArgs a) {
     for (int i = 0; i < EM; ++i) if (i < e) rws[rslot[i]] = (uint8_t)er[i];
 }
 
+// -------------------------------------------------------------------- framing
+// One thread per 4 bytes of a block; the packet payload sits one byte after the row, so
+// one side of every copy is unaligned (gfx950 serves unaligned dword accesses).
+typedef uint32_t lh_u32_unaligned __attribute__((aligned(1)));
+__global__ void __launch_bounds__(256) lh_frame_kernel(lh::FrameArgs a) {
+    const int words = (a.bytes + 3) / 4;
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long per_stripe = (long long)a.npk * words;
+    const long long s = t / per_stripe;
+    if (s >= a.stripes) return;
+    const int rem = (int)(t - s * per_stripe);
+    const int i = rem / words, w = rem - i * words;
+    uint8_t *pk = a.packets + s * a.packet_stride + (long long)i * (a.bytes + 1);
+    const uint8_t *src;
+    uint8_t *dst;
+    if (a.unframe) {
+        src = pk + 1;
+        dst = a.blocks + s * a.blocks_stride + (long long)i * a.bytes;
+        if (w == 0) a.rows[s * a.k + i] = pk[0];
+    } else {
+        src = i < a.k ? a.data + s * a.data_stride + (long long)i * a.bytes
+                      : a.rec + s * a.rec_stride + (long long)(i - a.k) * a.bytes;
+        dst = pk + 1;
+        if (w == 0) pk[0] = (uint8_t)i;
+    }
+    const int off = 4 * w, n = min(4, a.bytes - off);
+    if (n == 4) {
+        *(lh_u32_unaligned *)(dst + off) = *(const lh_u32_unaligned *)(src + off);
+    } else {
+        for (int q = 0; q < n; ++q) dst[off + q] = src[off + q];
+    }
+}
+
 // ------------------------------------------------------------------ host launchers
 namespace lh {
 
@@ -558,6 +591,13 @@ hipError_t launch_xor_reduce(const XorArgs &a, hipStream_t st) {
 hipError_t launch_scatter(const ScatterArgs &a, hipStream_t st) {
     const long long lanes = (long long)a.stripes * a.e_max * ((a.bytes + 15) / 16);
     hipLaunchKernelGGL(lh_scatter_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_frame(const FrameArgs &a, hipStream_t st) {
+    const long long threads = (long long)a.stripes * a.npk * ((a.bytes + 3) / 4);
+    if (threads <= 0) return hipSuccess;
+    hipLaunchKernelGGL(lh_frame_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

@@ -87,7 +87,21 @@ struct PlanArgs {
     int want_w;                   // emit the single-pass coefficients (generic path)
 };
 
+struct FrameArgs {
+    const uint8_t *data;          // frame: data blocks (stripe stride data_stride)
+    long long data_stride;
+    const uint8_t *rec;           // frame: recovery blocks
+    long long rec_stride;
+    uint8_t *packets;             // [stripe][packet i][row byte + block]
+    long long packet_stride;
+    uint8_t *blocks;              // unframe: decode slots
+    long long blocks_stride;
+    uint8_t *rows;                // unframe: Block.row bytes, stripes x k
+    int k, m, bytes, stripes, npk, unframe;
+};
+
 hipError_t launch_apply_generic(const ApplyArgs &a, int W, hipStream_t st);
+hipError_t launch_frame(const FrameArgs &a, hipStream_t st);
 hipError_t launch_xor_reduce(const XorArgs &a, hipStream_t st);
 hipError_t launch_scatter(const ScatterArgs &a, hipStream_t st);
 hipError_t launch_plan(const PlanArgs &a, hipStream_t st);

@@ -253,3 +253,28 @@ def test_host_batch_pipeline(lh, oracle, k, m, nbytes, stripes, chunk):
     assert (status == 0).all()
     assert np.array_equal(pr, exp_rows)
     assert np.array_equal(pb, exp_blocks)
+
+
+# ------------------------------------------------------------------- packet framing
+
+
+@pytest.mark.parametrize("k,m,nbytes,stripes", [(29, 4, 1296, 64), (10, 6, 24, 33), (3, 2, 8, 5)])
+def test_frame_unframe_decode(lh, k, m, nbytes, stripes):
+    """Encode, frame into [row][block] packets, keep k random packets per stripe in a
+    random order, unframe and decode: every stripe returns its data."""
+    import torch
+    g = torch.Generator(device="cuda").manual_seed(k * m)
+    data = torch.randint(0, 256, (stripes, k, nbytes), dtype=torch.uint8, device="cuda", generator=g)
+    rec = lh.encode_batch(data, m)
+    packets = lh.frame_batch(data, rec)
+    assert torch.equal(packets[:, :k, 1:], data) and torch.equal(packets[:, k:, 1:], rec)
+    assert packets[:, :, 0].cpu().tolist() == [list(range(k + m))] * stripes
+    pick = torch.argsort(torch.rand(stripes, k + m, device="cuda", generator=g), dim=1)[:, :k]
+    received = torch.gather(packets, 1, pick.unsqueeze(-1).expand(-1, -1, nbytes + 1)).contiguous()
+    blocks, rows = lh.unframe_batch(received)
+    assert torch.equal(rows, pick.to(torch.uint8))
+    status = lh.decode_batch(blocks, rows, m)
+    torch.cuda.synchronize()
+    assert int((status != 0).sum()) == 0
+    order = rows.long().argsort(dim=1)
+    assert torch.equal(torch.gather(blocks, 1, order.unsqueeze(-1).expand(-1, -1, nbytes)), data)
