@@ -501,23 +501,20 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
         const int n = stripes - s0 < chunk ? stripes - s0 : chunk;
         const int i = c % 3;
         hipStream_t st = d->pipe_stream[i];
-        int lo = k, hi = -1;
+        int lo = k, hi = -1;  // slot range [lo, hi] decode may write in this chunk
         if (k > 1) {
             for (int s = s0; s < s0 + n; ++s) {
                 const uint8_t *r = h_rows + (long long)s * k;
-                int last = -1;
+                int first = -1, last = -1;  // first / last recovery slot of the stripe
                 for (int x = 0; x < k; ++x) {
                     if (r[x] < k) continue;
-                    if (m > 1 || last < 0) lo = x < lo ? x : lo;
+                    if (first < 0) first = x;
                     last = x;
                 }
-                if (m == 1) {
-                    const int out = last < 0 ? 0 : last;
-                    lo = out < lo ? out : lo;
-                    hi = out > hi ? out : hi;
-                } else if (last > hi) {
-                    hi = last;
-                }
+                if (m == 1) first = last = (last < 0 ? 0 : last);  // the single output slot
+                if (first < 0) continue;
+                lo = first < lo ? first : lo;
+                hi = last > hi ? last : hi;
             }
         }
         LH_HIP(hipMemcpy2DAsync(d->pipe_blocks[i].ptr, sz, h_blocks + (long long)s0 * stride, stride, sz, n,
