@@ -221,7 +221,7 @@ static int encode_batch(int k, int m, int bytes, int stripes, const uint8_t *d_d
             long long in_stride = data_stride, out_stride = rec_stride;
             int n = stripes;
             void *args[] = {(void *)&d_data, &in_stride, (void *)&d_rec, &out_stride, &n};
-            LH_HIP(hipModuleLaunchKernel(jk->encode_dma ? jk->encode_dma : jk->encode, (unsigned)blocks, 1, 1, 256,
+            LH_HIP(hipModuleLaunchKernel(jk->encode, (unsigned)blocks, 1, 1, 256,
                                          1, 1, 0, st, args, nullptr));
             return kOk;
         }

@@ -61,7 +61,7 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     }
     if (const char *fw = std::getenv("LONGHAIR_AMD_JIT_W")) {  // tuning override
         const int W = std::atoi(fw);
-        if ((W == 1 || W == 2 || W == 4 || W == 8 || W == 16) && W <= sub &&
+        if ((W == 1 || W == 2 || W == 4 || W == 8 || W == 12 || W == 16) && W <= sub &&
             rows * 8 * ((W + 3) / 4) <= 2 * kMaxAccDwords) {
             const int nch = (sub + W - 1) / W;
             if (!(nch > 64 && decode && sub % W != 0)) { best_w = W; best_nch = nch; }
@@ -619,7 +619,6 @@ const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err) {
     };
     kern.encode = fn("lh_jit_encode");
     kern.decode = fn("lh_jit_decode");
-    kern.encode_dma = fn("lh_jit_encode_dma");
     kern.decode_fused = fn("lh_jit_decode_fused");
     kern.decode_pipe = fn("lh_jit_decode_pipe");
     if (kern.decode_pipe &&

@@ -30,7 +30,6 @@ struct JitKernels {
     hipModule_t module = nullptr;
     hipFunction_t encode = nullptr;
     hipFunction_t decode = nullptr;
-    hipFunction_t encode_dma = nullptr;    // present when compiled with LH_DMA=1
     hipFunction_t decode_fused = nullptr;  // plan computed in-kernel (e_max <= 4)
     hipFunction_t decode_pipe = nullptr;   // persistent software-pipelined variant of decode_fused
     int pipe_blocks_per_cu = 0;            // its occupancy (blocks of 256 threads per CU)

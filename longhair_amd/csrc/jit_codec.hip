@@ -47,6 +47,7 @@ struct lh_word {
 #define LH_NT 1  // non-temporal (streaming) loads and stores: +3% on k29/m4 (tools/tune.py)
 #endif
 typedef unsigned int lh_u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int lh_u32x3 __attribute__((ext_vector_type(3)));
 typedef unsigned int lh_u32x4 __attribute__((ext_vector_type(4)));
 
 // W-byte loads/stores at the sub-block's natural (often 2-byte) alignment: gfx950
@@ -56,6 +57,9 @@ __device__ __forceinline__ lh_word lh_load(const unsigned char *p) {
 #if LH_NT && LH_W == 16
     const lh_u32x4 v = __builtin_nontemporal_load((const lh_u32x4 *)p);
     w.v[0] = v.x; w.v[1] = v.y; w.v[2] = v.z; w.v[3] = v.w;
+#elif LH_NT && LH_W == 12
+    const lh_u32x3 v = __builtin_nontemporal_load((const lh_u32x3 *)p);
+    w.v[0] = v.x; w.v[1] = v.y; w.v[2] = v.z;
 #elif LH_NT && LH_W == 8
     const lh_u32x2 v = __builtin_nontemporal_load((const lh_u32x2 *)p);
     w.v[0] = v.x; w.v[1] = v.y;
@@ -76,6 +80,9 @@ __device__ __forceinline__ void lh_store(unsigned char *p, const lh_word &w) {
 #if LH_NT_ST && LH_W == 16
     lh_u32x4 v = {w.v[0], w.v[1], w.v[2], w.v[3]};
     __builtin_nontemporal_store(v, (lh_u32x4 *)p);
+#elif LH_NT_ST && LH_W == 12
+    lh_u32x3 v = {w.v[0], w.v[1], w.v[2]};
+    __builtin_nontemporal_store(v, (lh_u32x3 *)p);
 #elif LH_NT_ST && LH_W == 8
     lh_u32x2 v = {w.v[0], w.v[1]};
     __builtin_nontemporal_store(v, (lh_u32x2 *)p);
@@ -329,238 +336,6 @@ lh_jit_encode(const unsigned char *__restrict__ in, long long in_stride,
 }
 #endif
 
-// ------------------------------------------------------------- LDS-DMA staging
-// LH_DMA = 1 (host picks it when bytes % 16 == 0, LH_W == 8 and nch <= 64): instead of
-// every lane loading its 8 sub-block words straight from HBM at 2-byte alignment, each
-// wave streams its stripes' blocks into a private LDS ring with global_load_lds_dwordx4
-// (1 KiB contiguous per wave-instruction, no VGPRs), LH_DMA_X columns per ring slot and
-// LH_DMA_D slots in flight, then reads its words from LDS.  In LDS every lane's column
-// offset p is a multiple of 8, so the alignment of sub-block b (b * sub mod 8) is a
-// compile-time constant: aligned words use ds_read_b64, the rest two reads plus
-// v_alignbyte.  The tail lane reads past its sub-block inside LDS and stores only its
-// own bytes.
-#ifndef LH_DMA
-#define LH_DMA 0
-#endif
-#if LH_DMA
-#ifndef LH_DMA_X
-#define LH_DMA_X 2
-#endif
-#ifndef LH_DMA_D
-#define LH_DMA_D 3
-#endif
-#define LH_WPB 4  // waves per block
-#define LH_SLOT_BYTES (LH_SPW * LH_DMA_X * LH_BYTES)
-#define LH_WAVE_LDS (LH_DMA_D * LH_SLOT_BYTES + 64)
-#define LH_PIECES_PER_STRIPE (LH_DMA_X * LH_BYTES / 16)
-#define LH_PIECES (LH_SPW * LH_PIECES_PER_STRIPE)
-#define LH_DMA_INSTR ((LH_PIECES + 63) / 64)
-#define LH_TAIL (LH_SUB - 8 * (LH_NCH - 1))  // valid bytes of the last lane's word
-
-typedef __attribute__((address_space(3))) void *lh_lds_ptr;
-typedef __attribute__((address_space(1))) void *lh_glb_ptr;
-
-// Read 8 bytes at LDS byte offset `off` (off % 8 == S, compile time).
-template <int S>
-__device__ __forceinline__ lh_word lh_lds8(const unsigned char *lds, unsigned int off) {
-    lh_word w;
-    if (S == 0) {
-        const lh_u32x2 v = *(const lh_u32x2 *)(lds + off);
-        w.v[0] = v.x; w.v[1] = v.y;
-    } else if (S == 4) {
-        w.v[0] = *(const unsigned int *)(lds + off);
-        w.v[1] = *(const unsigned int *)(lds + off + 4);
-    } else if ((S & 3) == 0) {
-        // unreachable (S in {0, 4} handled)
-    } else {
-        const unsigned int a = off - (S & 3);  // 4-aligned
-        unsigned int w0, w1, w2;
-        if (((S - (S & 3)) & 7) == 0) {          // a % 8 == 0
-            const lh_u32x2 v = *(const lh_u32x2 *)(lds + a);
-            w0 = v.x; w1 = v.y;
-            w2 = *(const unsigned int *)(lds + a + 8);
-        } else {                                 // a % 8 == 4
-            w0 = *(const unsigned int *)(lds + a);
-            const lh_u32x2 v = *(const lh_u32x2 *)(lds + a + 4);
-            w1 = v.x; w2 = v.y;
-        }
-        w.v[0] = __builtin_amdgcn_alignbyte(w1, w0, S & 3);
-        w.v[1] = __builtin_amdgcn_alignbyte(w2, w1, S & 3);
-    }
-    return w;
-}
-
-template <int B>
-struct lh_lds_col {
-    __device__ __forceinline__ static void run(lh_word (&d)[8], const unsigned char *lds, unsigned int off) {
-        d[B] = lh_lds8<(B * LH_SUB) % 8>(lds, off + B * LH_SUB);
-        lh_lds_col<B + 1>::run(d, lds, off);
-    }
-};
-template <>
-struct lh_lds_col<8> {
-    __device__ __forceinline__ static void run(lh_word (&)[8], const unsigned char *, unsigned int) {}
-};
-
-// Per-lane DMA geometry, fixed for the whole kernel: for wave-instruction i of a stage
-// the lane copies piece q = 64 i + lane of the stage, i.e. stripe sl(q), column xl(q),
-// 16-byte piece within that column.  Offsets are relative to the wave's first stripe.
-struct lh_dma_geom {
-    unsigned int off[LH_DMA_INSTR];   // byte offset from the wave's first stripe base
-    unsigned int sl_xl[LH_DMA_INSTR]; // (sl << 8) | xl, 0xFFFF for a lane past the stage
-};
-
-__device__ __forceinline__ void lh_dma_geom_init(lh_dma_geom &g, long long in_stride) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int i = 0; i < LH_DMA_INSTR; ++i) {
-        const int q = i * 64 + lane;
-        const int sl = q / LH_PIECES_PER_STRIPE;
-        const int rem = q - sl * LH_PIECES_PER_STRIPE;
-        const int xl = rem / (LH_BYTES / 16);
-        g.off[i] = (unsigned int)(sl * in_stride) + (unsigned int)(xl * LH_BYTES) +
-                   (unsigned int)((rem - xl * (LH_BYTES / 16)) * 16);
-        g.sl_xl[i] = (q < LH_PIECES) ? (unsigned int)((sl << 8) | xl) : 0xFFFFu;
-    }
-}
-
-// Issue the DMA of stage G (columns G*X ..) of the wave whose first stripe starts at
-// `base` (wave-uniform); n_sl = stripes of this wave that exist.
-template <int G, int NCOLS>
-__device__ __forceinline__ void lh_issue_stage(unsigned char *lds_slot, const unsigned char *base, int n_sl,
-                                               const lh_dma_geom &geo) {
-    const unsigned char *gb = base + (long long)G * LH_DMA_X * LH_BYTES;
-#pragma unroll
-    for (int i = 0; i < LH_DMA_INSTR; ++i) {
-        const unsigned int sx = geo.sl_xl[i];
-        const bool ok = ((int)(sx >> 8) < n_sl) && ((int)(sx & 0xFF) < NCOLS - G * LH_DMA_X);
-        if (ok)
-            __builtin_amdgcn_global_load_lds((lh_glb_ptr)(gb + geo.off[i]), (lh_lds_ptr)(lds_slot + i * 1024), 16, 0,
-                                             LH_NT ? 2 : 0);
-    }
-}
-
-template <int N>
-__device__ __forceinline__ void lh_wait_vm() {
-    // s_waitcnt vmcnt(N), expcnt/lgkmcnt untouched (gfx9 encoding).
-    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-}
-
-#define LH_NSTAGE(NCOLS) (((NCOLS) + LH_DMA_X - 1) / LH_DMA_X)
-
-// Stage G of NCOLS columns: issue stage G + D - 1, wait for stage G, combine its columns.
-template <int G, int NCOLS, class COMBINE>
-struct lh_dma_loop {
-    __device__ __forceinline__ static void run(unsigned char *lds, const unsigned char *base, int n_sl,
-                                               const lh_dma_geom &geo, int sl, unsigned int p, COMBINE &comb) {
-        constexpr int NS = LH_NSTAGE(NCOLS);
-        if (G + LH_DMA_D - 1 < NS)
-            lh_issue_stage<(G + LH_DMA_D - 1 < NS ? G + LH_DMA_D - 1 : 0), NCOLS>(
-                lds + ((G + LH_DMA_D - 1) % LH_DMA_D) * LH_SLOT_BYTES, base, n_sl, geo);
-        constexpr int AHEAD = (NS - 1 - G) < (LH_DMA_D - 1) ? (NS - 1 - G) : (LH_DMA_D - 1);
-        lh_wait_vm<AHEAD * LH_DMA_INSTR>();
-        const unsigned char *slot = lds + (G % LH_DMA_D) * LH_SLOT_BYTES;
-#pragma unroll
-        for (int xl = 0; xl < LH_DMA_X; ++xl) {
-            if (G * LH_DMA_X + xl < NCOLS) {
-                lh_word d[8];
-                lh_lds_col<0>::run(d, slot, (unsigned int)(sl * LH_DMA_X + xl) * LH_BYTES + p);
-                comb.template column<G>(xl, d);
-                // Keep the next column's LDS reads below this column's XORs (register budget).
-                asm volatile("" ::: "memory");
-            }
-        }
-        lh_dma_loop<G + 1, NCOLS, COMBINE>::run(lds, base, n_sl, geo, sl, p, comb);
-    }
-};
-template <int NCOLS, class COMBINE>
-struct lh_dma_loop<LH_NSTAGE(NCOLS), NCOLS, COMBINE> {
-    __device__ __forceinline__ static void run(unsigned char *, const unsigned char *, int, const lh_dma_geom &, int,
-                                               unsigned int, COMBINE &) {}
-};
-
-// Column dispatcher with a runtime xl inside a compile-time stage: expands both
-// candidates' networks under a uniform branch.
-template <int X0, int N>
-struct lh_col_switch {
-    __device__ __forceinline__ static void run(int xl, lh_word (&acc)[LH_M][8], const lh_word (&d)[8]) {
-        if (xl == 0) lh_column<X0>(acc, d);
-        else lh_col_switch<X0 + 1, N - 1>::run(xl - 1, acc, d);
-    }
-};
-template <int X0>
-struct lh_col_switch<X0, 0> {
-    __device__ __forceinline__ static void run(int, lh_word (&)[LH_M][8], const lh_word (&)[8]) {}
-};
-
-struct lh_encode_comb {
-    lh_word (&acc)[LH_M][8];
-    __device__ __forceinline__ lh_encode_comb(lh_word (&a)[LH_M][8]) : acc(a) {}
-    template <int G>
-    __device__ __forceinline__ void column(int xl, const lh_word (&d)[8]) {
-        constexpr int X0 = G * LH_DMA_X;
-        constexpr int N = (LH_K - X0) < LH_DMA_X ? (LH_K - X0) : LH_DMA_X;
-        lh_col_switch<X0, N>::run(xl, acc, d);
-        lh_opaque(acc);
-    }
-};
-
-__device__ __forceinline__ void lh_store_tail(unsigned char *p, const lh_word &w, bool tail) {
-    if (!tail) {
-        lh_store(p, w);
-    } else {
-        // Only the first LH_TAIL bytes belong to this lane's sub-block.
-        unsigned char b[8];
-        __builtin_memcpy(b, &w.v[0], 8);
-#pragma unroll
-        for (int i = 0; i < LH_TAIL; ++i) p[i] = b[i];
-    }
-}
-
-#ifndef LH_DMA_LB
-#define LH_DMA_LB 2  // min waves per SIMD the register allocator must allow
-#endif
-extern "C" __global__ void __launch_bounds__(256, LH_DMA_LB)
-lh_jit_encode_dma(const unsigned char *__restrict__ in, long long in_stride,
-                  unsigned char *__restrict__ out, long long out_stride, int stripes) {
-    __shared__ __attribute__((aligned(16))) unsigned char lh_lds_all[LH_WPB * LH_WAVE_LDS];
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    unsigned char *lds = lh_lds_all + wid * LH_WAVE_LDS;
-    const int lane = threadIdx.x & 63;
-    const int sl = lane / LH_NCH;
-    const int c = lane - sl * LH_NCH;
-    const unsigned int p = (unsigned int)c * 8;
-    lh_dma_geom geo;
-    lh_dma_geom_init(geo, in_stride);
-    const long long nw = lh_total_waves(stripes);
-    const long long ws = (long long)gridDim.x * LH_WPB;
-    for (long long w = (long long)blockIdx.x * LH_WPB + wid; w < nw; w += ws) {
-        const long long s0 = w * LH_SPW;
-        const int n_sl = (int)((stripes - s0) < LH_SPW ? (stripes - s0) : LH_SPW);
-        const unsigned char *base = in + s0 * in_stride;
-        lh_word acc[LH_M][8];
-#pragma unroll
-        for (int r = 0; r < LH_M; ++r)
-#pragma unroll
-            for (int y = 0; y < 8; ++y)
-#pragma unroll
-                for (int i = 0; i < LH_NW; ++i) acc[r][y].v[i] = 0;
-        lh_issue_stage<0, LH_K>(lds, base, n_sl, geo);
-        if (LH_DMA_D > 2 && LH_NSTAGE(LH_K) > 1) lh_issue_stage<1, LH_K>(lds + LH_SLOT_BYTES, base, n_sl, geo);
-        if (LH_DMA_D > 3 && LH_NSTAGE(LH_K) > 2) lh_issue_stage<2, LH_K>(lds + 2 * LH_SLOT_BYTES, base, n_sl, geo);
-        lh_encode_comb comb(acc);
-        lh_dma_loop<0, LH_K, lh_encode_comb>::run(lds, base, n_sl, geo, sl, p, comb);
-        if (sl < n_sl) {
-            unsigned char *o = out + (s0 + sl) * out_stride + p;
-            const bool tail = (c == LH_NCH - 1) && (LH_TAIL != 8);
-#pragma unroll
-            for (int r = 0; r < LH_M; ++r)
-#pragma unroll
-                for (int y = 0; y < 8; ++y) lh_store_tail(o + (long long)r * LH_BYTES + y * LH_SUB, acc[r][y], tail);
-        }
-    }
-}
-#endif  // LH_DMA
 
 // ------------------------------------------------------------------------ decode
 // Plan record layout: kernels.hpp PlanView (e at [0], out_slot at [16], then src_slot[k],

@@ -19,8 +19,8 @@ import longhair_amd as lh  # noqa: E402
 
 VARIANTS = [
     ("base", {}),
-    ("pipe", {"LONGHAIR_AMD_DEC_PIPE": "1"}),
-    ("pipe_pf2", {"LONGHAIR_AMD_DEC_PIPE": "1", "LONGHAIR_AMD_JIT_DEFINES": "LH_PF_DEC=2"}),
+    ("w12", {"LONGHAIR_AMD_JIT_W": "12"}),
+    ("w12pf2", {"LONGHAIR_AMD_JIT_W": "12", "LONGHAIR_AMD_JIT_DEFINES": "LH_PF=2"}),
 ]
 KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID", "LONGHAIR_AMD_NO_FUSED_PLAN",
          "LONGHAIR_AMD_DEC_PIPE",
