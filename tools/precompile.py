@@ -3,8 +3,10 @@
 shapes, without a GPU, so the first GPU run does not pay the hiprtc compile (the large-m
 windowed modules take minutes).  Usage: python tools/precompile.py [--all | k m bytes ...]"""
 import os
+import subprocess
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import longhair_amd as lh  # noqa: E402
@@ -18,7 +20,15 @@ TESTS = [(29, 2, 1296), (29, 3, 1296), (29, 8, 1296), (4, 2, 16), (10, 6, 8), (1
 
 def main():
     if sys.argv[1:] == ["--all"]:
-        shapes = DEFAULT + TESTS
+        # One child process per shape, largest first: hiprtc is single-threaded and the
+        # k200/m56 module alone takes minutes, so the rest compile beside it.
+        jobs = max(1, min(8, (os.cpu_count() or 2) - 1))
+        cmd = [sys.executable, os.path.abspath(__file__)]
+        with ThreadPoolExecutor(jobs) as pool:
+            runs = list(pool.map(lambda s: subprocess.run(cmd + [str(v) for v in s]), DEFAULT + TESTS))
+        if any(r.returncode for r in runs):
+            sys.exit(1)
+        return
     else:
         args = [int(a) for a in sys.argv[1:]]
         shapes = [tuple(args[i:i + 3]) for i in range(0, len(args), 3)] or DEFAULT
