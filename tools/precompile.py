@@ -28,7 +28,8 @@ def main():
         jobs = max(1, min(8, (os.cpu_count() or 2) - 1))
         cmd = [sys.executable, os.path.abspath(__file__)]
         with ThreadPoolExecutor(jobs) as pool:
-            shapes = [s for s in DEFAULT + TESTS if s not in LARGE]
+            slow = [(250, 3, 24), (128, 32, 8192), (64, 5, 4096)]   # ~400, 120, 80 s alone: start first
+            shapes = slow + [s for s in DEFAULT + TESTS if s not in LARGE and s not in slow]
             runs = list(pool.map(lambda s: subprocess.run(cmd + [str(v) for v in s]), shapes))
         if any(r.returncode for r in runs):
             sys.exit(1)

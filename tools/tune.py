@@ -19,8 +19,9 @@ import longhair_amd as lh  # noqa: E402
 
 VARIANTS = [
     ("base", {}),
-    ("w12", {"LONGHAIR_AMD_JIT_W": "12"}),
-    ("w12pf2", {"LONGHAIR_AMD_JIT_W": "12", "LONGHAIR_AMD_JIT_DEFINES": "LH_PF=2"}),
+    ("noxcd", {"LONGHAIR_AMD_JIT_DEFINES": "LH_XCD=0"}),
+    ("base2", {}),
+    ("noxcd2", {"LONGHAIR_AMD_JIT_DEFINES": "LH_XCD=0"}),
 ]
 KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID", "LONGHAIR_AMD_NO_FUSED_PLAN",
          "LONGHAIR_AMD_DEC_PIPE",
@@ -46,7 +47,7 @@ def main():
     ref_rec = None
     results = {name: ([], []) for name, _ in VARIANTS}
     reps = 3 if m > 12 else 10
-    for rnd in range(3):
+    for rnd in range(int(os.environ.get('TUNE_ROUNDS', '3'))):
         for name, env in VARIANTS:
             for key in KNOBS:
                 os.environ.pop(key, None)
