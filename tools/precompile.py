@@ -12,9 +12,6 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import longhair_amd as lh  # noqa: E402
 
 DEFAULT = [(29, 4, 1296), (128, 32, 8192), (200, 56, 65536)]
-# --all (what build() runs) skips k200/m56: its module alone takes ~10 min of hiprtc and
-# only `bench.py --config k200m56` uses it (precompile it with `... 200 56 65536`).
-LARGE = [(200, 56, 65536)]
 # Further shapes the GPU parity tests run through the specialised path (tests/test_gpu_parity.py).
 TESTS = [(29, 2, 1296), (29, 3, 1296), (29, 8, 1296), (4, 2, 16), (10, 6, 8), (17, 6, 520), (64, 5, 4096),
          (3, 250, 24), (250, 3, 24), (2, 2, 8), (29, 4, 1304), (9, 7, 72), (29, 2, 16), (10, 8, 24),
@@ -28,8 +25,9 @@ def main():
         jobs = max(1, min(8, (os.cpu_count() or 2) - 1))
         cmd = [sys.executable, os.path.abspath(__file__)]
         with ThreadPoolExecutor(jobs) as pool:
-            slow = [(250, 3, 24), (128, 32, 8192), (64, 5, 4096)]   # ~400, 120, 80 s alone: start first
-            shapes = slow + [s for s in DEFAULT + TESTS if s not in LARGE and s not in slow]
+            # ~570, 400, 120, 80 s alone: start first (the GPU tests run k200/m56 too)
+            slow = [(200, 56, 65536), (250, 3, 24), (128, 32, 8192), (64, 5, 4096)]
+            shapes = slow + [s for s in DEFAULT + TESTS if s not in slow]
             runs = list(pool.map(lambda s: subprocess.run(cmd + [str(v) for v in s]), shapes))
         if any(r.returncode for r in runs):
             sys.exit(1)
