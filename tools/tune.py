@@ -19,9 +19,9 @@ import longhair_amd as lh  # noqa: E402
 
 VARIANTS = [
     ("base", {}),
-    ("noxcd", {"LONGHAIR_AMD_JIT_DEFINES": "LH_XCD=0"}),
-    ("base2", {}),
-    ("noxcd2", {"LONGHAIR_AMD_JIT_DEFINES": "LH_XCD=0"}),
+    ("pf2lb4", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=2 LH_ENC_LB=4"}),
+    ("pf2", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=2"}),
+    ("lb4", {"LONGHAIR_AMD_JIT_DEFINES": "LH_ENC_LB=4"}),
 ]
 KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID", "LONGHAIR_AMD_NO_FUSED_PLAN",
          "LONGHAIR_AMD_DEC_PIPE",
