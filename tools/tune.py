@@ -19,9 +19,8 @@ import longhair_amd as lh  # noqa: E402
 
 VARIANTS = [
     ("base", {}),
-    ("pf2lb4", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=2 LH_ENC_LB=4"}),
-    ("pf2", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=2"}),
-    ("lb4", {"LONGHAIR_AMD_JIT_DEFINES": "LH_ENC_LB=4"}),
+    ("noxcd", {"LONGHAIR_AMD_JIT_DEFINES": "LH_XCD=0"}),
+    ("nofused", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1"}),
 ]
 KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID", "LONGHAIR_AMD_NO_FUSED_PLAN",
          "LONGHAIR_AMD_DEC_PIPE",
