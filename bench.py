@@ -8,8 +8,18 @@ originals in a per-stripe shuffled order + e recovery blocks, e = min(k, m) eras
 originals chosen per stripe).  Input bytes per step = 2 * k * bytes * stripes.
 
 Default workload: BASELINE.json configs[1] -- k=29, m=4, 1296-byte blocks, 65536 stripes
-per GPU (weak scaling across ranks: every rank codes its own 65536 stripes, no collective
-on the data path).  N > 1: `python -m torch.distributed.run --nproc-per-node N bench.py`.
+per GPU.  Multi-GPU (one process per GPU, no collective on the data path):
+
+  python bench.py --gpus N                      weak scaling, 65536 stripes per rank
+                                                (N = 8 is BASELINE configs[3]: 524288 stripes)
+  python bench.py --gpus N --global-stripes G   strong scaling: G stripes split with
+                                                longhair_amd.shard.shard_range
+
+With --gpus N > 1 and no torchrun environment, this process starts
+`torch.distributed.run --nproc-per-node N` on itself before touching any GPU and exits
+with its code; under torchrun (WORLD_SIZE set) it must see WORLD_SIZE == N.
+`--dry-run` replaces the HIP work with a CPU stand-in over the gloo backend (tests the
+launcher and the aggregation on a machine without a GPU).
 
 Prints one JSON line (rank 0).  See DESIGN.md for the roofline and cpu_baseline definitions.
 """
@@ -30,45 +40,88 @@ CONFIGS = {
     "k128m32": (128, 32, 8192, 8192, "max"),     # BASELINE configs[2]
     "k200m56": (200, 56, 65536, 64, "random"),   # BASELINE configs[4] (device-resident part)
 }
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+# Measured streaming-read ceiling of this chip (dwordx4 lanes, tools/ubench_ceiling.hip;
+# profiles/r2_ubench_ceiling.txt): what HBM-bound kernels can reach in practice.
+HBM_CEILING_GBS = 6347.3
+HBM_CEILING_SRC = "profiles/r1b_ubench_loads.txt (dwordx4 stream read, best grid)"
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD
+# (SIMD-32, MI355X_MICROARCH.md 'Wave scheduling'), 2.4 GHz -> wave-instructions / s.
+VALU_PEAK_GINSTR = 256 * 4 * 2.4e9 / 2 / 1e9
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="k29m4", choices=sorted(CONFIGS))
-    ap.add_argument("--stripes", type=int, default=0, help="override stripes per GPU")
+    ap.add_argument("--stripes", type=int, default=0, help="override stripes per GPU (weak scaling)")
+    ap.add_argument("--global-stripes", type=int, default=0,
+                    help="strong scaling: total stripes split over the ranks with shard_range")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
-    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU work (thread-seconds) for the baseline")
-    return ap.parse_args()
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="wall-time budget of the CPU baseline leg")
+    ap.add_argument("--dropin-calls", type=int, default=-1,
+                    help="per-call drop-in latency leg (host pointers, one stripe per call); 0 = off")
+    ap.add_argument("--dry-run", action="store_true", help="no HIP work: CPU stand-in step over gloo")
+    return ap.parse_args(argv)
 
 
-def setup_dist():
+# ------------------------------------------------------------------------ launcher
+def launch(args):
+    """Parent of an N-rank run: start torch.distributed.run with one process per GPU on
+    this script and return its exit code.  Runs before anything touches a GPU (the
+    children select their devices themselves); the child is a subprocess, never an exec."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def setup_dist(dry):
     import torch
     import torch.distributed as dist
     from longhair_amd.shard import world_info
     world, rank, local = world_info()
-    torch.cuda.set_device(local)
+    if not dry:
+        torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if dry:
+            dist.init_process_group(backend="gloo")
+        else:
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
     return world, rank, local
 
 
-def barrier(world):
+def barrier(world, dry):
     import torch
     import torch.distributed as dist
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    if not dry:
+        torch.cuda.synchronize()
 
 
-def max_over_ranks(world, value):
-    from longhair_amd.shard import max_over_ranks as mx
-    return value if world == 1 else mx(value, device="cuda")
+def per_rank(world, rank, value, dry):
+    """Every rank's `value`, in rank order (one all-reduce of a one-hot vector)."""
+    if world == 1:
+        return [float(value)]
+    import torch
+    import torch.distributed as dist
+    t = torch.zeros(world, dtype=torch.float64, device="cpu" if dry else "cuda")
+    t[rank] = float(value)
+    dist.all_reduce(t)
+    return [float(v) for v in t.cpu().tolist()]
 
 
+# ------------------------------------------------------------------------ workload
 def make_workload(k, m, nbytes, stripes, seed, erasures="max"):
     """Data X [S, k, bytes] and a decode buffer D [S, k, bytes] whose first slots hold the
     surviving originals of each stripe in a shuffled order and whose last e_s slots
@@ -110,10 +163,87 @@ def make_workload(k, m, nbytes, stripes, seed, erasures="max"):
     return X, D, rows0.to(torch.uint8).contiguous(), idx
 
 
-def cpu_baseline(k, m, nbytes, target_seconds, stripes=4096):
+# ------------------------------------------------------------------ CPU baseline leg
+def effective_cpus():
+    """(threads to use, CPUs in our affinity mask, cgroup CPU quota or None): the
+    threads are the affinity count capped by the cgroup quota the box grants."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    n = aff if quota is None else max(1, min(aff, int(quota)))
+    return n, aff, quota
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def per_call_us(enc, dec, k, m, nbytes, calls, data, blocks_for):
+    """Mean microseconds of one cauchy_256_encode and one cauchy_256_decode call (one
+    stripe, host pointers, the reference's call shape), timed over `calls` calls each.
+    blocks_for(i) -> a fresh ctypes Block array (rows reset to the erased state)."""
+    import numpy as np
+    ptrs = (ctypes.POINTER(ctypes.c_ubyte) * k)()
+    for x in range(k):
+        ptrs[x] = ctypes.cast(data.ctypes.data + x * nbytes, ctypes.POINTER(ctypes.c_ubyte))
+    rec = np.zeros(m * nbytes, dtype=np.uint8)
+    rp = ctypes.c_void_p(rec.ctypes.data)
+    for _ in range(5):
+        assert enc(k, m, ptrs, rp, nbytes) == 0
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        enc(k, m, ptrs, rp, nbytes)
+    t_enc = (time.perf_counter() - t0) / calls
+    arrays = [blocks_for(i, rec) for i in range(calls + 5)]
+    for i in range(5):
+        assert dec(k, m, arrays[i], nbytes) == 0
+    t0 = time.perf_counter()
+    for i in range(calls):
+        dec(k, m, arrays[5 + i], nbytes)
+    t_dec = (time.perf_counter() - t0) / calls
+    return {"encode_us": round(t_enc * 1e6, 2), "decode_us": round(t_dec * 1e6, 2), "calls": calls}
+
+
+def dropin_blocks(k, m, nbytes, data, erased_rows=None):
+    """Factory of decode Block arrays: the first min(k, m) originals erased and replaced
+    by recovery blocks k.. (each array gets its own recovery copies, so every timed call
+    decodes a fresh stripe)."""
+    import numpy as np
+    import lhutil
+    e = min(k, m)
+    keep = [x for x in range(k)][e:]
+    store = []
+
+    def make(i, rec):
+        r = rec.copy()
+        store.append(r)
+        arr = (lhutil.Block * k)()
+        for j, x in enumerate(keep):
+            arr[j].data = ctypes.cast(data.ctypes.data + x * nbytes, ctypes.POINTER(ctypes.c_ubyte))
+            arr[j].row = x
+        for j in range(e):
+            arr[len(keep) + j].data = ctypes.cast(r.ctypes.data + j * nbytes, ctypes.POINTER(ctypes.c_ubyte))
+            arr[len(keep) + j].row = k + j
+        return arr
+    return make
+
+
+def cpu_baseline(k, m, nbytes, budget_s, stripes):
     """Reference codec (oracle/_ref, compiled from the reference sources) -- or, if that
     build is absent, the oracle restatement -- on the host cores, same step definition,
-    a bounded sample of stripes."""
+    a bounded sample of stripes: all granted cores, then one thread; plus the per-call
+    latency of one-stripe encode / decode (the reference API shape)."""
     import numpy as np
     import lhutil
     bench_so = os.path.join(REPO, "oracle", "liblh_cpubench.so")
@@ -131,98 +261,168 @@ def cpu_baseline(k, m, nbytes, target_seconds, stripes=4096):
     data = lhutil.fill(99, stripes * k * nbytes)
     rng = np.random.Generator(np.random.PCG64(5))
     erased = np.stack([rng.choice(k, size=e, replace=False) for _ in range(stripes)]).astype(np.uint8)
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, aff, quota = effective_cpus()
     ok = ctypes.c_int(0)
-    args = lambda passes: (ctypes.cast(enc, ctypes.c_void_p), ctypes.cast(dec, ctypes.c_void_p),
-                           k, m, nbytes, stripes, data.ctypes.data_as(ctypes.c_void_p),
-                           erased.ctypes.data_as(ctypes.c_void_p), e, threads, passes, ctypes.byref(ok))
-    t1 = hb.lhb_run(*args(1))  # warm-up + correctness pass
-    if not ok.value:
+    cpu_s = ctypes.c_double(0.0)
+
+    def run(nstripes, nthreads, passes):
+        t = hb.lhb_run(ctypes.cast(enc, ctypes.c_void_p), ctypes.cast(dec, ctypes.c_void_p), k, m, nbytes,
+                       nstripes, data.ctypes.data_as(ctypes.c_void_p), erased.ctypes.data_as(ctypes.c_void_p), e,
+                       nthreads, passes, ctypes.byref(ok), ctypes.byref(cpu_s))
+        return t, cpu_s.value, bool(ok.value)
+
+    t1, _, good = run(stripes, threads, 1)  # warm-up + correctness pass
+    if not good:
         return {"error": "cpu baseline produced wrong data"}
-    passes = max(1, int(target_seconds / max(t1 * threads, 1e-6)))
-    t = hb.lhb_run(*args(passes))
+    passes = max(1, int(0.65 * budget_s / max(t1, 1e-6)))
+    t, cs, good = run(stripes, threads, passes)
     gbs = 2.0 * k * nbytes * stripes * passes / t / 1e9
-    return {"value": round(gbs, 3), "unit": "GB/s", "cores": threads, "kind": kind,
-            "sample": f"{stripes} stripes x {passes} passes of encode+decode (e={e}), "
-                      f"{threads} threads, {t:.1f} s wall, {t * threads:.1f} s CPU",
-            "ok": bool(ok.value)}
+    s1 = max(2, min(stripes, stripes // max(1, threads)))
+    t1a, _, _ = run(s1, 1, 1)
+    p1 = max(1, int(0.25 * budget_s / max(t1a, 1e-6)))
+    tb, cs1, good1 = run(s1, 1, p1)
+    gbs1 = 2.0 * k * nbytes * s1 * p1 / tb / 1e9
+    out = {"value": round(gbs, 3), "unit": "GB/s", "cores": threads, "kind": kind,
+           "sample": f"{stripes} stripes x {passes} passes of encode+decode (e={e}), {threads} threads: "
+                     f"{t:.1f} s wall, {cs:.1f} s CPU measured; 1 thread: {s1} stripes x {p1} passes, "
+                     f"{tb:.1f} s wall",
+           "value_1thread": round(gbs1, 3), "cpu_seconds": round(cs, 2), "wall_seconds": round(t, 2),
+           "cpu_model": cpu_model(), "cores_affinity": aff, "cgroup_cpu_quota": quota,
+           "ok": bool(good and good1)}
+    calls = max(10, min(2000, int(4e7 / (k * nbytes))))
+    d0 = lhutil.fill(7, k * nbytes)
+    enc.restype = dec.restype = ctypes.c_int
+    out["per_call_us"] = per_call_us(enc, dec, k, m, nbytes, calls, d0, dropin_blocks(k, m, nbytes, d0))
+    return out
 
 
+def dropin_leg(lh, k, m, nbytes, calls):
+    """Per-call latency of the product's drop-in cauchy_256_encode / cauchy_256_decode with
+    host pointers, one stripe per call (the reference API shape), plus the ctypes call
+    overhead of this harness."""
+    import numpy as np
+    import lhutil
+    lib = lh.lib()
+    d0 = lhutil.fill(7, k * nbytes)
+    out = per_call_us(lib.cauchy_256_encode, lib.cauchy_256_decode, k, m, nbytes, calls, d0,
+                      dropin_blocks(k, m, nbytes, d0))
+    # the recovered blocks of the last decoded array must equal the erased originals
+    ref = lhutil.fill(7, k * nbytes).reshape(k, nbytes)
+    rec = np.zeros(m * nbytes, dtype=np.uint8)
+    ptrs = (ctypes.POINTER(ctypes.c_ubyte) * k)()
+    for x in range(k):
+        ptrs[x] = ctypes.cast(d0.ctypes.data + x * nbytes, ctypes.POINTER(ctypes.c_ubyte))
+    assert lib.cauchy_256_encode(k, m, ptrs, ctypes.c_void_p(rec.ctypes.data), nbytes) == 0
+    arr = dropin_blocks(k, m, nbytes, d0)(0, rec)
+    assert lib.cauchy_256_decode(k, m, arr, nbytes) == 0
+    for j in range(k):
+        got = np.ctypeslib.as_array(arr[j].data, shape=(nbytes,))
+        assert got.tobytes() == ref[arr[j].row].tobytes(), "drop-in decode mismatch"
+    noop = lib.cauchy_256_last_error
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        noop()
+    out["ctypes_overhead_us"] = round((time.perf_counter() - t0) / calls * 1e6, 2)
+    out["dispatch"] = lh.dispatch_policy() if hasattr(lh, "dispatch_policy") else "gpu"
+    return out
+
+
+def load_profile(name):
+    path = os.path.join(REPO, "profiles", name)
+    return json.load(open(path)) if os.path.exists(path) else None
+
+
+# ------------------------------------------------------------------------------ main
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args))
+    dry = args.dry_run
     import torch
-    world, rank, local = setup_dist()
-    import longhair_amd as lh
+    world, rank, local = setup_dist(dry)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    from longhair_amd.shard import shard_range
 
     k, m, nbytes, stripes, erasures = CONFIGS[args.config]
     if args.stripes:
         stripes = args.stripes
-    assert lh.cauchy_256_init() == 0, lh.lib().cauchy_256_last_error()
-    lh.prepare(k, m, nbytes, stripes)
-    X, D, rows0, rec_index = make_workload(k, m, nbytes, stripes, seed=1234 + rank, erasures=erasures)
-    e_mean = float((rows0 >= k).sum()) / stripes
-    if rec_index is None:
-        rec_view = D[:, k - m:]     # the encode writes straight into D's recovery slots
-    else:
-        R = torch.empty((stripes, m, nbytes), dtype=torch.uint8, device="cuda")
-        rec_view = R
-        Dflat, Rflat = D.view(-1, nbytes), R.view(-1, nbytes)
-    rows = rows0.clone()
-    stream = torch.cuda.current_stream()
+    scaling = "weak"
+    lo = rank * stripes
+    if args.global_stripes:
+        scaling = "strong"
+        lo, hi = shard_range(args.global_stripes, world, rank)
+        stripes = hi - lo
+    total_stripes = args.global_stripes or stripes * world
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        lh.encode_batch(X, m, recovery=rec_view)
-        if ev is not None:
-            ev[1].record(stream)
-        if rec_index is not None:   # deliver the received recovery blocks to their slots
-            Dflat.index_copy_(0, rec_index[0], Rflat.index_select(0, rec_index[1]))
-        rows.copy_(rows0)
-        if ev is not None:
-            ev[2].record(stream)
-        lh.decode_batch(D, rows, m)
-        if ev is not None:
-            ev[3].record(stream)
+    if dry:
+        import numpy as np
+        buf = np.ones((1 << 20,), dtype=np.uint8)
+        out_buf = np.empty_like(buf)
+        e_mean = float(min(k, m))
+
+        def step(ev=None):
+            np.bitwise_xor(buf, buf, out=out_buf)
+    else:
+        import longhair_amd as lh
+        assert lh.cauchy_256_init() == 0, lh.lib().cauchy_256_last_error()
+        lh.prepare(k, m, nbytes, stripes)
+        X, D, rows0, rec_index = make_workload(k, m, nbytes, stripes, seed=1234 + lo, erasures=erasures)
+        e_mean = float((rows0 >= k).sum()) / max(1, stripes)
+        if rec_index is None:
+            rec_view = D[:, k - m:]     # the encode writes straight into D's recovery slots
+        else:
+            R = torch.empty((stripes, m, nbytes), dtype=torch.uint8, device="cuda")
+            rec_view = R
+            Dflat, Rflat = D.view(-1, nbytes), R.view(-1, nbytes)
+        rows = rows0.clone()
+        stream = torch.cuda.current_stream()  # every kernel below is launched on this stream
+
+        def step(ev=None):
+            if ev is not None:
+                ev[0].record(stream)
+            lh.encode_batch(X, m, recovery=rec_view, stream=stream)
+            if ev is not None:
+                ev[1].record(stream)
+            if rec_index is not None:   # deliver the received recovery blocks to their slots
+                Dflat.index_copy_(0, rec_index[0], Rflat.index_select(0, rec_index[1]))
+            rows.copy_(rows0)
+            if ev is not None:
+                ev[2].record(stream)
+            lh.decode_batch(D, rows, m, stream=stream)
+            if ev is not None:
+                ev[3].record(stream)
 
     for _ in range(args.warmup):
         step()
-    # Correctness gate on the final warm-up state: decoded slots must equal the data.
-    barrier(world)
-    if args.warmup:
+    barrier(world, dry)
+    if args.warmup and not dry:
+        # Correctness gate on the final warm-up state: decoded slots must equal the data.
         order = rows.long().argsort(dim=1)
         restored = torch.gather(D, 1, order.unsqueeze(-1).expand(-1, -1, nbytes))
         assert torch.equal(restored, X), "decode did not restore the data"
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
-    barrier(world)
+    evs = None if dry else [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    barrier(world, dry)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(evs[i])
-    barrier(world)
+        step(None if dry else evs[i])
+    barrier(world, dry)
     t1 = time.perf_counter()
-    elapsed = max_over_ranks(world, t1 - t0)
+    elapsed_ranks = per_rank(world, rank, t1 - t0, dry)
+    stripes_ranks = per_rank(world, rank, stripes, dry)
+    elapsed = max(elapsed_ranks)
 
-    enc_ms = sum(ev[0].elapsed_time(ev[1]) for ev in evs) / args.steps
-    dec_ms = sum(ev[2].elapsed_time(ev[3]) for ev in evs) / args.steps
+    step_bytes = 2.0 * k * nbytes                  # input bytes per stripe per step
     ms_per_step = elapsed / args.steps * 1e3
-    in_bytes = 2.0 * k * nbytes * stripes * world
-    value = in_bytes * args.steps / elapsed / 1e9
-    enc_alg = float(k + m) * nbytes * stripes           # read k, write m blocks per stripe
-    dec_alg = (k + e_mean) * nbytes * stripes           # read k slots, write e blocks
-    enc_k, dec_k = lh.kernel_names(k, m, nbytes)
-    roof = {
-        "encode": {"kernel": "+".join(enc_k), "ms": round(enc_ms, 4),
-                   "achieved": round(enc_alg / (enc_ms * 1e-3) / 1e9, 1)},
-        "decode": {"kernel": "+".join(dec_k), "ms": round(dec_ms, 4),
-                   "achieved": round(dec_alg / (dec_ms * 1e-3) / 1e9, 1)},
-    }
-    dom = "decode" if dec_ms > enc_ms else "encode"
-    traffic = None
-    pmc_path = os.path.join(REPO, "profiles", f"pmc_{args.config}.json")
-    if os.path.exists(pmc_path):
-        pmc = json.load(open(pmc_path))
-        traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch")
+    value = step_bytes * sum(stripes_ranks) * args.steps / elapsed / 1e9
+    per_gpu = [round(step_bytes * s * args.steps / t / 1e9, 2) for s, t in zip(stripes_ranks, elapsed_ranks)]
+    workload = (f"k={k} m={m} bytes={nbytes}, "
+                + (f"{args.global_stripes} stripes split over {world} GPU(s)" if scaling == "strong"
+                   else f"{stripes} stripes per GPU")
+                + f", encode + decode with "
+                + ("e=" + str(min(k, m)) if erasures == "max" else "random e in [1," + str(min(k, m)) + "]")
+                + f" erased originals per stripe (mean {e_mean:.1f})")
     out = {
         "metric": "GB/s of input data encoded+decoded, device-resident, per GPU and whole node",
         "value": round(value, 2),
@@ -232,25 +432,63 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
-        "config": {"workload": f"k={k} m={m} bytes={nbytes}, {stripes} stripes per GPU, encode + "
-                               f"decode with {'e=' + str(min(k, m)) if erasures == 'max' else 'random e in [1,' + str(min(k, m)) + ']'}"
-                               f" erased originals per stripe (mean {e_mean:.1f})",
-                   "k": k, "m": m, "block_bytes": nbytes, "stripes_per_gpu": stripes,
+        "config": {"workload": workload, "k": k, "m": m, "block_bytes": nbytes,
+                   "stripes_per_gpu": stripes if scaling == "weak" else None,
+                   "global_stripes": total_stripes,
                    "parallelism": f"stripes sharded over {world} rank(s), no collective"},
-        "encode_GBps": round(k * nbytes * stripes / (enc_ms * 1e-3) / 1e9, 1),
-        "decode_GBps": round(k * nbytes * stripes / (dec_ms * 1e-3) / 1e9, 1),
-        "roofline": {"bound": "hbm", "kernel": roof[dom]["kernel"], "achieved": roof[dom]["achieved"],
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(roof[dom]["achieved"] / HBM_PEAK_GBS, 4), "traffic": traffic},
-        "kernels": roof,
+        "per_gpu_GBps": per_gpu,
+        "node_GBps": round(value, 2),
     }
-    if rank == 0 and world == 1 and args.cpu_baseline != "off":
-        out["cpu_baseline"] = cpu_baseline(k, m, nbytes, args.cpu_seconds,
-                                           stripes=max(2, min(4096, (256 << 20) // (k * nbytes))))
+    if dry:
+        out["dry_run"] = True
+    else:
+        enc_ms = sum(ev[0].elapsed_time(ev[1]) for ev in evs) / args.steps
+        dec_ms = sum(ev[2].elapsed_time(ev[3]) for ev in evs) / args.steps
+        enc_alg = float(k + m) * nbytes * stripes           # read k, write m blocks per stripe
+        dec_alg = (k + e_mean) * nbytes * stripes           # read k slots, write e blocks
+        enc_k, dec_k = lh.kernel_names(k, m, nbytes)
+        roof = {
+            "encode": {"kernel": "+".join(enc_k), "ms": round(enc_ms, 4),
+                       "achieved": round(enc_alg / (enc_ms * 1e-3) / 1e9, 1)},
+            "decode": {"kernel": "+".join(dec_k), "ms": round(dec_ms, 4),
+                       "achieved": round(dec_alg / (dec_ms * 1e-3) / 1e9, 1)},
+        }
+        dom = "decode" if dec_ms > enc_ms else "encode"
+        pmc = load_profile(f"pmc_{args.config}.json")
+        traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch") if pmc and stripes == CONFIGS[args.config][3] else None
+        hbm = {"bound": "hbm", "kernel": roof[dom]["kernel"], "achieved": roof[dom]["achieved"],
+               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(roof[dom]["achieved"] / HBM_PEAK_GBS, 4),
+               "traffic": traffic, "measured_ceiling": HBM_CEILING_GBS, "ceiling_source": HBM_CEILING_SRC,
+               "frac_of_measured_ceiling": round(roof[dom]["achieved"] / HBM_CEILING_GBS, 4)}
+        out["encode_GBps"] = round(k * nbytes * stripes / (enc_ms * 1e-3) / 1e9, 1)
+        out["decode_GBps"] = round(k * nbytes * stripes / (dec_ms * 1e-3) / 1e9, 1)
+        out["roofline"] = hbm
+        # Large m is VALU-issue-bound: price the dominant kernel against the VALU
+        # peak from its committed SQ_INSTS_VALU count per launch (profiles/sq_<config>.json).
+        sq = load_profile(f"sq_{args.config}.json")
+        if sq and args.config != "k29m4" and stripes == CONFIGS[args.config][3]:
+            names = dec_k if dom == "decode" else enc_k
+            counts = [sq.get("kernels", {}).get(n, {}).get("SQ_INSTS_VALU") for n in names]
+            if all(counts):
+                insts = float(sum(counts))   # every kernel of the phase, over the phase's event time
+                ach = insts / (roof[dom]["ms"] * 1e-3) / 1e9
+                out["roofline"] = {"bound": "valu", "kernel": roof[dom]["kernel"], "achieved": round(ach, 1),
+                                   "peak": round(VALU_PEAK_GINSTR, 1), "unit": "G wave-instr/s",
+                                   "frac": round(ach / VALU_PEAK_GINSTR, 4), "traffic": traffic,
+                                   "valu_insts_per_launch": insts, "valu_source": f"profiles/sq_{args.config}.json",
+                                   "hbm": hbm}
+        out["kernels"] = roof
+    if rank == 0 and world == 1 and not dry:
+        calls = args.dropin_calls if args.dropin_calls >= 0 else max(10, min(2000, int(4e7 / (k * nbytes))))
+        if calls:
+            out["dropin_per_call"] = dropin_leg(lh, k, m, nbytes, calls)
+        if args.cpu_baseline != "off":
+            out["cpu_baseline"] = cpu_baseline(k, m, nbytes, args.cpu_seconds,
+                                               stripes=max(2, min(4096, (256 << 20) // (k * nbytes))))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

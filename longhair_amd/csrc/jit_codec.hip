@@ -618,6 +618,8 @@ static constexpr unsigned char LH_GRAW[LH_M][LH_K] = LH_G_INIT;
 #define LH_P4(n) (((n) + 3) / 4 * 4)
 #define LH_SR (2 * LH_P4(LH_K) + LH_P4(LH_M))  // per-stripe scratch: rows | src map | rec map
 #define LH_NRW ((LH_K + LH_NCH - 1) / LH_NCH)    // Block.row bytes per lane
+// Lanes of one stripe as a ballot mask (LH_NCH may be 64: a 64-bit shift by 64 is UB).
+#define LH_STRIPE_LANES (LH_NCH >= 64 ? ~0ull : ((1ull << (LH_NCH & 63)) - 1))
 
 // The lane's Block.row bytes (slots c, c + LH_NCH, ...), loaded ahead of the plan.
 __device__ __forceinline__ void lh_fused_rows(const lh_lane &l, int c, const unsigned char *__restrict__ rows,
@@ -674,7 +676,7 @@ __device__ __forceinline__ bool lh_fused_plan(const lh_lane &l, int c, int sl, u
         if (r < LH_K + LH_M && (r < LH_K ? lsrc[r] : lrec[r - LH_K]) != i) bad = true;
     }
     const unsigned long long lanes_bad = __ballot(bad);
-    const unsigned long long my = ((1ull << LH_NCH) - 1) << (sl * LH_NCH);
+    const unsigned long long my = LH_STRIPE_LANES << (sl * LH_NCH);
     const bool invalid = (lanes_bad & my) != 0;
     // Recovery slots in array order and missing originals ascending, as per-stripe bit
     // masks gathered with wave ballots (slot/row i = c + t * LH_NCH), then unpacked by
@@ -685,7 +687,7 @@ __device__ __forceinline__ bool lh_fused_plan(const lh_lane &l, int c, int sl, u
         const int i = c + t * LH_NCH;
         const bool isrcv = (i < LH_K) && (lrows[i] >= LH_K);
         const bool iser = (i < LH_K) && (lsrc[i] == 0xFF);
-        const unsigned long long lanes = (1ull << LH_NCH) - 1;
+        const unsigned long long lanes = LH_STRIPE_LANES;
         rcvmask |= ((__ballot(isrcv) >> (sl * LH_NCH)) & lanes) << (t * LH_NCH);
         ermask |= ((__ballot(iser) >> (sl * LH_NCH)) & lanes) << (t * LH_NCH);
     }

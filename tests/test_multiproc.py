@@ -78,3 +78,42 @@ def test_gloo_sharded_encode_matches_single_process(world):
             assert not (set(d) & set(merged))   # shards are disjoint
             merged.update(d)
         assert merged == expect
+
+
+def _bench(*argv, env=None):
+    import json
+    import subprocess
+    import sys
+    e = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(v, None)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(lhutil.REPO, "bench.py"), *argv], capture_output=True,
+                       text=True, timeout=300, env=e, cwd=lhutil.REPO)
+    return r, (json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else None)
+
+
+def test_bench_launcher_weak_world2():
+    """`bench.py --gpus 2` starts torch.distributed.run with two ranks itself (dry run: gloo,
+    CPU stand-in step) and reports the whole-job rate over both ranks."""
+    r, line = _bench("--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["dry_run"]
+    assert len(line["per_gpu_GBps"]) == 2
+    assert line["config"]["global_stripes"] == 2 * 65536
+    # value = all ranks' bytes / slowest rank's time
+    per_step = 2 * 29 * 1296 * 65536 * 2 * 3 / 1e9
+    assert abs(line["value"] - per_step / (line["ms_per_step"] * 3 / 1e3)) / line["value"] < 0.01
+
+
+def test_bench_launcher_strong_world2():
+    r, line = _bench("--gpus", "2", "--dry-run", "--steps", "2", "--warmup", "0", "--global-stripes", "1001")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["config"]["global_stripes"] == 1001 and line["config"]["stripes_per_gpu"] is None
+
+
+def test_bench_rejects_world_mismatch():
+    """Under a torchrun environment the world size must equal --gpus."""
+    r, _ = _bench("--gpus", "2", "--dry-run", "--steps", "1", env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
