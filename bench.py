@@ -43,11 +43,13 @@ CONFIGS = {
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 # Measured streaming-read ceiling of this chip (dwordx4 lanes, tools/ubench_ceiling.hip;
 # profiles/r2_ubench_ceiling.txt): what HBM-bound kernels can reach in practice.
-HBM_CEILING_GBS = 6347.3
-HBM_CEILING_SRC = "profiles/r1b_ubench_loads.txt (dwordx4 stream read, best grid)"
+HBM_CEILING_GBS = 6573.4
+HBM_CEILING_SRC = "profiles/r2_ubench_ceiling.txt (dwordx4 non-temporal stream read, 8 loads in flight, best grid)"
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD
 # (SIMD-32, MI355X_MICROARCH.md 'Wave scheduling'), 2.4 GHz -> wave-instructions / s.
 VALU_PEAK_GINSTR = 256 * 4 * 2.4e9 / 2 / 1e9
+# Measured v_bitop3_b32 issue rate at 8 waves/SIMD (profiles/r2_ubench_ceiling.txt).
+VALU_CEILING_GINSTR = 761.5
 
 
 def parse(argv=None):
@@ -313,7 +315,8 @@ def dropin_leg(lh, k, m, nbytes, calls):
     for x in range(k):
         ptrs[x] = ctypes.cast(d0.ctypes.data + x * nbytes, ctypes.POINTER(ctypes.c_ubyte))
     assert lib.cauchy_256_encode(k, m, ptrs, ctypes.c_void_p(rec.ctypes.data), nbytes) == 0
-    arr = dropin_blocks(k, m, nbytes, d0)(0, rec)
+    make = dropin_blocks(k, m, nbytes, d0)   # holds the recovery copies the Block array points at
+    arr = make(0, rec)
     assert lib.cauchy_256_decode(k, m, arr, nbytes) == 0
     for j in range(k):
         got = np.ctypeslib.as_array(arr[j].data, shape=(nbytes,))
@@ -479,6 +482,8 @@ def main():
                 out["roofline"] = {"bound": "valu", "kernel": roof[dom]["kernel"], "achieved": round(ach, 1),
                                    "peak": round(VALU_PEAK_GINSTR, 1), "unit": "G wave-instr/s",
                                    "frac": round(ach / VALU_PEAK_GINSTR, 4), "traffic": traffic,
+                                   "measured_ceiling": VALU_CEILING_GINSTR,
+                                   "frac_of_measured_ceiling": round(ach / VALU_CEILING_GINSTR, 4),
                                    "valu_insts_per_launch": insts, "valu_source": f"profiles/sq_{args.config}.json",
                                    "hbm": hbm}
         out["kernels"] = roof

@@ -551,6 +551,14 @@ static std::string cache_path(const std::string &src) {
 bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::string *err) {
     const std::string src = jit_source_for(cfg);
     const std::string path = cache_path(src);
+    if (const char *dump = std::getenv("LONGHAIR_AMD_DUMP_SRC")) {  // tuning aid: the generated source
+        const std::string p = std::string(dump) + "/lh_" + std::to_string(cfg.k) + "_" + std::to_string(cfg.m) + "_" +
+                              std::to_string(cfg.bytes) + "_w" + std::to_string(cfg.win) + ".hip";
+        if (FILE *f = fopen(p.c_str(), "w")) {
+            fwrite(src.data(), 1, src.size(), f);
+            fclose(f);
+        }
+    }
     if (!path.empty()) {
         if (FILE *f = fopen(path.c_str(), "rb")) {
             fseek(f, 0, SEEK_END);
