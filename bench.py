@@ -306,8 +306,15 @@ def dropin_leg(lh, k, m, nbytes, calls):
     import lhutil
     lib = lh.lib()
     d0 = lhutil.fill(7, k * nbytes)
+    prev = lh.set_dispatch("gpu")
     out = per_call_us(lib.cauchy_256_encode, lib.cauchy_256_decode, k, m, nbytes, calls, d0,
                       dropin_blocks(k, m, nbytes, d0))
+    # the same calls under the AUTO dispatch policy (include/cauchy_256_dispatch.h)
+    lh.set_dispatch("auto")
+    out["auto"] = per_call_us(lib.cauchy_256_encode, lib.cauchy_256_decode, k, m, nbytes, calls, d0,
+                              dropin_blocks(k, m, nbytes, d0))
+    out["auto"]["host_isa"] = lh.host_isa()
+    lh.set_dispatch(prev)
     # the recovered blocks of the last decoded array must equal the erased originals
     ref = lhutil.fill(7, k * nbytes).reshape(k, nbytes)
     rec = np.zeros(m * nbytes, dtype=np.uint8)
@@ -326,7 +333,7 @@ def dropin_leg(lh, k, m, nbytes, calls):
     for _ in range(calls):
         noop()
     out["ctypes_overhead_us"] = round((time.perf_counter() - t0) / calls * 1e6, 2)
-    out["dispatch"] = lh.dispatch_policy() if hasattr(lh, "dispatch_policy") else "gpu"
+    out["dispatch"] = "gpu (top level) / auto (out['auto'])"
     return out
 
 

@@ -188,6 +188,28 @@ def unframe_batch(packets, blocks=None, rows=None, stream=None):
     return blocks, rows
 
 
+_POLICIES = {"gpu": 0, "auto": 1, "host": 2}
+
+
+def set_dispatch(policy, host_max_work=-1):
+    """Drop-in dispatch policy (include/cauchy_256_dispatch.h): 'gpu' (default), 'auto'
+    (small all-host-memory calls on the host SIMD engine) or 'host'.  Returns the
+    previous policy name.  The library needs a GPU under every policy."""
+    prev = lib().cauchy_256_set_dispatch(_POLICIES[policy], host_max_work)
+    if prev < 0:
+        raise LonghairError(prev, "cauchy_256_set_dispatch")
+    return {v: k for k, v in _POLICIES.items()}[prev]
+
+
+def dispatch_policy():
+    return {v: k for k, v in _POLICIES.items()}[lib().cauchy_256_get_dispatch()]
+
+
+def host_isa():
+    """Instruction set of the host engine on this CPU ('avx512bw', 'avx2', 'scalar')."""
+    return lib().cauchy_256_host_isa().decode()
+
+
 def prepare(k, m, block_bytes, max_stripes=0):
     """Compile the specialised kernels / reserve workspace for a shape (synchronous)."""
     rc = lib().cauchy_256_batch_prepare(k, m, block_bytes, max_stripes)

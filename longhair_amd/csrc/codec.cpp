@@ -5,6 +5,7 @@
 // byte of encode/decode output is produced by GPU kernels (kernels.hip, jit_codec.hip).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -18,6 +19,7 @@
 #include "../../include/cauchy_256_batch.h"
 #include "field.hpp"
 #include "jit.hpp"
+#include "host_codec.hpp"
 #include "kernels.hpp"
 
 namespace lh {
@@ -90,7 +92,7 @@ struct Device {
     // drop-in (single stripe, host pointers) staging
     std::mutex dropin_mu;
     hipStream_t stream = nullptr;
-    DevBuf stage, stage_rows, stage_status;
+    DevBuf stage;
     HostPinned host_stage;
     // host-batch pipeline: per ring slot a stream, device buffers and an event
     std::mutex pipe_mu;
@@ -535,23 +537,68 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
     return kOk;
 }
 
+// ------------------------------------------------------------ drop-in dispatch
+// Where a drop-in call (one stripe, the reference's call shape) runs.  kGpu: always on the
+// device (default).  kAuto: calls whose blocks all live in host memory and whose XOR work
+// is at most g_host_max_work bytes run on the host SIMD engine (host_codec.cpp), the rest
+// on the device.  kHost: every all-host-memory call on the host engine.  Device (or mixed)
+// pointers always go to the device.  The library needs a GPU under every policy.
+enum { kDispatchGpu = 0, kDispatchAuto = 1, kDispatchHost = 2 };
+
+static int env_dispatch() {
+    const char *e = std::getenv("LONGHAIR_AMD_DISPATCH");
+    if (!e) return kDispatchGpu;
+    const std::string v(e);
+    return v == "auto" ? kDispatchAuto : v == "host" ? kDispatchHost : kDispatchGpu;
+}
+static std::atomic<int> g_dispatch{env_dispatch()};
+static std::atomic<long long> g_host_max_work{[] {
+    const char *e = std::getenv("LONGHAIR_AMD_HOST_MAX_WORK");
+    return e ? std::atoll(e) : (4ll << 20);
+}()};
+
+// XOR work of one call in bytes (terms x sub-block bytes): encode = the generator's ones
+// plus the row-0 XOR; decode ~ half of the e x k x 64 bit-matrix entries.
+static long long host_work(int k, int m, int e, int bytes, bool decode) {
+    const long long sub = bytes / 8;
+    if (!decode) return (generator_ones(k, m) - 8ll * k + k) * sub;
+    return 32ll * e * k * sub;
+}
+
+static bool want_host(long long work) {
+    const int pol = g_dispatch.load(std::memory_order_relaxed);
+    return pol == kDispatchHost || (pol == kDispatchAuto && work <= g_host_max_work.load(std::memory_order_relaxed));
+}
+
+// 1 if every pointer is host memory, 0 if every one is device memory, -1 if mixed.
+static int classify(const void *const *ptrs, int n, const void *extra) {
+    int dev = 0;
+    for (int i = 0; i < n; ++i) dev += is_device_pointer(ptrs[i]) ? 1 : 0;
+    const int tot = n + (extra ? 1 : 0);
+    if (extra) dev += is_device_pointer(extra) ? 1 : 0;
+    return dev == 0 ? 1 : dev == tot ? 0 : -1;
+}
+
 static int dropin_encode(int k, int m, const unsigned char *data_ptrs[], void *recovery, int bytes) {
     if (k < 1 || m < 1 || bytes <= 0 || k > 256 || m > 256) return fail(kInvalid, "invalid k, m or block_bytes");
     Device *d = nullptr;
     if (int rc = current_device(&d)) return rc;
+    const int where = classify((const void *const *)data_ptrs, k, recovery);
+    if (where == 1 && want_host(k > 1 && m > 1 && k + m <= 256 && bytes % 8 == 0 ? host_work(k, m, 0, bytes, false) : 0)) {
+        const int rc = host::encode(k, m, (const uint8_t *const *)data_ptrs, (uint8_t *)recovery, bytes);
+        return rc == 0 ? kOk : fail(kInvalid, "k + m > 256 or block_bytes % 8 != 0");
+    }
     std::lock_guard<std::mutex> g(d->dropin_mu);
     const size_t in_n = (size_t)k * bytes, out_n = (size_t)m * bytes;
     LH_HIP(d->stage.reserve(in_n + out_n));
     LH_HIP(d->host_stage.reserve(in_n + out_n));
     hipStream_t st = d->stream;
-    const bool dev_in = is_device_pointer(data_ptrs[0]);
-    const bool dev_out = is_device_pointer(recovery);
     uint8_t *din = d->stage.ptr, *dout = d->stage.ptr + in_n;
-    if (dev_in) {
-        for (int x = 0; x < k; ++x) LH_HIP(hipMemcpyAsync(din + (size_t)x * bytes, data_ptrs[x], bytes, hipMemcpyDefault, st));
-    } else {
+    if (where == 1) {  // gather into pinned staging, one host-to-device copy
         for (int x = 0; x < k; ++x) std::memcpy(d->host_stage.ptr + (size_t)x * bytes, data_ptrs[x], bytes);
         LH_HIP(hipMemcpyAsync(din, d->host_stage.ptr, in_n, hipMemcpyHostToDevice, st));
+    } else {  // device or mixed pointers: the runtime resolves each copy's direction
+        for (int x = 0; x < k; ++x) LH_HIP(hipMemcpyAsync(din + (size_t)x * bytes, data_ptrs[x], bytes, hipMemcpyDefault, st));
     }
     const int rc = encode_batch(k, m, bytes, 1, din, (long long)in_n, dout, (long long)out_n, st, false);
     if (rc != kOk && rc != kInvalid) {
@@ -560,13 +607,13 @@ static int dropin_encode(int k, int m, const unsigned char *data_ptrs[], void *r
     }
     // On kInvalid only recovery block 0 was produced (reference behaviour).
     const size_t n = (rc == kOk) ? out_n : (size_t)bytes;
-    if (dev_out) {
-        LH_HIP(hipMemcpyAsync(recovery, dout, n, hipMemcpyDefault, st));
-        LH_HIP(hipStreamSynchronize(st));
-    } else {
+    if (where == 1) {
         LH_HIP(hipMemcpyAsync(d->host_stage.ptr + in_n, dout, n, hipMemcpyDeviceToHost, st));
         LH_HIP(hipStreamSynchronize(st));
         std::memcpy(recovery, d->host_stage.ptr + in_n, n);
+    } else {
+        LH_HIP(hipMemcpyAsync(recovery, dout, n, hipMemcpyDefault, st));
+        LH_HIP(hipStreamSynchronize(st));
     }
     return rc;
 }
@@ -585,57 +632,65 @@ static int dropin_decode(int k, int m, Block *blocks, int bytes) {
     }
     Device *d = nullptr;
     if (int rc = current_device(&d)) return rc;
-    std::lock_guard<std::mutex> g(d->dropin_mu);
-    const size_t in_n = (size_t)k * bytes;
-    LH_HIP(d->stage.reserve(in_n));
-    LH_HIP(d->stage_rows.reserve(256));
-    LH_HIP(d->stage_status.reserve(16));
-    LH_HIP(d->host_stage.reserve(in_n + 1024));
-    hipStream_t st = d->stream;
-    const bool dev = is_device_pointer(blocks[0].data);
-    uint8_t *hs = d->host_stage.ptr;
-    uint8_t *hrows = hs + in_n;  // [0,256) rows in, [256,512) rows out, [512] status
-    for (int i = 0; i < k; ++i) hrows[i] = blocks[i].row;
-    if (dev) {
-        for (int i = 0; i < k; ++i)
-            LH_HIP(hipMemcpyAsync(d->stage.ptr + (size_t)i * bytes, blocks[i].data, bytes, hipMemcpyDefault, st));
-    } else {
-        for (int i = 0; i < k; ++i) std::memcpy(hs + (size_t)i * bytes, blocks[i].data, bytes);
-        LH_HIP(hipMemcpyAsync(d->stage.ptr, hs, in_n, hipMemcpyHostToDevice, st));
+    const void *ptrs[256];
+    for (int i = 0; i < k; ++i) ptrs[i] = blocks[i].data;
+    const int where = classify(ptrs, k, nullptr);
+    if (where == 1 && want_host(m == 1 ? (long long)k * bytes : host_work(k, m, n_rcv, bytes, true))) {
+        if (m == 1) {
+            host::decode_m1(k, blocks, bytes);
+            return kOk;
+        }
+        return host::decode(k, m, blocks, bytes) == 0 ? kOk : fail(kInvalid, "invalid or duplicated block rows");
     }
-    LH_HIP(hipMemcpyAsync(d->stage_rows.ptr, hrows, k, hipMemcpyHostToDevice, st));
-    int rc = decode_batch(k, m, bytes, 1, d->stage.ptr, (long long)in_n, d->stage_rows.ptr,
-                          (int8_t *)d->stage_status.ptr, st, false);
+    std::lock_guard<std::mutex> g(d->dropin_mu);
+    // Device and host staging share one layout: [k blocks][256 rows][16 status], so each
+    // direction is a single copy for host pointers.
+    const size_t in_n = (size_t)k * bytes, tot = in_n + 256 + 16;
+    LH_HIP(d->stage.reserve(tot));
+    LH_HIP(d->host_stage.reserve(tot));
+    hipStream_t st = d->stream;
+    uint8_t *hs = d->host_stage.ptr, *ds = d->stage.ptr;
+    uint8_t *hrows = hs + in_n, *drows = ds + in_n;
+    for (int i = 0; i < k; ++i) hrows[i] = blocks[i].row;
+    if (where == 1) {
+        for (int i = 0; i < k; ++i) std::memcpy(hs + (size_t)i * bytes, blocks[i].data, bytes);
+        LH_HIP(hipMemcpyAsync(ds, hs, in_n + k, hipMemcpyHostToDevice, st));
+    } else {
+        for (int i = 0; i < k; ++i)
+            LH_HIP(hipMemcpyAsync(ds + (size_t)i * bytes, blocks[i].data, bytes, hipMemcpyDefault, st));
+        LH_HIP(hipMemcpyAsync(drows, hrows, k, hipMemcpyHostToDevice, st));
+    }
+    int rc = decode_batch(k, m, bytes, 1, ds, (long long)in_n, drows, (int8_t *)(drows + 256), st, false);
     if (rc != kOk) {
         (void)hipStreamSynchronize(st);
         return rc;
     }
-    uint8_t *hout = hrows + 256;
-    LH_HIP(hipMemcpyAsync(hout, d->stage_rows.ptr, k, hipMemcpyDeviceToHost, st));
-    LH_HIP(hipMemcpyAsync(hout + 256, d->stage_status.ptr, 1, hipMemcpyDeviceToHost, st));
     // Slots whose bytes can change: recovery slots (m > 1); for m == 1 the recovery slot
     // or, when none is present, slot 0 (cauchy_decode_m1's quirk).
-    std::vector<int> changed;
+    int changed[256], nch = 0;
     if (m == 1) {
         int out = 0;
         for (int i = 0; i < k; ++i) if (blocks[i].row >= k) out = i;
-        changed.push_back(out);
+        changed[nch++] = out;
     } else {
-        for (int i = 0; i < k; ++i) if (blocks[i].row >= k) changed.push_back(i);
+        for (int i = 0; i < k; ++i) if (blocks[i].row >= k) changed[nch++] = i;
     }
-    if (dev) {
-        for (int i : changed)
-            LH_HIP(hipMemcpyAsync(blocks[i].data, d->stage.ptr + (size_t)i * bytes, bytes, hipMemcpyDefault, st));
+    if (where == 1) {  // one copy back: blocks, rows, status
+        LH_HIP(hipMemcpyAsync(hs, ds, tot, hipMemcpyDeviceToHost, st));
         LH_HIP(hipStreamSynchronize(st));
     } else {
-        for (int i : changed)
-            LH_HIP(hipMemcpyAsync(hs + (size_t)i * bytes, d->stage.ptr + (size_t)i * bytes, bytes, hipMemcpyDeviceToHost, st));
+        LH_HIP(hipMemcpyAsync(hrows, drows, 256 + 16, hipMemcpyDeviceToHost, st));
         LH_HIP(hipStreamSynchronize(st));
     }
-    if ((int8_t)hout[256] != 0) return fail(kInvalid, "invalid or duplicated block rows");
-    if (!dev)
-        for (int i : changed) std::memcpy(blocks[i].data, hs + (size_t)i * bytes, bytes);
-    for (int i = 0; i < k; ++i) blocks[i].row = hout[i];
+    if ((int8_t)hrows[256] != 0) return fail(kInvalid, "invalid or duplicated block rows");
+    if (where == 1) {
+        for (int j = 0; j < nch; ++j) std::memcpy(blocks[changed[j]].data, hs + (size_t)changed[j] * bytes, bytes);
+    } else {
+        for (int j = 0; j < nch; ++j)
+            LH_HIP(hipMemcpyAsync(blocks[changed[j]].data, ds + (size_t)changed[j] * bytes, bytes, hipMemcpyDefault, st));
+        LH_HIP(hipStreamSynchronize(st));
+    }
+    for (int i = 0; i < k; ++i) blocks[i].row = hrows[i];
     return kOk;
 }
 
@@ -806,5 +861,15 @@ LH_API int cauchy_256_unframe_batch(int k, int block_bytes, int stripes, const v
 }
 
 LH_API const char *cauchy_256_last_error(void) { return lh::g_last_error.c_str(); }
+
+LH_API int cauchy_256_set_dispatch(int policy, long long host_max_work) {
+    if (policy < lh::kDispatchGpu || policy > lh::kDispatchHost) return lh::fail(lh::kInvalid, "unknown dispatch policy");
+    if (host_max_work >= 0) lh::g_host_max_work.store(host_max_work);
+    return lh::g_dispatch.exchange(policy);
+}
+
+LH_API int cauchy_256_get_dispatch(void) { return lh::g_dispatch.load(); }
+
+LH_API const char *cauchy_256_host_isa(void) { return lh::host::isa_name(); }
 
 }  // extern "C"

@@ -390,9 +390,15 @@ __device__ __forceinline__ const unsigned char *lh_slot_ptr(unsigned int slot, c
 // Phase A streams LH_K data columns (erased ones read the zero page) and then the LH_M
 // recovery rows (absent ones read the zero page) through one prefetch ring, so the
 // recovery loads are in flight while the last data columns combine.
-#define LH_DCOLS (LH_K + LH_M)
+#ifndef LH_COLS_PROBE
+#define LH_COLS_PROBE 0  // timing probe only: phase A streams the k data columns, no recovery rows
+#endif
+#define LH_DCOLS (LH_COLS_PROBE ? LH_K : LH_K + LH_M)
 #ifndef LH_PF_DEC
 #define LH_PF_DEC 1  // decode prefetch depth (tools/tune.py, fused plan: 1 > 2 > 3)
+#endif
+#ifndef LH_REFILL
+#define LH_REFILL 0  // decode ring: refill a slot right after its column is combined (no staging copy)
 #endif
 #ifndef LH_PREP_FIRST
 #define LH_PREP_FIRST 0  // fused decode: solve the plan before (1) or while (0) the first columns load
@@ -445,6 +451,16 @@ struct lh_unroll_decode {
                                                const unsigned char *base, const unsigned char *zero,
                                                const unsigned int (&srcw)[LH_NSRC], const unsigned int (&recw)[LH_NREC]) {
         if (X + LH_PF_DEC < LH_DCOLS) {
+#if LH_REFILL
+            // Combine column X, then refill its ring slot with column X + PF: no staging
+            // copy (16 VGPRs fewer), and the refill's address passes through an empty asm
+            // after the accumulator pin, so the load cannot be hoisted above the combine.
+            lh_dcombine<X>(acc, ring[X % LH_PF_DEC]);
+            lh_opaque(acc);
+            const unsigned char *src = lh_dcol_src<(X + LH_PF_DEC < LH_DCOLS ? X + LH_PF_DEC : 0)>(srcw, recw, base, zero);
+            asm volatile("" : "+v"(src));
+            lh_load_col(ring[X % LH_PF_DEC], src, zero);
+#else
             const unsigned char *src = lh_dcol_src<(X + LH_PF_DEC < LH_DCOLS ? X + LH_PF_DEC : 0)>(srcw, recw, base, zero);
             lh_word nxt[8];
             lh_load_col(nxt, src, zero);
@@ -452,6 +468,7 @@ struct lh_unroll_decode {
             lh_opaque(acc);
 #pragma unroll
             for (int b = 0; b < 8; ++b) ring[X % LH_PF_DEC][b] = nxt[b];
+#endif
         } else {
             lh_dcombine<X>(acc, ring[X % LH_PF_DEC]);
             lh_opaque(acc);
@@ -510,9 +527,20 @@ __device__ __forceinline__ void lh_dec_phase_a(lh_word (&v)[LH_M][8], lh_word (&
 // Phase B: D_{E_i} = sum_r B(coef[i][r]) V_r with the per-stripe inverse, by Horner over
 // the coefficient bits: B(c) v = B(2)(...B(2)(c_7 v)...) + c_0 v, one v_bitop3 masked XOR
 // per (row, bit, sub-row); the recovered blocks go to the plan's output slots.
+#ifndef LH_PB_PROBE
+#define LH_PB_PROBE 0  // timing probe only (tools/tune.py): V_i stored as output i, no phase-B XORs
+#endif
 __device__ __forceinline__ void lh_dec_phase_b(const lh_word (&v)[LH_M][8], const lh_plan_regs &pr,
                                                unsigned char *base) {
     const int e = pr.e;
+#if LH_PB_PROBE
+#pragma unroll
+    for (int i = 0; i < LH_EMAX; ++i)
+        if (i < e)
+#pragma unroll
+            for (int y = 0; y < 8; ++y) lh_store(base + (long long)LH_BYTE(pr.outw, i) * LH_BYTES + y * LH_SUB, v[i][y]);
+    return;
+#endif
     const unsigned int(&coefw)[LH_NCOEF] = pr.coefw;
     const unsigned int(&outw)[LH_NOUT] = pr.outw;
 #pragma unroll
@@ -775,6 +803,14 @@ __device__ __forceinline__ void lh_fused_solve::operator()(lh_plan_regs &pr) con
     if (c == 0)
 #pragma unroll
         for (int i = 0; i < LH_EMAX; ++i) if (i < nr) grow[rs[i]] = (unsigned char)er[i];
+    // Materialise the packed plan here, so the solve's matrices die before phase A: left
+    // alone, the compiler sinks the packing into phase B and keeps the e x e inverse and
+    // the row lists live across all k + m columns (k29/m4: 218 -> 158 VGPRs, 2 -> 3
+    // waves/SIMD).
+#pragma unroll
+    for (int q = 0; q < LH_NCOEF; ++q) asm volatile("" : "+v"(pr.coefw[q]));
+#pragma unroll
+    for (int q = 0; q < LH_NOUT; ++q) asm volatile("" : "+v"(pr.outw[q]));
 }
 
 #ifndef LH_DEC_LB

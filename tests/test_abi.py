@@ -12,7 +12,7 @@ REPO = lhutil.REPO
 
 def _declared_functions():
     names = set()
-    for h in ("cauchy_256.h", "cauchy_256_batch.h"):
+    for h in ("cauchy_256.h", "cauchy_256_batch.h", "cauchy_256_dispatch.h"):
         text = open(os.path.join(REPO, "include", h)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         for m in re.finditer(r"^\s*(?:extern\s+)?(?:const\s+)?\w+\s*\*?\s*(\w+)\s*\(", text, flags=re.M):
@@ -73,3 +73,21 @@ def test_no_silent_cpu_path():
     rec = np.zeros(m * nbytes, dtype=np.uint8)
     assert longhair_amd.cauchy_256_encode(k, m, ptrs, rec, nbytes) == -2
     assert not rec.any()
+    # the host SIMD engine of the drop-in dispatch policy is no fallback either
+    for policy in ("host", "auto"):
+        prev = longhair_amd.set_dispatch(policy)
+        try:
+            assert longhair_amd.cauchy_256_encode(k, m, ptrs, rec, nbytes) == -2
+            assert not rec.any()
+        finally:
+            longhair_amd.set_dispatch(prev)
+
+
+def test_dispatch_policy_api():
+    import longhair_amd
+    assert longhair_amd.dispatch_policy() == "gpu"  # default without LONGHAIR_AMD_DISPATCH
+    assert longhair_amd.set_dispatch("auto") == "gpu"
+    assert longhair_amd.dispatch_policy() == "auto"
+    assert longhair_amd.set_dispatch("gpu") == "auto"
+    assert longhair_amd.lib().cauchy_256_set_dispatch(7, -1) == -1
+    assert longhair_amd.host_isa() in ("avx512bw", "avx2", "scalar")

@@ -34,6 +34,23 @@ def _load(name):
     return json.load(open(os.path.join(lhutil.GOLDEN, name)))
 
 
+@pytest.fixture(params=["gpu", "host-avx512bw", "host-avx2", "host-scalar"])
+def policy(request, lh, monkeypatch):
+    """Drop-in dispatch policy (include/cauchy_256_dispatch.h): every drop-in test runs on
+    the GPU and on each instruction-set level of the host SIMD engine."""
+    if request.param == "gpu":
+        prev = lh.set_dispatch("gpu")
+    else:
+        isa = request.param.split("-")[1]
+        if isa == "avx512bw" and lh.host_isa() != "avx512bw":
+            pytest.skip("host CPU without AVX-512BW")
+        monkeypatch.setenv("LONGHAIR_AMD_HOST_ISA", isa)
+        prev = lh.set_dispatch("host")
+        assert lh.host_isa() == isa
+    yield request.param
+    lh.set_dispatch(prev)
+
+
 class DropIn(lhutil._Codec):
     """The product's drop-in entry points driven exactly like the reference (host memory)."""
 
@@ -50,7 +67,7 @@ def _gpu_tensor(arr):
 # ----------------------------------------------------------------- drop-in ABI
 
 
-def test_dropin_encode_golden_grid(lh):
+def test_dropin_encode_golden_grid(lh, policy):
     codec = DropIn(lh)
     for k, m, bytes_, seed, rc, digest in _load("encode_grid.json")["cases"]:
         data = lhutil.fill(seed, k * bytes_)
@@ -61,7 +78,7 @@ def test_dropin_encode_golden_grid(lh):
         assert lhutil.h64(rec) == digest, (k, m, bytes_)
 
 
-def test_dropin_encode_full_bytes(lh):
+def test_dropin_encode_full_bytes(lh, policy):
     codec = DropIn(lh)
     for c in _load("encode_full.json"):
         data = np.frombuffer(bytes.fromhex(c["data"]), dtype=np.uint8)
@@ -70,7 +87,7 @@ def test_dropin_encode_full_bytes(lh):
         assert rec.tobytes().hex() == c["recovery"]
 
 
-def test_dropin_decode_golden(lh):
+def test_dropin_decode_golden(lh, policy):
     codec = DropIn(lh)
     for c in _load("decode_cases.json"):
         k, m, bytes_ = c["k"], c["m"], c["bytes"]
@@ -83,6 +100,79 @@ def test_dropin_decode_golden(lh):
         assert rc == c["rc"], c["tag"]
         assert rows == c["rows_out"], c["tag"]
         assert [lhutil.h64(b) for b in bufs] == c["digests"], c["tag"]
+
+
+@pytest.mark.parametrize("k,m,nbytes,cases", [(29, 4, 1296, 40), (29, 1, 1296, 6), (128, 32, 8192, 3),
+                                              (200, 56, 65536, 1), (17, 6, 520, 20), (250, 6, 16, 4), (2, 2, 8, 8)])
+def test_dropin_random_vs_oracle(lh, oracle, policy, k, m, nbytes, cases):
+    """Drop-in encode + decode of random stripes (random e, random recovery rows, shuffled
+    slots) against the oracle, on the GPU and on the host engine."""
+    codec = DropIn(lh)
+    rng = np.random.Generator(np.random.PCG64(k * 1000 + m))
+    for c in range(cases):
+        data = lhutil.fill(int(rng.integers(0, 2**31)), k * nbytes).reshape(k, nbytes)
+        rc, rec = codec.encode(k, m, data, nbytes)
+        rc_o, rec_o = oracle.encode(k, m, data, nbytes)
+        assert rc == rc_o == 0 and rec.tobytes() == rec_o.tobytes(), (k, m, c)
+        rec = rec.reshape(m, nbytes)
+        e = int(rng.integers(0, min(k, m) + 1))
+        slots, rows = lhutil.erasure_case(int(rng.integers(0, 2**31)), k, m, e)
+        bufs = [(data[x] if kind == "d" else rec[x]).copy() for kind, x in slots]
+        exp = [b.copy() for b in bufs]
+        rc, got_rows = codec.decode(k, m, bufs, rows, nbytes)
+        rc_o, exp_rows = oracle.decode(k, m, exp, rows, nbytes)
+        assert rc == rc_o and got_rows == exp_rows, (k, m, c, e)
+        assert all(a.tobytes() == b.tobytes() for a, b in zip(bufs, exp)), (k, m, c, e)
+
+
+def test_dropin_invalid_rows_untouched(lh, policy):
+    """Duplicate or out-of-range rows: -1 and the blocks untouched (documented deviation:
+    undefined behaviour in the reference, cauchy_256.cpp:612-614, :733)."""
+    codec = DropIn(lh)
+    k, m, nbytes = 6, 3, 16
+    for rows in ([0, 1, 2, 3, 6, 6], [0, 1, 2, 3, 4, 9]):
+        bufs = [lhutil.fill(i, nbytes) for i in range(k)]
+        before = [b.copy() for b in bufs]
+        rc, got = codec.decode(k, m, bufs, rows, nbytes)
+        assert rc == -1 and got == rows
+        assert all(a.tobytes() == b.tobytes() for a, b in zip(bufs, before))
+
+
+def test_dropin_auto_policy_routes_by_size(lh, oracle):
+    """AUTO: a small all-host call runs on the host engine, a large one on the GPU; both
+    return the oracle's bytes."""
+    codec = DropIn(lh)
+    prev = lh.set_dispatch("auto", 1 << 20)
+    try:
+        for k, m, nbytes in ((29, 4, 1296), (128, 32, 8192)):
+            data = lhutil.fill(k + m, k * nbytes)
+            rc, rec = codec.encode(k, m, data, nbytes)
+            assert rc == 0 and rec.tobytes() == oracle.encode(k, m, data, nbytes)[1].tobytes()
+    finally:
+        lh.set_dispatch(prev, 4 << 20)
+
+
+def test_dropin_mixed_pointers(lh):
+    """One call with host and device blocks (classified per pointer) gives the
+    oracle's bytes under every policy."""
+    import torch
+    k, m, nbytes = 29, 4, 1296
+    data = lhutil.fill(78, k * nbytes)
+    ref_rc, ref_rec = lhutil.Oracle().encode(k, m, data, nbytes)
+    d = _gpu_tensor(data)
+    ptrs = (ctypes.POINTER(ctypes.c_ubyte) * k)()
+    for x in range(k):
+        addr = (d.data_ptr() if x % 2 else data.ctypes.data) + x * nbytes
+        ptrs[x] = ctypes.cast(addr, ctypes.POINTER(ctypes.c_ubyte))
+    for pol in ("gpu", "host"):
+        prev = lh.set_dispatch(pol)
+        try:
+            rec = np.zeros(m * nbytes, dtype=np.uint8)
+            assert lh.cauchy_256_encode(k, m, ptrs, rec, nbytes) == 0
+            assert rec.tobytes() == ref_rec.tobytes()
+        finally:
+            lh.set_dispatch(prev)
+    del torch
 
 
 def test_dropin_device_pointers(lh):

@@ -30,6 +30,10 @@ if has large; then
     cat "$OUT/bench_$cfg.json"
   done
 fi
+if has tune; then
+  timeout -k 10 600 python tools/tune.py ${TUNE_SHAPE:-} > "$OUT/tune.txt" 2>&1 || { tail -20 "$OUT/tune.txt"; exit 1; }
+  tail -8 "$OUT/tune.txt"
+fi
 if has ubench; then
   timeout -k 10 120 tools/ubench_ceiling > "$OUT/ubench_ceiling.txt" 2>&1 || { tail -20 "$OUT/ubench_ceiling.txt"; exit 1; }
   cat "$OUT/ubench_ceiling.txt"
