@@ -40,22 +40,45 @@ static int fail(int code, const std::string &msg) {
             return fail(kHipError, std::string(#expr) + ": " + hipGetErrorString(e_));     \
     } while (0)
 
-// Grow-only device buffer.
+// Grow-only device buffer.  Growing never synchronises the device:
+//  - reserve(n): for buffers whose every earlier use the caller has already waited for
+//    (drop-in staging, host-batch pipelines: both end in a stream synchronisation);
+//  - reserve(n, st): for buffers used on one stream only (per-stream workspaces): the old
+//    allocation is released and the new one allocated in that stream's order
+//    (hipFreeAsync / hipMallocAsync), so later kernels on `st` see the new buffer and
+//    earlier ones finish with the old.
 struct DevBuf {
     uint8_t *ptr = nullptr;
     size_t size = 0;
+    bool stream_ordered = false;
     hipError_t reserve(size_t n) {
         if (n <= size) return hipSuccess;
-        if (ptr) {
-            hipError_t e = hipDeviceSynchronize();  // the old buffer may still be in use
-            if (e != hipSuccess) return e;
-            (void)hipFree(ptr);
-            ptr = nullptr;
-            size = 0;
-        }
+        release(nullptr);
         hipError_t e = hipMalloc(&ptr, n);
         if (e == hipSuccess) size = n;
+        else ptr = nullptr;
         return e;
+    }
+    hipError_t reserve(size_t n, hipStream_t st) {
+        if (n <= size) return hipSuccess;
+        release(st);
+        hipError_t e = hipMallocAsync((void **)&ptr, n, st);
+        if (e == hipSuccess) {
+            size = n;
+            stream_ordered = true;
+        } else {
+            ptr = nullptr;
+        }
+        return e;
+    }
+    void release(hipStream_t st) {
+        if (ptr) {
+            if (stream_ordered) (void)hipFreeAsync(ptr, st);
+            else (void)hipFree(ptr);
+        }
+        ptr = nullptr;
+        size = 0;
+        stream_ordered = false;
     }
 };
 
@@ -87,6 +110,7 @@ struct Device {
     int16_t *gf_log = nullptr;           // 256 x int16
     std::map<std::pair<int, int>, uint8_t *> generators;  // (k, m) -> m x k on device
     DevBuf zero;                         // zero page (>= block bytes)
+    std::vector<uint8_t *> retired;      // outgrown zero pages (never freed: see zero_page)
     std::map<hipStream_t, Workspace> ws;
     JitCache jit;
     // drop-in (single stripe, host pointers) staging
@@ -141,11 +165,23 @@ static int device_generator(Device *d, int k, int m, const uint8_t **out) {
     return kOk;
 }
 
+// Zero pages: kZeroPages copies of a zero block (the specialised decode spreads its stripes
+// over them, LH_NZ), shared by every stream.  A larger one replaces it without a
+// device synchronisation: the old page stays allocated (kernels in flight on other streams
+// may still read it) and the new page is cleared on the null stream, which this thread
+// waits for before publishing the pointer (non-blocking streams are not stalled).
+static constexpr size_t kZeroPages = 64;
 static int zero_page(Device *d, size_t bytes, const uint8_t **out) {
+    bytes *= kZeroPages;
     std::lock_guard<std::mutex> g(d->mu);
     if (d->zero.size < bytes) {
-        LH_HIP(d->zero.reserve(bytes));
-        LH_HIP(hipMemset(d->zero.ptr, 0, d->zero.size));
+        uint8_t *p = nullptr;
+        LH_HIP(hipMalloc(&p, bytes));
+        LH_HIP(hipMemsetAsync(p, 0, bytes, nullptr));
+        LH_HIP(hipStreamSynchronize(nullptr));
+        if (d->zero.ptr) d->retired.push_back(d->zero.ptr);
+        d->zero.ptr = p;
+        d->zero.size = bytes;
     }
     *out = d->zero.ptr;
     return kOk;
@@ -154,8 +190,8 @@ static int zero_page(Device *d, size_t bytes, const uint8_t **out) {
 static int workspace(Device *d, hipStream_t st, size_t plan_bytes, size_t work_bytes, Workspace **out) {
     std::lock_guard<std::mutex> g(d->mu);
     Workspace &w = d->ws[st];
-    LH_HIP(w.plan.reserve(plan_bytes));
-    if (work_bytes) LH_HIP(w.work.reserve(work_bytes));
+    LH_HIP(w.plan.reserve(plan_bytes, st));
+    if (work_bytes) LH_HIP(w.work.reserve(work_bytes, st));
     *out = &w;
     return kOk;
 }
@@ -438,6 +474,17 @@ static int pipe_streams(Device *d) {
     return kOk;
 }
 
+// On every exit from a host-batch call (errors included), wait for the three pipe
+// streams: earlier chunks' asynchronous copies into or out of the caller's (pinned)
+// buffers must not outlive the call.
+struct PipeDrain {
+    Device *d;
+    ~PipeDrain() {
+        for (auto s : d->pipe_stream)
+            if (s) (void)hipStreamSynchronize(s);
+    }
+};
+
 static int auto_chunk(long long stripe_bytes, int stripes, int chunk) {
     if (chunk > 0) return chunk < stripes ? chunk : stripes;
     long long c = (64ll << 20) / (stripe_bytes > 0 ? stripe_bytes : 1);  // ~64 MiB per chunk
@@ -455,6 +502,7 @@ static int host_encode_batch(int k, int m, int bytes, int stripes, const uint8_t
     if (int rc = current_device(&d)) return rc;
     std::lock_guard<std::mutex> g(d->pipe_mu);
     if (int rc = pipe_streams(d)) return rc;
+    PipeDrain drain{d};
     const long long in_sz = (long long)k * bytes, out_sz = (long long)m * bytes;
     chunk = auto_chunk(in_sz + out_sz, stripes, chunk);
     for (int i = 0; i < 3; ++i) {
@@ -488,6 +536,7 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
     if (int rc = current_device(&d)) return rc;
     std::lock_guard<std::mutex> g(d->pipe_mu);
     if (int rc = pipe_streams(d)) return rc;
+    PipeDrain drain{d};
     const long long sz = (long long)k * bytes;
     chunk = auto_chunk(sz, stripes, chunk);
     for (int i = 0; i < 3; ++i) {

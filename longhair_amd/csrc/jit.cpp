@@ -540,17 +540,24 @@ static std::string cache_dir() {
 }
 
 static std::string cache_path(const std::string &src) {
+    // Key: generated source, compile options and the hiprtc / HIP runtime versions, so a
+    // cache made by another ROCm is never loaded.
     std::string key = src;
     for (const char *o : kOpts) key += std::string("\n") + o;
+    int major = 0, minor = 0, rt = 0;
+    (void)hiprtcVersion(&major, &minor);
+    (void)hipRuntimeGetVersion(&rt);
+    key += "\nhiprtc " + std::to_string(major) + "." + std::to_string(minor) + " hip " + std::to_string(rt);
     char name[64];
     snprintf(name, sizeof(name), "/lh_%016llx.co", (unsigned long long)fnv1a(key));
     const std::string d = cache_dir();
     return d.empty() ? "" : d + name;
 }
 
-bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::string *err) {
+bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::string *err, bool fresh) {
     const std::string src = jit_source_for(cfg);
     const std::string path = cache_path(src);
+    if (fresh && !path.empty()) unlink(path.c_str());  // a cached object the loader rejected
     if (const char *dump = std::getenv("LONGHAIR_AMD_DUMP_SRC")) {  // tuning aid: the generated source
         const std::string p = std::string(dump) + "/lh_" + std::to_string(cfg.k) + "_" + std::to_string(cfg.m) + "_" +
                               std::to_string(cfg.bytes) + "_w" + std::to_string(cfg.win) + ".hip";
@@ -614,8 +621,13 @@ const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err) {
     JitKernels kern;
     kern.cfg = cfg;
     if (hipModuleLoadData(&kern.module, code.data()) != hipSuccess) {
-        *err = "hipModuleLoadData failed for the specialised kernels";
-        return nullptr;
+        // A damaged or foreign cached object: drop it and compile once more.
+        (void)hipGetLastError();
+        if (!compile_code_object(cfg, &code, err, true)) return nullptr;
+        if (hipModuleLoadData(&kern.module, code.data()) != hipSuccess) {
+            *err = "hipModuleLoadData failed for the specialised kernels";
+            return nullptr;
+        }
     }
     auto fn = [&](const char *name) -> hipFunction_t {
         hipFunction_t f = nullptr;

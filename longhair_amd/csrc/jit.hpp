@@ -67,6 +67,7 @@ std::string jit_source_for(const JitConfig &cfg);
 
 // Compile (or fetch from the on-disk cache) the code object of a configuration.  Needs
 // no GPU, so build steps can pre-populate the cache.
-bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::string *err);
+// fresh: ignore (and delete) a cached object.
+bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::string *err, bool fresh = false);
 
 }  // namespace lh

@@ -415,6 +415,10 @@ __device__ __forceinline__ const unsigned char *lh_dcol_src(const unsigned int (
 // Column load of the decode ring.  LH_ZSKIP: lanes whose column is absent (erased
 // original, missing recovery row) do not load the zero page, they zero their words under
 // the exec mask, so no wave-instruction fetches from one hot 1.3-KB page.
+#ifndef LH_NZ
+#define LH_NZ 1  // zero pages the stripes spread over (the host allocates 64): one hot page
+                 // concentrates every erased column's reads on a few L2 channels
+#endif
 #ifndef LH_ZSKIP
 #define LH_ZSKIP 0  // measured equal (0.6255 vs 0.6212 ms, k29/m4): the zero page stays L2-resident
 #endif
@@ -457,9 +461,13 @@ struct lh_unroll_decode {
             // after the accumulator pin, so the load cannot be hoisted above the combine.
             lh_dcombine<X>(acc, ring[X % LH_PF_DEC]);
             lh_opaque(acc);
-            const unsigned char *src = lh_dcol_src<(X + LH_PF_DEC < LH_DCOLS ? X + LH_PF_DEC : 0)>(srcw, recw, base, zero);
-            asm volatile("" : "+v"(src));
-            lh_load_col(ring[X % LH_PF_DEC], src, zero);
+            constexpr int XN = X + LH_PF_DEC < LH_DCOLS ? X + LH_PF_DEC : 0;
+            // (an integer passes through the asm: a pointer would lose its global address
+            // space and turn the loads into flat loads)
+            unsigned int w = XN < LH_K ? srcw[(XN < LH_K ? XN : 0) / 4] : recw[(XN >= LH_K ? XN - LH_K : 0) / 4];
+            asm volatile("" : "+v"(w));
+            const unsigned int slot = (w >> (8 * ((XN < LH_K ? XN : XN - LH_K) % 4))) & 0xFFu;
+            lh_load_col(ring[X % LH_PF_DEC], lh_slot_ptr(slot, base, zero), zero);
 #else
             const unsigned char *src = lh_dcol_src<(X + LH_PF_DEC < LH_DCOLS ? X + LH_PF_DEC : 0)>(srcw, recw, base, zero);
             lh_word nxt[8];
@@ -591,7 +599,7 @@ __device__ __forceinline__ void lh_decode_body(const lh_lane &l, unsigned char *
                                                long long stripe_stride, lh_plan_regs &pr,
                                                const unsigned char *__restrict__ zero_page, const PREP &prep) {
     unsigned char *base = blocks + l.stripe * stripe_stride + l.p;
-    const unsigned char *zero = zero_page + l.p;
+    const unsigned char *zero = zero_page + (l.stripe % LH_NZ) * LH_BYTES + l.p;
     lh_word v[LH_M][8];
     {
 #if LH_PREP_FIRST
@@ -813,6 +821,9 @@ __device__ __forceinline__ void lh_fused_solve::operator()(lh_plan_regs &pr) con
     for (int q = 0; q < LH_NOUT; ++q) asm volatile("" : "+v"(pr.outw[q]));
 }
 
+#ifndef LH_ROWPF
+#define LH_ROWPF 0  // fused decode: prefetch the next grid-stride group's rows (persistent grids)
+#endif
 #ifndef LH_DEC_LB
 #define LH_DEC_LB 1  // min waves per SIMD the register allocator must allow (tools/tune.py)
 #endif
@@ -830,6 +841,34 @@ lh_jit_decode_fused(unsigned char *__restrict__ blocks, long long stripe_stride,
     }
     __syncthreads();
     const int wid = threadIdx.x >> 6;
+#if LH_ROWPF
+    // Grid-stride waves (the host caps the grid, LONGHAIR_AMD_GRID) with the next stripe
+    // group's Block.row bytes loaded while the current group decodes, so a group's plan
+    // starts without a global-memory round trip.
+    {
+        const int lane = threadIdx.x & 63;
+        const int sl = lane / LH_NCH;
+        const int c = lane - sl * LH_NCH;
+        const long long nw = lh_total_waves(stripes);
+        const long long ws = (long long)gridDim.x * (blockDim.x >> 6);
+        long long w = (lh_block_id() * blockDim.x + threadIdx.x) >> 6;
+        unsigned int rowv[LH_NRW];
+        if (w < nw) lh_fused_rows(lh_map_lane(stripes, w), c, rows, rowv);
+        for (; w < nw; w += ws) {
+            const lh_lane l = lh_map_lane(stripes, w);
+            unsigned int cur[LH_NRW];
+#pragma unroll
+            for (int t = 0; t < LH_NRW; ++t) cur[t] = rowv[t];
+            if (w + ws < nw) lh_fused_rows(lh_map_lane(stripes, w + ws), c, rows, rowv);
+            lh_plan_regs pr;
+            lh_fused_solve sv;
+            sv.gexp = gexp;
+            sv.glog = glog;
+            if (l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], cur, rows, status, sv, pr))
+                lh_decode_body(l, blocks, stripe_stride, pr, zero_page, sv);
+        }
+    }
+#else
     LH_WAVE_LOOP(stripes) {
         const lh_lane l = lh_map_lane(stripes, lh_w);
         const int lane = threadIdx.x & 63;
@@ -844,6 +883,7 @@ lh_jit_decode_fused(unsigned char *__restrict__ blocks, long long stripe_stride,
         if (l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr))
             lh_decode_body(l, blocks, stripe_stride, pr, zero_page, sv);
     }
+#endif
 }
 
 // Persistent, software-pipelined variant (host launches at most one resident grid): while

@@ -48,6 +48,10 @@ def main():
     X, D, rows0, _ = bench.make_workload(k, m, nbytes, stripes, seed=7)
     e = min(k, m)
     rec_view = D[:, k - e:]
+    if os.environ.get("TUNE_REC_FIRST"):  # recovery blocks in slots 0..e-1 (probe)
+        D = torch.roll(D, e, dims=1).contiguous()
+        rows0 = torch.roll(rows0, e, dims=1).contiguous()
+        rec_view = D[:, :e]
     rows = rows0.clone()
     ref_rec = None
     results = {name: ([], []) for name, _ in VARIANTS}
