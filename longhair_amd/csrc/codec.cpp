@@ -165,14 +165,11 @@ static int device_generator(Device *d, int k, int m, const uint8_t **out) {
     return kOk;
 }
 
-// Zero pages: kZeroPages copies of a zero block (the specialised decode spreads its stripes
-// over them, LH_NZ), shared by every stream.  A larger one replaces it without a
+// Zero page (>= block bytes), shared by every stream.  A larger one replaces it without a
 // device synchronisation: the old page stays allocated (kernels in flight on other streams
 // may still read it) and the new page is cleared on the null stream, which this thread
 // waits for before publishing the pointer (non-blocking streams are not stalled).
-static constexpr size_t kZeroPages = 64;
 static int zero_page(Device *d, size_t bytes, const uint8_t **out) {
-    bytes *= kZeroPages;
     std::lock_guard<std::mutex> g(d->mu);
     if (d->zero.size < bytes) {
         uint8_t *p = nullptr;
@@ -250,7 +247,9 @@ static int encode_batch(int k, int m, int bytes, int stripes, const uint8_t *d_d
     }
 
     JitConfig cfg;
-    if (jit_config_for(k, m, bytes, false, &cfg)) {
+    // (the specialised encode reads a wave's stripes through one buffer resource, whose
+    // 32-bit range must cover them: jit_codec.hip lh_encode_wave)
+    if (jit_config_for(k, m, bytes, false, &cfg) && data_stride * (cfg.spw ? cfg.spw : 1) < (1ll << 31)) {
         std::string err;
         const JitKernels *jk = allow_compile ? d->jit.get(cfg, &err) : d->jit.peek(cfg);
         if (jk) {
@@ -315,7 +314,10 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
     const int e_max = (m == 1 || k <= 1) ? 1 : (k < m ? k : m);
     const long long plan_stride = PlanView::bytes(k, m, e_max);
     JitConfig cfg;
-    const bool jit_ok = (k > 1 && m > 1) && jit_config_for(k, m, bytes, true, &cfg);
+    // The specialised decode reads a wave's stripes through one buffer resource, whose
+    // 32-bit range must cover them (jit_codec.hip lh_make_dsrc).
+    const bool jit_ok = (k > 1 && m > 1) && jit_config_for(k, m, bytes, true, &cfg) &&
+                        stride * (cfg.spw ? cfg.spw : 1) < (1ll << 31);
     const JitKernels *jk = nullptr;
     std::string err;
     if (jit_ok) {
@@ -327,15 +329,8 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         // Plan computed inside the decode kernel: one launch, no plan workspace.
         const uint8_t *zero = nullptr;
         if (int rc = zero_page(d, (size_t)bytes, &zero)) return rc;
-        long long blocks = jit_blocks(cfg, stripes);
+        const long long blocks = jit_blocks(cfg, stripes);
         hipFunction_t fn = jk->decode_fused;
-        const char *pipe = std::getenv("LONGHAIR_AMD_DEC_PIPE");
-        if (pipe && std::atoi(pipe) && jk->decode_pipe && jk->pipe_blocks_per_cu > 0 && d->cus > 0) {
-            // Persistent pipelined variant: at most one resident grid.
-            const long long resident = (long long)d->cus * jk->pipe_blocks_per_cu;
-            if (blocks > resident) blocks = resident;
-            fn = jk->decode_pipe;
-        }
         long long s1 = stride;
         const uint8_t *gexp = d->gf_exp;
         const int16_t *glog = d->gf_log;

@@ -5,6 +5,7 @@
 #include <dlfcn.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <utime.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -20,6 +21,7 @@ namespace lh {
 namespace {
 constexpr long long kMaxNetworkOnes = 24000;  // keeps the unrolled network in the I-cache
 constexpr int kMaxAccDwords = 96;              // accumulator registers per lane
+constexpr int kMaxJitColumns = 128;            // data columns of a register-resident network
 }  // namespace
 
 long long generator_ones(int k, int m) {
@@ -34,6 +36,10 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
         if (std::string(env) == "generic") return false;
     }
     if (k < 2 || m < 2 || k + m > 256 || bytes % 8 != 0 || bytes <= 0) return false;
+    // k > 128 with few rows: the generic kernel.  Its straight-line network of > 128
+    // columns took hiprtc ~7 minutes per module (k250/m3) for a shape outside the
+    // benchmarked configurations.
+    if (k > kMaxJitColumns) return false;
     const int sub = bytes / 8;
     const int emax = k < m ? k : m;
     if (decode && (long long)emax * m > 64) return false;
@@ -544,10 +550,11 @@ static std::string cache_path(const std::string &src) {
     // cache made by another ROCm is never loaded.
     std::string key = src;
     for (const char *o : kOpts) key += std::string("\n") + o;
-    int major = 0, minor = 0, rt = 0;
+    // (HIP_VERSION is the build's headers; hipRuntimeGetVersion would need a device, and
+    // the cache is filled on a machine without one.)
+    int major = 0, minor = 0;
     (void)hiprtcVersion(&major, &minor);
-    (void)hipRuntimeGetVersion(&rt);
-    key += "\nhiprtc " + std::to_string(major) + "." + std::to_string(minor) + " hip " + std::to_string(rt);
+    key += "\nhiprtc " + std::to_string(major) + "." + std::to_string(minor) + " hip " + std::to_string(HIP_VERSION);
     char name[64];
     snprintf(name, sizeof(name), "/lh_%016llx.co", (unsigned long long)fnv1a(key));
     const std::string d = cache_dir();
@@ -574,7 +581,10 @@ bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::str
             code->resize(n > 0 ? (size_t)n : 0);
             const bool ok = n > 0 && fread(code->data(), 1, (size_t)n, f) == (size_t)n;
             fclose(f);
-            if (ok) return true;
+            if (ok) {
+                (void)utime(path.c_str(), nullptr);  // mark as used (tools/precompile.py --prune)
+                return true;
+            }
         }
     }
     hiprtcProgram prog;
@@ -640,13 +650,6 @@ const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err) {
     kern.encode = fn("lh_jit_encode");
     kern.decode = fn("lh_jit_decode");
     kern.decode_fused = fn("lh_jit_decode_fused");
-    kern.decode_pipe = fn("lh_jit_decode_pipe");
-    if (kern.decode_pipe &&
-        hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&kern.pipe_blocks_per_cu, kern.decode_pipe, 256, 0) !=
-            hipSuccess) {
-        (void)hipGetLastError();
-        kern.pipe_blocks_per_cu = 0;
-    }
     kern.encode_win = fn("lh_jit_encode_win");
     kern.decode_wide = fn("lh_jit_decode_wide");
     if (!kern.encode && !kern.encode_win && !kern.decode_wide) {

@@ -31,8 +31,6 @@ struct JitKernels {
     hipFunction_t encode = nullptr;
     hipFunction_t decode = nullptr;
     hipFunction_t decode_fused = nullptr;  // plan computed in-kernel (e_max <= 4)
-    hipFunction_t decode_pipe = nullptr;   // persistent software-pipelined variant of decode_fused
-    int pipe_blocks_per_cu = 0;            // its occupancy (blocks of 256 threads per CU)
     hipFunction_t encode_win = nullptr;    // windowed large-m encode (win modules)
     hipFunction_t decode_wide = nullptr;   // fused windowed decode (win == 2 modules, m <= 64)
     JitConfig cfg{};

@@ -76,6 +76,44 @@ __device__ __forceinline__ lh_word lh_load(const unsigned char *p) {
 #ifndef LH_NT_ST
 #define LH_NT_ST LH_NT  // non-temporal stores (tools/tune.py knob, independent of the loads)
 #endif
+#ifndef LH_BUF
+// Column loads through buffer resources (32-bit lane offsets, wave-uniform column offsets in
+// SGPRs, out-of-range offsets read as zero): k29/m4 access pattern 0.5175 against 0.549 ms
+// for 64-bit global addresses (profiles/r2_ubench_pattern.txt).
+#define LH_BUF 1
+#endif
+#ifndef LH_NT_DEC
+// Decode loads: default cache policy.  The decode writes its outputs in place, into lines
+// it (or a neighbour stripe's wave) read; non-temporal loads of those lines cost ~6 % in
+// the access-pattern microbenchmark (profiles/r2_ubench_pattern.txt: 0.623 vs 0.587 ms).
+#define LH_NT_DEC 0
+#endif
+
+// Decode-side column loads (W-byte lanes as lh_load, cache policy LH_NT_DEC).
+__device__ __forceinline__ lh_word lh_load_dec(const unsigned char *p) {
+#if LH_NT_DEC
+    return lh_load(p);
+#else
+    lh_word w;
+#if LH_W == 16
+    const lh_u32x4 v = *(const lh_u32x4 *)p;
+    w.v[0] = v.x; w.v[1] = v.y; w.v[2] = v.z; w.v[3] = v.w;
+#elif LH_W == 12
+    const lh_u32x3 v = *(const lh_u32x3 *)p;
+    w.v[0] = v.x; w.v[1] = v.y; w.v[2] = v.z;
+#elif LH_W == 8
+    const lh_u32x2 v = *(const lh_u32x2 *)p;
+    w.v[0] = v.x; w.v[1] = v.y;
+#elif LH_W == 4
+    w.v[0] = *(const unsigned int *)p;
+#else
+#pragma unroll
+    for (int i = 0; i < LH_NW; ++i) w.v[i] = 0;
+    __builtin_memcpy(&w.v[0], p, LH_W);
+#endif
+    return w;
+#endif
+}
 __device__ __forceinline__ void lh_store(unsigned char *p, const lh_word &w) {
 #if LH_NT_ST && LH_W == 16
     lh_u32x4 v = {w.v[0], w.v[1], w.v[2], w.v[3]};
@@ -98,6 +136,28 @@ __device__ __forceinline__ void lh_xor(lh_word &a, const lh_word &b) {
     for (int i = 0; i < LH_NW; ++i) a.v[i] ^= b.v[i];
 }
 
+// W-byte lane load through a buffer resource: voffset `off` (per lane), soffset `soff`
+// (wave-uniform, e.g. a column offset), cache policy `aux` (2 = non-temporal).
+template <int AUX>
+__device__ __forceinline__ lh_word lh_load_buf(const __amdgpu_buffer_rsrc_t &rs, int off, int soff = 0) {
+    lh_word w;
+#if LH_W == 16
+    const lh_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, soff, AUX);
+    w.v[0] = v.x; w.v[1] = v.y; w.v[2] = v.z; w.v[3] = v.w;
+#elif LH_W == 12
+    const lh_u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(rs, off, soff, AUX);
+    w.v[0] = v.x; w.v[1] = v.y; w.v[2] = v.z;
+#elif LH_W == 8
+    const lh_u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, off, soff, AUX);
+    w.v[0] = v.x; w.v[1] = v.y;
+#elif LH_W == 4
+    w.v[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, soff, AUX);
+#else  // 1- or 2-byte lanes (tiny sub-blocks)
+    w.v[0] = LH_W == 2 ? (unsigned int)__builtin_amdgcn_raw_buffer_load_b16(rs, off, soff, AUX)
+                       : (unsigned int)__builtin_amdgcn_raw_buffer_load_b8(rs, off, soff, AUX);
+#endif
+    return w;
+}
 // gfx950 v_bitop3_b32: any 3-input boolean function in one VALU op.  The LUT index is
 // (src0 << 2) | (src1 << 1) | src2: 0x96 = src0 ^ src1 ^ src2, 0x78 = src0 ^ (src1 & src2).
 // hipcc does not fuse XOR chains on its own (it emits one v_xor_b32 per term).
@@ -139,9 +199,17 @@ struct lh_col_net {
         }
     }
 };
+#ifndef LH_NET_PROBE
+#define LH_NET_PROBE 0  // timing probe only (tools/tune.py): one XOR per sub-block instead of the network
+#endif
 template <int X>
 __device__ __forceinline__ void lh_column(lh_word (&acc)[LH_M][8], const lh_word (&d)[8]) {
+#if LH_NET_PROBE
+#pragma unroll
+    for (int y = 0; y < 8; ++y) lh_xor(acc[X % LH_M][y], d[y]);
+#else
     lh_col_net<X>::run(acc, d);
+#endif
 }
 
 struct lh_lane {
@@ -213,6 +281,24 @@ __device__ __forceinline__ void lh_opaque(lh_word (&acc)[LH_M][8]) {
             for (int i = 0; i < LH_NW; ++i) asm volatile("" : "+v"(acc[r][y].v[i]));
 }
 
+// Encode column source of a lane: with LH_BUF one buffer resource over the wave's stripes
+// (column x at soffset x * LH_BYTES, a wave-uniform SGPR; sub-block b in the immediate
+// offset; one 32-bit lane offset), else the lane's 64-bit chunk pointer.
+struct lh_esrc {
+#if LH_BUF
+    __amdgpu_buffer_rsrc_t rs;
+    int lbase;
+    __device__ __forceinline__ lh_word load(int x, int b) const {
+        return lh_load_buf<LH_NT ? 2 : 0>(rs, lbase + b * LH_SUB, x * LH_BYTES);
+    }
+#else
+    const unsigned char *base;
+    __device__ __forceinline__ lh_word load(int x, int b) const {
+        return lh_load(base + (long long)x * LH_BYTES + b * LH_SUB);
+    }
+#endif
+};
+
 // Column loop, unrolled at compile time, with the next LH_PF columns' loads in flight
 // while column X is combined.
 #ifndef LH_PF
@@ -220,12 +306,11 @@ __device__ __forceinline__ void lh_opaque(lh_word (&acc)[LH_M][8]) {
 #endif
 template <int X>
 struct lh_unroll_encode {
-    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], lh_word (&ring)[LH_PF][8],
-                                               const unsigned char *base) {
+    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], lh_word (&ring)[LH_PF][8], const lh_esrc &S) {
         if (X + LH_PF < LH_K) {
             lh_word nxt[8];
 #pragma unroll
-            for (int b = 0; b < 8; ++b) nxt[b] = lh_load(base + (long long)(X + LH_PF) * LH_BYTES + b * LH_SUB);
+            for (int b = 0; b < 8; ++b) nxt[b] = S.load(X + LH_PF, b);
             lh_column<X>(acc, ring[X % LH_PF]);
             lh_opaque(acc);
 #pragma unroll
@@ -234,78 +319,12 @@ struct lh_unroll_encode {
             lh_column<X>(acc, ring[X % LH_PF]);
             lh_opaque(acc);
         }
-        lh_unroll_encode<X + 1>::run(acc, ring, base);
+        lh_unroll_encode<X + 1>::run(acc, ring, S);
     }
 };
 template <>
 struct lh_unroll_encode<LH_K> {
-    __device__ __forceinline__ static void run(lh_word (&)[LH_M][8], lh_word (&)[LH_PF][8], const unsigned char *) {}
-};
-
-// LH_PAIR = 1: columns combined two at a time, so the odd terms left by one column's
-// XOR3 pairing pair up with the next column's (row 0 of the generator is all ones: its
-// eight single terms per column halve).  Needs LH_PF >= 2.
-#ifndef LH_PAIR
-#define LH_PAIR 0
-#endif
-template <unsigned S0, unsigned S1, int B = 0, int P = -1>
-struct lh_net2 {
-    __device__ __forceinline__ static void run(lh_word &a, const lh_word (&d0)[8], const lh_word (&d1)[8]) {
-        constexpr unsigned S = S0 | (S1 << 8);
-        if constexpr (B == 16) {
-            if constexpr (P >= 0) lh_xor(a, P < 8 ? d0[P & 7] : d1[P & 7]);
-        } else if constexpr (((S >> B) & 1u) == 0) {
-            lh_net2<S0, S1, B + 1, P>::run(a, d0, d1);
-        } else if constexpr (P < 0) {
-            lh_net2<S0, S1, B + 1, B>::run(a, d0, d1);
-        } else {
-            lh_xor2(a, P < 8 ? d0[P & 7] : d1[P & 7], B < 8 ? d0[B & 7] : d1[B & 7]);
-            lh_net2<S0, S1, B + 1, -1>::run(a, d0, d1);
-        }
-    }
-};
-template <int X, int I = 0>
-struct lh_col_net2 {
-    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], const lh_word (&d0)[8], const lh_word (&d1)[8]) {
-        if constexpr (I < LH_M * 8) {
-            lh_net2<LH_BM[I / 8][X][I % 8], LH_BM[I / 8][X + 1][I % 8]>::run(acc[I / 8][I % 8], d0, d1);
-            lh_col_net2<X, I + 1>::run(acc, d0, d1);
-        }
-    }
-};
-template <int X>
-struct lh_unroll_encode2 {
-    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], lh_word (&ring)[LH_PF][8],
-                                               const unsigned char *base) {
-        if constexpr (X + 1 >= LH_K) {
-            lh_unroll_encode<X>::run(acc, ring, base);  // odd column count: last one alone
-        } else {
-            lh_word n0[8], n1[8];
-            if constexpr (X + LH_PF < LH_K) {
-#pragma unroll
-                for (int b = 0; b < 8; ++b) n0[b] = lh_load(base + (long long)(X + LH_PF) * LH_BYTES + b * LH_SUB);
-            }
-            if constexpr (X + 1 + LH_PF < LH_K) {
-#pragma unroll
-                for (int b = 0; b < 8; ++b) n1[b] = lh_load(base + (long long)(X + 1 + LH_PF) * LH_BYTES + b * LH_SUB);
-            }
-            lh_col_net2<X>::run(acc, ring[X % LH_PF], ring[(X + 1) % LH_PF]);
-            lh_opaque(acc);
-            if constexpr (X + LH_PF < LH_K) {
-#pragma unroll
-                for (int b = 0; b < 8; ++b) ring[X % LH_PF][b] = n0[b];
-            }
-            if constexpr (X + 1 + LH_PF < LH_K) {
-#pragma unroll
-                for (int b = 0; b < 8; ++b) ring[(X + 1) % LH_PF][b] = n1[b];
-            }
-            lh_unroll_encode2<X + 2>::run(acc, ring, base);
-        }
-    }
-};
-template <>
-struct lh_unroll_encode2<LH_K> {
-    __device__ __forceinline__ static void run(lh_word (&)[LH_M][8], lh_word (&)[LH_PF][8], const unsigned char *) {}
+    __device__ __forceinline__ static void run(lh_word (&)[LH_M][8], lh_word (&)[LH_PF][8], const lh_esrc &) {}
 };
 
 __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned char *__restrict__ in,
@@ -320,18 +339,27 @@ __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned ch
         for (int y = 0; y < 8; ++y)
 #pragma unroll
             for (int i = 0; i < LH_NW; ++i) acc[r][y].v[i] = 0;
-    const unsigned char *base = in + l.stripe * in_stride + l.p;
+    lh_esrc S;
+#if LH_BUF
+#if LH_NCH <= 64
+    const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)wave) * LH_SPW;  // wave-uniform
+    const long long nst = (stripes - s0) < LH_SPW ? (stripes - s0) : LH_SPW;
+#else
+    const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)(wave / LH_WPS));
+    const long long nst = 1;
+#endif
+    S.rs = __builtin_amdgcn_make_buffer_rsrc((void *)(in + s0 * in_stride), 0, (int)(nst * in_stride), 0x00020000);
+    S.lbase = (int)((l.stripe - s0) * in_stride) + l.p;
+#else
+    S.base = in + l.stripe * in_stride + l.p;
+#endif
     lh_word ring[LH_PF][8];
 #pragma unroll
     for (int q = 0; q < LH_PF; ++q)
         if (q < LH_K)
 #pragma unroll
-            for (int b = 0; b < 8; ++b) ring[q][b] = lh_load(base + (long long)q * LH_BYTES + b * LH_SUB);
-#if LH_PAIR && LH_PF >= 2
-    lh_unroll_encode2<0>::run(acc, ring, base);
-#else
-    lh_unroll_encode<0>::run(acc, ring, base);
-#endif
+            for (int b = 0; b < 8; ++b) ring[q][b] = S.load(q, b);
+    lh_unroll_encode<0>::run(acc, ring, S);
     unsigned char *o = out + l.stripe * out_stride + l.p;
 #pragma unroll
     for (int r = 0; r < LH_M; ++r)
@@ -382,51 +410,51 @@ __device__ __forceinline__ void lh_load_packed(unsigned int (&w)[N], const unsig
 
 #define LH_BYTE(w, idx) (((w)[(idx) / 4] >> (8 * ((idx) % 4))) & 0xFFu)
 
-__device__ __forceinline__ const unsigned char *lh_slot_ptr(unsigned int slot, const unsigned char *base,
-                                                            const unsigned char *zero) {
-    return (slot == 0xFFu) ? zero : base + (long long)slot * LH_BYTES;
-}
-
-// Phase A streams LH_K data columns (erased ones read the zero page) and then the LH_M
-// recovery rows (absent ones read the zero page) through one prefetch ring, so the
-// recovery loads are in flight while the last data columns combine.
-#ifndef LH_COLS_PROBE
-#define LH_COLS_PROBE 0  // timing probe only: phase A streams the k data columns, no recovery rows
-#endif
-#define LH_DCOLS (LH_COLS_PROBE ? LH_K : LH_K + LH_M)
+// Phase A streams LH_K data columns (erased ones read as zeros) and then the LH_M recovery
+// rows (absent ones read as zeros) through one prefetch ring, so the recovery loads are in
+// flight while the last data columns combine.
+#define LH_DCOLS (LH_K + LH_M)
 #ifndef LH_PF_DEC
-#define LH_PF_DEC 1  // decode prefetch depth (tools/tune.py, fused plan: 1 > 2 > 3)
-#endif
-#ifndef LH_REFILL
-#define LH_REFILL 0  // decode ring: refill a slot right after its column is combined (no staging copy)
+#define LH_PF_DEC 1  // decode prefetch depth (tools/tune.py, fused plan: 1 >= 2 > 3)
 #endif
 #ifndef LH_PREP_FIRST
 #define LH_PREP_FIRST 0  // fused decode: solve the plan before (1) or while (0) the first columns load
 #endif
-
-template <int X>
-__device__ __forceinline__ const unsigned char *lh_dcol_src(const unsigned int (&srcw)[LH_NSRC],
-                                                            const unsigned int (&recw)[LH_NREC],
-                                                            const unsigned char *base, const unsigned char *zero) {
-    if (X < LH_K) return lh_slot_ptr(LH_BYTE(srcw, X < LH_K ? X : 0), base, zero);
-    return lh_slot_ptr(LH_BYTE(recw, X >= LH_K ? X - LH_K : 0), base, zero);
-}
-
-// Column load of the decode ring.  LH_ZSKIP: lanes whose column is absent (erased
-// original, missing recovery row) do not load the zero page, they zero their words under
-// the exec mask, so no wave-instruction fetches from one hot 1.3-KB page.
-#ifndef LH_NZ
-#define LH_NZ 1  // zero pages the stripes spread over (the host allocates 64): one hot page
-                 // concentrates every erased column's reads on a few L2 channels
-#endif
-#ifndef LH_ZSKIP
-#define LH_ZSKIP 0  // measured equal (0.6255 vs 0.6212 ms, k29/m4): the zero page stays L2-resident
-#endif
-__device__ __forceinline__ void lh_load_col(lh_word (&d)[8], const unsigned char *src, const unsigned char *zero) {
-#if LH_ZSKIP
-    if (src != zero) {
+#if LH_BUF
+// Column source of a wave: one buffer resource over the wave's stripes (wave-uniform base,
+// num_records = their bytes; the host keeps that below 2^31).  An absent column (erased
+// original, missing recovery row) gets an out-of-range offset, which the hardware answers
+// with zeros without a memory request -- no zero page and no extra L2 traffic -- and every
+// column address is one 32-bit offset instead of a 64-bit pointer.
+struct lh_dsrc {
+    __amdgpu_buffer_rsrc_t rs;
+    int lbase;  // this lane's offset: (stripe - first stripe of the wave) * stride + chunk
+    __device__ __forceinline__ int col(unsigned int slot) const {
+        return slot == 0xFFu ? (int)0x80000000 : lbase + (int)slot * LH_BYTES;
+    }
+};
+__device__ __forceinline__ void lh_load_col(lh_word (&d)[8], const lh_dsrc &S, unsigned int slot) {
+    const int off = S.col(slot);
 #pragma unroll
-        for (int b = 0; b < 8; ++b) d[b] = lh_load(src + b * LH_SUB);
+    for (int b = 0; b < 8; ++b) d[b] = lh_load_buf<LH_NT_DEC ? 2 : 0>(S.rs, off + b * LH_SUB);
+}
+#else
+// Column source of a lane: its stripe's chunk pointer and the zero page.
+struct lh_dsrc {
+    const unsigned char *base, *zero;
+    __device__ __forceinline__ const unsigned char *col(unsigned int slot) const {
+        return (slot == 0xFFu) ? zero : base + (long long)slot * LH_BYTES;
+    }
+};
+#ifndef LH_ZSKIP
+#define LH_ZSKIP 0  // lanes of absent columns skip the zero-page load (exec-masked)
+#endif
+__device__ __forceinline__ void lh_load_col(lh_word (&d)[8], const lh_dsrc &S, unsigned int slot) {
+    const unsigned char *src = S.col(slot);
+#if LH_ZSKIP
+    if (slot != 0xFFu) {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) d[b] = lh_load_dec(src + b * LH_SUB);
     } else {
 #pragma unroll
         for (int b = 0; b < 8; ++b)
@@ -435,8 +463,17 @@ __device__ __forceinline__ void lh_load_col(lh_word (&d)[8], const unsigned char
     }
 #else
 #pragma unroll
-    for (int b = 0; b < 8; ++b) d[b] = lh_load(src + b * LH_SUB);
+    for (int b = 0; b < 8; ++b) d[b] = lh_load_dec(src + b * LH_SUB);
 #endif
+}
+#endif
+
+// Slot of decode column X: the slot holding original X (X < k) or recovery row X - k.
+template <int X>
+__device__ __forceinline__ unsigned int lh_dcol_slot(const unsigned int (&srcw)[LH_NSRC],
+                                                     const unsigned int (&recw)[LH_NREC]) {
+    if (X < LH_K) return LH_BYTE(srcw, X < LH_K ? X : 0);
+    return LH_BYTE(recw, X >= LH_K ? X - LH_K : 0);
 }
 
 template <int X>
@@ -452,43 +489,26 @@ __device__ __forceinline__ void lh_dcombine(lh_word (&acc)[LH_M][8], const lh_wo
 template <int X>
 struct lh_unroll_decode {
     __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], lh_word (&ring)[LH_PF_DEC][8],
-                                               const unsigned char *base, const unsigned char *zero,
-                                               const unsigned int (&srcw)[LH_NSRC], const unsigned int (&recw)[LH_NREC]) {
+                                               const lh_dsrc &S, const unsigned int (&srcw)[LH_NSRC],
+                                               const unsigned int (&recw)[LH_NREC]) {
         if (X + LH_PF_DEC < LH_DCOLS) {
-#if LH_REFILL
-            // Combine column X, then refill its ring slot with column X + PF: no staging
-            // copy (16 VGPRs fewer), and the refill's address passes through an empty asm
-            // after the accumulator pin, so the load cannot be hoisted above the combine.
-            lh_dcombine<X>(acc, ring[X % LH_PF_DEC]);
-            lh_opaque(acc);
-            constexpr int XN = X + LH_PF_DEC < LH_DCOLS ? X + LH_PF_DEC : 0;
-            // (an integer passes through the asm: a pointer would lose its global address
-            // space and turn the loads into flat loads)
-            unsigned int w = XN < LH_K ? srcw[(XN < LH_K ? XN : 0) / 4] : recw[(XN >= LH_K ? XN - LH_K : 0) / 4];
-            asm volatile("" : "+v"(w));
-            const unsigned int slot = (w >> (8 * ((XN < LH_K ? XN : XN - LH_K) % 4))) & 0xFFu;
-            lh_load_col(ring[X % LH_PF_DEC], lh_slot_ptr(slot, base, zero), zero);
-#else
-            const unsigned char *src = lh_dcol_src<(X + LH_PF_DEC < LH_DCOLS ? X + LH_PF_DEC : 0)>(srcw, recw, base, zero);
             lh_word nxt[8];
-            lh_load_col(nxt, src, zero);
+            lh_load_col(nxt, S, lh_dcol_slot<(X + LH_PF_DEC < LH_DCOLS ? X + LH_PF_DEC : 0)>(srcw, recw));
             lh_dcombine<X>(acc, ring[X % LH_PF_DEC]);
             lh_opaque(acc);
 #pragma unroll
             for (int b = 0; b < 8; ++b) ring[X % LH_PF_DEC][b] = nxt[b];
-#endif
         } else {
             lh_dcombine<X>(acc, ring[X % LH_PF_DEC]);
             lh_opaque(acc);
         }
-        lh_unroll_decode<X + 1>::run(acc, ring, base, zero, srcw, recw);
+        lh_unroll_decode<X + 1>::run(acc, ring, S, srcw, recw);
     }
 };
 template <>
 struct lh_unroll_decode<LH_DCOLS> {
-    __device__ __forceinline__ static void run(lh_word (&)[LH_M][8], lh_word (&)[LH_PF_DEC][8], const unsigned char *,
-                                               const unsigned char *, const unsigned int (&)[LH_NSRC],
-                                               const unsigned int (&)[LH_NREC]) {}
+    __device__ __forceinline__ static void run(lh_word (&)[LH_M][8], lh_word (&)[LH_PF_DEC][8], const lh_dsrc &,
+                                               const unsigned int (&)[LH_NSRC], const unsigned int (&)[LH_NREC]) {}
 };
 
 // Per-stripe decode plan in registers: e, packed src/rec slot maps, coef, out slots.
@@ -506,30 +526,28 @@ struct lh_no_prep {
 // by Horner over the coefficient bits: B(c) v = B(2)(...B(2)(c_7 v)...) + c_0 v.
 // `prep` runs while the first columns are in flight (the fused kernel solves its plan there).
 // Decode pieces.  Ring issue: the first LH_PF_DEC columns of a stripe group.
-__device__ __forceinline__ void lh_dec_issue(lh_word (&ring)[LH_PF_DEC][8], const lh_plan_regs &pr,
-                                             const unsigned char *base, const unsigned char *zero) {
+__device__ __forceinline__ void lh_dec_issue(lh_word (&ring)[LH_PF_DEC][8], const lh_plan_regs &pr, const lh_dsrc &S) {
 #pragma unroll
     for (int q = 0; q < LH_PF_DEC; ++q) {
-        const unsigned char *src = (q == 0) ? lh_dcol_src<0>(pr.srcw, pr.recw, base, zero)
-                                 : (q == 1) ? lh_dcol_src<1>(pr.srcw, pr.recw, base, zero)
-                                 : (q == 2) ? lh_dcol_src<2>(pr.srcw, pr.recw, base, zero)
-                                            : lh_dcol_src<3>(pr.srcw, pr.recw, base, zero);
-        lh_load_col(ring[q], src, zero);
+        const unsigned int slot = (q == 0) ? lh_dcol_slot<0>(pr.srcw, pr.recw)
+                                : (q == 1) ? lh_dcol_slot<1>(pr.srcw, pr.recw)
+                                : (q == 2) ? lh_dcol_slot<2>(pr.srcw, pr.recw)
+                                           : lh_dcol_slot<3>(pr.srcw, pr.recw);
+        lh_load_col(ring[q], S, slot);
     }
 }
 
 // Phase A: V_r = R_r + sum_{x present} B(G[r][x]) D_x for every recovery row r, streaming
 // the ring (already issued) through all k + m columns.
 __device__ __forceinline__ void lh_dec_phase_a(lh_word (&v)[LH_M][8], lh_word (&ring)[LH_PF_DEC][8],
-                                               const lh_plan_regs &pr, const unsigned char *base,
-                                               const unsigned char *zero) {
+                                               const lh_plan_regs &pr, const lh_dsrc &S) {
 #pragma unroll
     for (int r = 0; r < LH_M; ++r)
 #pragma unroll
         for (int y = 0; y < 8; ++y)
 #pragma unroll
             for (int i = 0; i < LH_NW; ++i) v[r][y].v[i] = 0;
-    lh_unroll_decode<0>::run(v, ring, base, zero, pr.srcw, pr.recw);
+    lh_unroll_decode<0>::run(v, ring, S, pr.srcw, pr.recw);
 }
 
 // Phase B: D_{E_i} = sum_r B(coef[i][r]) V_r with the per-stripe inverse, by Horner over
@@ -592,27 +610,49 @@ __device__ __forceinline__ void lh_dec_phase_b(const lh_word (&v)[LH_M][8], cons
     }
 }
 
+// Column source of lane `l` (stripe l.stripe, chunk l.p) of wave `wave`.
+__device__ __forceinline__ lh_dsrc lh_make_dsrc(const lh_lane &l, long long wave, unsigned char *__restrict__ blocks,
+                                               long long stripe_stride, const unsigned char *__restrict__ zero_page,
+                                               int stripes) {
+    lh_dsrc S;
+#if LH_BUF
+#if LH_NCH <= 64
+    const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)wave) * LH_SPW;  // wave-uniform
+    const long long nst = (stripes - s0) < LH_SPW ? (stripes - s0) : LH_SPW;
+#else
+    const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)(wave / LH_WPS));
+    const long long nst = 1;
+#endif
+    S.rs = __builtin_amdgcn_make_buffer_rsrc(blocks + s0 * stripe_stride, 0, (int)(nst * stripe_stride), 0x00020000);
+    S.lbase = (int)((l.stripe - s0) * stripe_stride) + l.p;
+#else
+    S.base = blocks + l.stripe * stripe_stride + l.p;
+    S.zero = zero_page + l.p;
+#endif
+    return S;
+}
+
 // In-place erasure decode of one stripe group: ring issue, `prep` (the fused kernel
 // solves its plan there, while the first columns are in flight), phase A, phase B.
 template <class PREP>
-__device__ __forceinline__ void lh_decode_body(const lh_lane &l, unsigned char *__restrict__ blocks,
+__device__ __forceinline__ void lh_decode_body(const lh_lane &l, long long wave, unsigned char *__restrict__ blocks,
                                                long long stripe_stride, lh_plan_regs &pr,
-                                               const unsigned char *__restrict__ zero_page, const PREP &prep) {
-    unsigned char *base = blocks + l.stripe * stripe_stride + l.p;
-    const unsigned char *zero = zero_page + (l.stripe % LH_NZ) * LH_BYTES + l.p;
+                                               const unsigned char *__restrict__ zero_page, int stripes,
+                                               const PREP &prep) {
+    const lh_dsrc S = lh_make_dsrc(l, wave, blocks, stripe_stride, zero_page, stripes);
     lh_word v[LH_M][8];
     {
 #if LH_PREP_FIRST
         prep(pr);  // solve before the first loads: the ring is not live across the solve
 #endif
         lh_word ring[LH_PF_DEC][8];
-        lh_dec_issue(ring, pr, base, zero);
+        lh_dec_issue(ring, pr, S);
 #if !LH_PREP_FIRST
         prep(pr);
 #endif
-        lh_dec_phase_a(v, ring, pr, base, zero);
+        lh_dec_phase_a(v, ring, pr, S);
     }
-    lh_dec_phase_b(v, pr, base);
+    lh_dec_phase_b(v, pr, blocks + l.stripe * stripe_stride + l.p);
 }
 
 __device__ __forceinline__ void lh_decode_wave(long long wave, unsigned char *__restrict__ blocks,
@@ -629,7 +669,7 @@ __device__ __forceinline__ void lh_decode_wave(long long wave, unsigned char *__
     lh_load_packed(pr.recw, pl + LH_P_REC);
     lh_load_packed(pr.coefw, pl + LH_P_COEF);
     lh_load_packed(pr.outw, pl + LH_P_OUT);
-    lh_decode_body(l, blocks, stripe_stride, pr, zero_page, lh_no_prep());
+    lh_decode_body(l, wave, blocks, stripe_stride, pr, zero_page, stripes, lh_no_prep());
 }
 
 #if 1
@@ -821,9 +861,6 @@ __device__ __forceinline__ void lh_fused_solve::operator()(lh_plan_regs &pr) con
     for (int q = 0; q < LH_NOUT; ++q) asm volatile("" : "+v"(pr.outw[q]));
 }
 
-#ifndef LH_ROWPF
-#define LH_ROWPF 0  // fused decode: prefetch the next grid-stride group's rows (persistent grids)
-#endif
 #ifndef LH_DEC_LB
 #define LH_DEC_LB 1  // min waves per SIMD the register allocator must allow (tools/tune.py)
 #endif
@@ -841,34 +878,6 @@ lh_jit_decode_fused(unsigned char *__restrict__ blocks, long long stripe_stride,
     }
     __syncthreads();
     const int wid = threadIdx.x >> 6;
-#if LH_ROWPF
-    // Grid-stride waves (the host caps the grid, LONGHAIR_AMD_GRID) with the next stripe
-    // group's Block.row bytes loaded while the current group decodes, so a group's plan
-    // starts without a global-memory round trip.
-    {
-        const int lane = threadIdx.x & 63;
-        const int sl = lane / LH_NCH;
-        const int c = lane - sl * LH_NCH;
-        const long long nw = lh_total_waves(stripes);
-        const long long ws = (long long)gridDim.x * (blockDim.x >> 6);
-        long long w = (lh_block_id() * blockDim.x + threadIdx.x) >> 6;
-        unsigned int rowv[LH_NRW];
-        if (w < nw) lh_fused_rows(lh_map_lane(stripes, w), c, rows, rowv);
-        for (; w < nw; w += ws) {
-            const lh_lane l = lh_map_lane(stripes, w);
-            unsigned int cur[LH_NRW];
-#pragma unroll
-            for (int t = 0; t < LH_NRW; ++t) cur[t] = rowv[t];
-            if (w + ws < nw) lh_fused_rows(lh_map_lane(stripes, w + ws), c, rows, rowv);
-            lh_plan_regs pr;
-            lh_fused_solve sv;
-            sv.gexp = gexp;
-            sv.glog = glog;
-            if (l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], cur, rows, status, sv, pr))
-                lh_decode_body(l, blocks, stripe_stride, pr, zero_page, sv);
-        }
-    }
-#else
     LH_WAVE_LOOP(stripes) {
         const lh_lane l = lh_map_lane(stripes, lh_w);
         const int lane = threadIdx.x & 63;
@@ -881,73 +890,7 @@ lh_jit_decode_fused(unsigned char *__restrict__ blocks, long long stripe_stride,
         unsigned int rowv[LH_NRW];
         lh_fused_rows(l, c, rows, rowv);
         if (l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr))
-            lh_decode_body(l, blocks, stripe_stride, pr, zero_page, sv);
-    }
-#endif
-}
-
-// Persistent, software-pipelined variant (host launches at most one resident grid): while
-// a wave runs phase B of its stripe group, the next group's plan is already derived (its
-// Block.row bytes were loaded before phase A) and its first columns are in flight.
-extern "C" __global__ void __launch_bounds__(256, LH_DEC_LB)
-lh_jit_decode_pipe(unsigned char *__restrict__ blocks, long long stripe_stride, unsigned char *__restrict__ rows,
-                   signed char *__restrict__ status, const unsigned char *__restrict__ zero_page,
-                   const unsigned char *__restrict__ gf_exp, const short *__restrict__ gf_log, int stripes) {
-    __shared__ unsigned char gexp[512];
-    __shared__ short glog[256];
-    __shared__ __attribute__((aligned(16))) unsigned char scratch[4][LH_SPW > 0 ? LH_SPW : 1][LH_SR];
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-        gexp[i] = gf_exp[i];
-        gexp[i + 256] = gf_exp[i + 256];
-        glog[i] = gf_log[i];
-    }
-    __syncthreads();
-    const int wid = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
-    const int sl = lane / LH_NCH;
-    const int c = lane - sl * LH_NCH;
-    const long long nw = lh_total_waves(stripes);
-    const long long wstride = (long long)gridDim.x * (blockDim.x >> 6);
-    long long w = (long long)blockIdx.x * (blockDim.x >> 6) + wid;
-    if (w >= nw) return;
-    lh_lane l = lh_map_lane(stripes, w);
-    unsigned int rowv[LH_NRW];
-    lh_fused_rows(l, c, rows, rowv);
-    lh_plan_regs pr;
-    lh_fused_solve sv;
-    sv.gexp = gexp;
-    sv.glog = glog;
-    bool go = l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr);
-    lh_word ring[LH_PF_DEC][8];
-    if (go) lh_dec_issue(ring, pr, blocks + l.stripe * stripe_stride + l.p, zero_page + l.p);
-    for (;;) {
-        const long long w2 = w + wstride;
-        const bool more = w2 < nw;
-        const lh_lane l2 = lh_map_lane(stripes, w2);
-        unsigned int rowv2[LH_NRW];
-        if (more) lh_fused_rows(l2, c, rows, rowv2);  // in flight during phase A
-        unsigned char *base = blocks + l.stripe * stripe_stride + l.p;
-        lh_word v[LH_M][8];
-        if (go) {
-            sv(pr);
-            lh_dec_phase_a(v, ring, pr, base, zero_page + l.p);
-        }
-        lh_plan_regs pr2;
-        lh_fused_solve sv2;
-        sv2.gexp = gexp;
-        sv2.glog = glog;
-        bool go2 = false;
-        if (more) {
-            go2 = l2.active && lh_fused_plan(l2, c, sl, &scratch[wid][sl][0], rowv2, rows, status, sv2, pr2);
-            if (go2) lh_dec_issue(ring, pr2, blocks + l2.stripe * stripe_stride + l2.p, zero_page + l2.p);
-        }
-        if (go) lh_dec_phase_b(v, pr, base);
-        if (!more) break;
-        w = w2;
-        l = l2;
-        pr = pr2;
-        sv = sv2;
-        go = go2;
+            lh_decode_body(l, lh_w, blocks, stripe_stride, pr, zero_page, stripes, sv);
     }
 }
 #endif  // LH_EMAX <= 4 && LH_NCH <= 64 && LH_K <= 64

@@ -48,6 +48,8 @@ def main():
     X, D, rows0, _ = bench.make_workload(k, m, nbytes, stripes, seed=7)
     e = min(k, m)
     rec_view = D[:, k - e:]
+    if os.environ.get("TUNE_COMPACT_REC"):  # encode into a compact [S, m, B] buffer (probe)
+        rec_view = torch.empty((stripes, m, nbytes), dtype=torch.uint8, device="cuda")
     if os.environ.get("TUNE_REC_FIRST"):  # recovery blocks in slots 0..e-1 (probe)
         D = torch.roll(D, e, dims=1).contiguous()
         rows0 = torch.roll(rows0, e, dims=1).contiguous()
@@ -69,6 +71,8 @@ def main():
             elif rnd == 0:
                 assert torch.equal(rec_view, ref_rec) or "probe" in name, f"{name}: encode bytes differ"
             rows.copy_(rows0)
+            if rec_view.data_ptr() != D[:, k - e:].data_ptr() and not os.environ.get("TUNE_REC_FIRST"):
+                D[:, k - e:] = rec_view
             lh.decode_batch(D, rows, m)
             torch.cuda.synchronize()
             if rnd == 0:
