@@ -823,19 +823,22 @@ LH_API int cauchy_256_batch_prepare(int k, int m, int block_bytes, int max_strip
 
 // Compile the specialised code objects of a shape into the on-disk cache without a GPU
 // (build-time warm-up for shapes whose compilation takes long).  0 ok, -3 on failure.
+// LONGHAIR_AMD_PRECOMPILE_PART=enc|dec restricts it to the encode or decode modules, so
+// a build can compile the two large-m modules of a shape in parallel processes.
 LH_API int cauchy_256_jit_precompile(int k, int m, int block_bytes) {
     std::string err;
     std::vector<char> code;
     lh::JitConfig cfg;
-    for (int dec = 0; dec < 2; ++dec)
-        if (lh::jit_config_for(k, m, block_bytes, dec == 1, &cfg) && !lh::compile_code_object(cfg, &code, &err))
+    const char *part = std::getenv("LONGHAIR_AMD_PRECOMPILE_PART");
+    for (int dec = 0; dec < 2; ++dec) {
+        if (part && std::string(part) != (dec ? "dec" : "enc")) continue;
+        if (lh::jit_config_for(k, m, block_bytes, dec == 1, &cfg)) {
+            if (!lh::compile_code_object(cfg, &code, &err)) return lh::fail(lh::kHipError, err);
+        } else if (lh::jit_win_config_for(k, m, block_bytes, &cfg, dec == 1) &&
+                   !lh::compile_code_object(cfg, &code, &err)) {
             return lh::fail(lh::kHipError, err);
-    if (!lh::jit_config_for(k, m, block_bytes, false, &cfg) && lh::jit_win_config_for(k, m, block_bytes, &cfg) &&
-        !lh::compile_code_object(cfg, &code, &err))
-        return lh::fail(lh::kHipError, err);
-    if (!lh::jit_config_for(k, m, block_bytes, true, &cfg) && lh::jit_win_config_for(k, m, block_bytes, &cfg, true) &&
-        !lh::compile_code_object(cfg, &code, &err))
-        return lh::fail(lh::kHipError, err);
+        }
+    }
     return 0;
 }
 

@@ -3,7 +3,7 @@
 # time-out stops the session), smoke, the k29m4 bench, the ceiling microbenchmark, a
 # kernel-trace profile of the bench and SQ counter passes of the large-m configs.
 # Every GPU step has its own time limit.  Usage: tools/gpu_r2.sh OUT_NAME [steps...]
-# steps: tests smoke bench ubench prof sq large (default: all but large)
+# steps: tests smoke bench large ubench tune prof profall sq pmc pcie (default: tests smoke bench ubench prof sq)
 set -o pipefail
 cd "$(dirname "$0")/.."
 OUT=gpurun_out/${1:-r2}; shift
@@ -49,5 +49,24 @@ if has sq; then
     python3 tools/sq_summary.py "$f" $cfg > "$OUT/sq_$cfg.json" && cp profiles/sq_$cfg.json "$OUT/" || exit 1
     grep -E '"lh_|SQ_INSTS_VALU|wait_any' "$OUT/sq_$cfg.json"
   done
+fi
+if has pmc; then
+  for cfg in k29m4 k128m32 k200m56; do
+    mkdir -p "$OUT/pmc_$cfg"
+    timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_$cfg/pmc_fetch" -o run --output-format csv -- python3 tools/prof_kernels.py $cfg > "$OUT/pmc_$cfg/fetch.log" 2>&1 || { tail -20 "$OUT/pmc_$cfg/fetch.log"; exit 1; }
+    timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_$cfg/pmc_write" -o run --output-format csv -- python3 tools/prof_kernels.py $cfg > "$OUT/pmc_$cfg/write.log" 2>&1 || { tail -20 "$OUT/pmc_$cfg/write.log"; exit 1; }
+    python3 tools/pmc_summary.py "$OUT/pmc_$cfg" $cfg > "$OUT/pmc_$cfg/summary.json" && cp profiles/pmc_$cfg.json "$OUT/pmc_$cfg/" || exit 1
+    grep -E '"(kernel|ratio_to_algorithmic)"' "$OUT/pmc_$cfg/summary.json"
+  done
+fi
+if has profall; then
+  for cfg in k128m32 k200m56; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$cfg" -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --cpu-baseline off --dropin-calls 0 > "$OUT/prof_$cfg.log" 2>&1 || { tail -20 "$OUT/prof_$cfg.log"; exit 1; }
+    find "$OUT/prof_$cfg" -name "*kernel_stats.csv" -exec grep -E "lh_" {} \; | cut -c1-160
+  done
+fi
+if has pcie; then
+  timeout -k 10 600 python tools/pcie_bench.py k29m4 k200m56 > "$OUT/pcie.json" 2> "$OUT/pcie.err" || { tail -20 "$OUT/pcie.err"; exit 1; }
+  cat "$OUT/pcie.json"
 fi
 echo "session done"

@@ -40,8 +40,17 @@ def main():
         with ThreadPoolExecutor(jobs) as pool:
             # ~570, 130, 190, 110 s alone: start first (the GPU tests run k200/m56 too)
             slow = [(200, 56, 65536), (128, 32, 8192), (64, 3, 4096), (64, 5, 4096)]
-            shapes = slow + [s for s in DEFAULT + TESTS if s not in slow]
-            runs = list(pool.map(lambda s: subprocess.run(cmd + [str(v) for v in s]), shapes))
+            # the large-m shapes' encode and decode modules compile in separate processes
+            jobs_list = [(s, part) for s in slow[:2] for part in ("dec", "enc")]
+            jobs_list += [(s, None) for s in slow[2:] + [s for s in DEFAULT + TESTS if s not in slow]]
+
+            def run(job):
+                shape, part = job
+                env = dict(os.environ)
+                if part:
+                    env["LONGHAIR_AMD_PRECOMPILE_PART"] = part
+                return subprocess.run(cmd + [str(v) for v in shape], env=env)
+            runs = list(pool.map(run, jobs_list))
         if any(r.returncode for r in runs):
             sys.exit(1)
         return
