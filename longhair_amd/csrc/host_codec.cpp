@@ -9,9 +9,9 @@
 // Both operations are one bit-sliced coefficient apply (same algebra as the GPU kernels):
 //   out[i] sub-row y  ^=  in[j] sub-block b   for every bit b of C[i][j] * 2^y,
 // encode with C = the generator rows 1..m-1 (row 0 is the plain XOR, as the reference
-// writes it first: cauchy_256.cpp:1511-1516), decode with C = [A^-1 G_present | A^-1]
-// over the k received blocks, A = G[recovery rows][erased rows] (cauchy_256.cpp:707-790
-// solve the same system bit by bit; the solution is unique, so the bytes are equal).
+// writes it first: cauchy_256.cpp:1511-1516); decode in two applies, V = R + G_p D_p and
+// D_E = A^-1 V, A = G[recovery rows][erased rows] (cauchy_256.cpp:707-790 solve the same
+// system bit by bit; the solution is unique, so the bytes are equal).
 // The apply walks the sub-block in 64-byte (AVX-512BW) or 32-byte (AVX2) chunks, every
 // output sub-row of a chunk accumulated in a register from L1-resident input chunks,
 // input terms paired through a 3-input XOR (vpternlogq 0x96).
@@ -43,88 +43,105 @@ struct Terms {
     std::vector<uint16_t> idx;
 };
 
+// BM[c][y] = bit-row y of element c (c * 2^y): the input sub-blocks of output sub-row y.
+struct BitRows {
+    uint8_t r[256][8];
+    BitRows() {
+        for (int c = 0; c < 256; ++c) {
+            const uint64_t bm = bitmatrix((uint8_t)c);
+            for (int y = 0; y < 8; ++y) r[c][y] = (uint8_t)(bm >> (8 * y));
+        }
+    }
+};
+const BitRows &bitrows() {
+    static const BitRows t;
+    return t;
+}
+
 void build_terms(const uint8_t *C, int nout, int nin, Terms *T) {
+    const BitRows &BR = bitrows();
     T->nout = nout;
     T->nin = nin;
-    T->begin.assign((size_t)nout * 8 + 1, 0);
-    T->idx.clear();
-    T->idx.reserve((size_t)nout * nin * 32);
-    std::vector<uint64_t> bm((size_t)nin);
+    T->begin.resize((size_t)nout * 8 + 1);
+    T->idx.resize((size_t)nout * nin * 64);  // upper bound: every bit set
+    uint16_t *out = T->idx.data();
+    uint32_t n = 0;
     for (int i = 0; i < nout; ++i) {
-        for (int j = 0; j < nin; ++j) bm[j] = bitmatrix(C[(size_t)i * nin + j]);
+        const uint8_t *row = C + (size_t)i * nin;
         for (int y = 0; y < 8; ++y) {
-            T->begin[(size_t)i * 8 + y] = (uint32_t)T->idx.size();
-            for (int j = 0; j < nin; ++j) {
-                const unsigned s = (unsigned)((bm[j] >> (8 * y)) & 0xFF);
-                for (unsigned b = 0; b < 8; ++b)
-                    if (s & (1u << b)) T->idx.push_back((uint16_t)(8 * j + b));
-            }
+            T->begin[(size_t)i * 8 + y] = n;
+            for (int j = 0; j < nin; ++j)
+                for (unsigned s = BR.r[row[j]][y]; s; s &= s - 1) out[n++] = (uint16_t)(8 * j + __builtin_ctz(s));
         }
     }
-    T->begin[(size_t)nout * 8] = (uint32_t)T->idx.size();
+    T->begin[(size_t)nout * 8] = n;
+    T->idx.resize(n);
 }
 
-// Scalar tail / fallback: bytes [p0, sub) of every output sub-row, through a staging row
-// so in-place outputs never feed later terms.
-void apply_scalar(const Terms &T, const uint8_t *const *src, uint8_t *const *dst, int sub, int p0, uint8_t *tmp) {
-    const int nrow = T.nout * 8;
-    for (int p = p0; p < sub; p += 64) {
-        const int n = std::min(64, sub - p);
-        for (int o = 0; o < nrow; ++o) {
-            uint8_t acc[64];
-            std::memset(acc, 0, (size_t)n);
-            for (uint32_t t = T.begin[o]; t < T.begin[o + 1]; ++t) {
-                const uint8_t *s = src[T.idx[t]] + p;
-                for (int q = 0; q < n; ++q) acc[q] ^= s[q];
-            }
-            std::memcpy(tmp + (size_t)o * 64, acc, (size_t)n);
+// One output sub-row of an apply: dst = (init ? init : 0) ^ XOR of src[idx[0..n)].  No
+// output may alias an input of the same apply (decode phase A writes a scratch V, phase B
+// reads it), so chunks are written straight back.
+struct OutRow {
+    const uint16_t *idx;
+    uint32_t n;
+    uint8_t *dst;
+    const uint8_t *init;
+};
+
+void apply_scalar(const OutRow *rows, int nrows, const uint8_t *const *src, int sub, int p0) {
+    for (int o = 0; o < nrows; ++o) {
+        const OutRow &R = rows[o];
+        for (int p = p0; p < sub; ++p) {
+            uint8_t acc = R.init ? R.init[p] : 0;
+            for (uint32_t t = 0; t < R.n; ++t) acc ^= src[R.idx[t]][p];
+            R.dst[p] = acc;
         }
-        for (int o = 0; o < nrow; ++o) std::memcpy(dst[o] + p, tmp + (size_t)o * 64, (size_t)n);
     }
 }
 
-__attribute__((target("avx512f,avx512bw"))) void apply_avx512(const Terms &T, const uint8_t *const *src,
-                                                                 uint8_t *const *dst, int sub, uint8_t *tmp) {
-    const int nrow = T.nout * 8;
+__attribute__((target("avx512f,avx512bw"))) void apply_avx512(const OutRow *rows, int nrows,
+                                                                 const uint8_t *const *src, int sub) {
     for (int p = 0; p < sub; p += 64) {
-        const int n = std::min(64, sub - p);
-        const __mmask64 mk = n == 64 ? ~0ull : ((1ull << n) - 1);
-        for (int o = 0; o < nrow; ++o) {
-            __m512i acc = _mm512_setzero_si512();
-            uint32_t t = T.begin[o];
-            const uint32_t e = T.begin[o + 1];
-            for (; t + 1 < e; t += 2)
-                acc = _mm512_ternarylogic_epi64(acc, _mm512_maskz_loadu_epi8(mk, src[T.idx[t]] + p),
-                                                _mm512_maskz_loadu_epi8(mk, src[T.idx[t + 1]] + p), 0x96);
-            if (t < e) acc = _mm512_xor_si512(acc, _mm512_maskz_loadu_epi8(mk, src[T.idx[t]] + p));
-            _mm512_store_si512((void *)(tmp + (size_t)o * 64), acc);
+        const int w = std::min(64, sub - p);
+        const __mmask64 mk = w == 64 ? ~0ull : ((1ull << w) - 1);
+        for (int o = 0; o < nrows; ++o) {
+            const OutRow &R = rows[o];
+            __m512i acc = R.init ? _mm512_maskz_loadu_epi8(mk, R.init + p) : _mm512_setzero_si512();
+            uint32_t t = 0;
+            if (w == 64) {
+                for (; t + 1 < R.n; t += 2)
+                    acc = _mm512_ternarylogic_epi64(acc, _mm512_loadu_si512((const void *)(src[R.idx[t]] + p)),
+                                                    _mm512_loadu_si512((const void *)(src[R.idx[t + 1]] + p)), 0x96);
+                if (t < R.n) acc = _mm512_xor_si512(acc, _mm512_loadu_si512((const void *)(src[R.idx[t]] + p)));
+                _mm512_storeu_si512((void *)(R.dst + p), acc);
+            } else {
+                for (; t + 1 < R.n; t += 2)
+                    acc = _mm512_ternarylogic_epi64(acc, _mm512_maskz_loadu_epi8(mk, src[R.idx[t]] + p),
+                                                    _mm512_maskz_loadu_epi8(mk, src[R.idx[t + 1]] + p), 0x96);
+                if (t < R.n) acc = _mm512_xor_si512(acc, _mm512_maskz_loadu_epi8(mk, src[R.idx[t]] + p));
+                _mm512_mask_storeu_epi8(R.dst + p, mk, acc);
+            }
         }
-        // Outputs are written after every input of this chunk was read (in-place decode).
-        for (int o = 0; o < nrow; ++o)
-            _mm512_mask_storeu_epi8(dst[o] + p, mk, _mm512_load_si512((const void *)(tmp + (size_t)o * 64)));
     }
 }
 
-__attribute__((target("avx2"))) void apply_avx2(const Terms &T, const uint8_t *const *src, uint8_t *const *dst,
-                                                 int sub, uint8_t *tmp) {
-    const int nrow = T.nout * 8;
+__attribute__((target("avx2"))) void apply_avx2(const OutRow *rows, int nrows, const uint8_t *const *src, int sub) {
     const int full = sub & ~31;
     for (int p = 0; p < full; p += 32) {
-        for (int o = 0; o < nrow; ++o) {
-            __m256i a0 = _mm256_setzero_si256(), a1 = _mm256_setzero_si256();
-            uint32_t t = T.begin[o];
-            const uint32_t e = T.begin[o + 1];
-            for (; t + 1 < e; t += 2) {
-                a0 = _mm256_xor_si256(a0, _mm256_loadu_si256((const __m256i *)(src[T.idx[t]] + p)));
-                a1 = _mm256_xor_si256(a1, _mm256_loadu_si256((const __m256i *)(src[T.idx[t + 1]] + p)));
+        for (int o = 0; o < nrows; ++o) {
+            const OutRow &R = rows[o];
+            __m256i a0 = R.init ? _mm256_loadu_si256((const __m256i *)(R.init + p)) : _mm256_setzero_si256();
+            __m256i a1 = _mm256_setzero_si256();
+            uint32_t t = 0;
+            for (; t + 1 < R.n; t += 2) {
+                a0 = _mm256_xor_si256(a0, _mm256_loadu_si256((const __m256i *)(src[R.idx[t]] + p)));
+                a1 = _mm256_xor_si256(a1, _mm256_loadu_si256((const __m256i *)(src[R.idx[t + 1]] + p)));
             }
-            if (t < e) a0 = _mm256_xor_si256(a0, _mm256_loadu_si256((const __m256i *)(src[T.idx[t]] + p)));
-            _mm256_storeu_si256((__m256i *)(tmp + (size_t)o * 32), _mm256_xor_si256(a0, a1));
+            if (t < R.n) a0 = _mm256_xor_si256(a0, _mm256_loadu_si256((const __m256i *)(src[R.idx[t]] + p)));
+            _mm256_storeu_si256((__m256i *)(R.dst + p), _mm256_xor_si256(a0, a1));
         }
-        for (int o = 0; o < nrow; ++o)
-            _mm256_storeu_si256((__m256i *)(dst[o] + p), _mm256_loadu_si256((const __m256i *)(tmp + (size_t)o * 32)));
     }
-    if (full < sub) apply_scalar(T, src, dst, sub, full, tmp);
+    if (full < sub) apply_scalar(rows, nrows, src, sub, full);
 }
 
 enum Isa { kScalar = 0, kAvx2 = 1, kAvx512 = 2 };
@@ -143,16 +160,19 @@ Isa detect() {
     return hw < lim ? hw : lim;
 }
 
-// src: nin * 8 sub-block pointers, dst: nout * 8 sub-row pointers.
-void apply(const Terms &T, const uint8_t *const *src, uint8_t *const *dst, int sub) {
-    thread_local std::vector<uint8_t> tmp_store;
-    const size_t need = (size_t)T.nout * 8 * 64 + 64;
-    if (tmp_store.size() < need) tmp_store.resize(need);
-    uint8_t *tmp = (uint8_t *)(((uintptr_t)tmp_store.data() + 63) & ~(uintptr_t)63);
+void apply(const OutRow *rows, int nrows, const uint8_t *const *src, int sub) {
     switch (detect()) {
-        case kAvx512: apply_avx512(T, src, dst, sub, tmp); break;
-        case kAvx2: apply_avx2(T, src, dst, sub, tmp); break;
-        default: apply_scalar(T, src, dst, sub, 0, tmp); break;
+        case kAvx512: apply_avx512(rows, nrows, src, sub); break;
+        case kAvx2: apply_avx2(rows, nrows, src, sub); break;
+        default: apply_scalar(rows, nrows, src, sub, 0); break;
+    }
+}
+
+// The 8 output rows of matrix row r of term list T, written to dst + y * sub.
+void term_rows(const Terms &T, int r, uint8_t *dst, int sub, const uint8_t *init, int init_sub, OutRow *out) {
+    for (int y = 0; y < 8; ++y) {
+        const uint32_t b = T.begin[(size_t)8 * r + y], e = T.begin[(size_t)8 * r + y + 1];
+        out[y] = OutRow{T.idx.data() + b, e - b, dst + (size_t)y * sub, init ? init + (size_t)y * init_sub : nullptr};
     }
 }
 
@@ -200,14 +220,27 @@ void xor_blocks(uint8_t *out, const uint8_t *const *in, int n, int bytes) {
     }
 }
 
-struct EncodeCache {
+// Per (k, m): the generator and its full term list (rows 0..m-1), built once.
+struct ShapeCache {
     std::mutex mu;
-    std::map<std::pair<int, int>, Terms> terms;  // (k, m) -> rows 1..m-1 of the generator
+    struct Entry {
+        std::vector<uint8_t> G;
+        Terms T;
+    };
+    std::map<std::pair<int, int>, Entry> shapes;  // entries are never erased
 };
 
-EncodeCache &encode_cache() {
-    static EncodeCache c;
-    return c;
+const ShapeCache::Entry &shape(int k, int m) {
+    static ShapeCache c;
+    std::lock_guard<std::mutex> g(c.mu);
+    auto it = c.shapes.find({k, m});
+    if (it == c.shapes.end()) {
+        ShapeCache::Entry e;
+        e.G = generator_matrix(k, m);
+        build_terms(e.G.data(), m, k, &e.T);
+        it = c.shapes.emplace(std::make_pair(k, m), std::move(e)).first;
+    }
+    return it->second;  // the reference stays valid unlocked
 }
 
 }  // namespace
@@ -230,50 +263,42 @@ int encode(int k, int m, const uint8_t *const *data, uint8_t *rec, int bytes) {
     if (m == 1) return 0;
     if (k + m > 256 || bytes % 8 != 0) return -1;
     const int sub = bytes / 8;
-    const Terms *T = nullptr;
-    {
-        EncodeCache &c = encode_cache();
-        std::lock_guard<std::mutex> g(c.mu);
-        auto it = c.terms.find({k, m});
-        if (it == c.terms.end()) {
-            const std::vector<uint8_t> G = generator_matrix(k, m);
-            Terms t;
-            build_terms(G.data() + k, m - 1, k, &t);
-            it = c.terms.emplace(std::make_pair(k, m), std::move(t)).first;
-        }
-        T = &it->second;  // entries are never erased: the reference stays valid unlocked
-    }
-    std::vector<const uint8_t *> src((size_t)k * 8);
+    const ShapeCache::Entry &S = shape(k, m);
+    const uint8_t *src[256 * 8];
     for (int x = 0; x < k; ++x)
-        for (int b = 0; b < 8; ++b) src[(size_t)8 * x + b] = data[x] + (size_t)b * sub;
-    std::vector<uint8_t *> dst((size_t)(m - 1) * 8);
-    for (int r = 1; r < m; ++r)
-        for (int y = 0; y < 8; ++y) dst[(size_t)8 * (r - 1) + y] = rec + (size_t)r * bytes + (size_t)y * sub;
-    apply(*T, src.data(), dst.data(), sub);
+        for (int b = 0; b < 8; ++b) src[8 * x + b] = data[x] + (size_t)b * sub;
+    OutRow rows[255 * 8];
+    for (int r = 1; r < m; ++r) term_rows(S.T, r, rec + (size_t)r * bytes, sub, nullptr, 0, rows + 8 * (r - 1));
+    apply(rows, 8 * (m - 1), src, sub);
     return 0;
 }
 
 // cauchy_256_decode semantics for valid parameters with at least one recovery block and
 // m > 1 (the caller handles k <= 1, m == 1, no erasure and the parameter checks).
-// Returns -1 (blocks untouched) for duplicate or out-of-range rows.
+// Returns -1 (blocks untouched) for duplicate or out-of-range rows.  Same two phases as
+// the GPU kernels: V_j = R_j + sum_{x present} B(G[r_j][x]) D_x for each recovery block j
+// (the cached generator terms; erased columns read a zero block), then
+// D_{E_i} = sum_j B(A^-1[i][j]) V_j with A = G[rows of the recovery blocks][erased rows].
 int decode(int k, int m, Block *blocks, int bytes) {
     const Field &F = Field::get();
     int slot_of_row[256];
     for (int r = 0; r < k + m; ++r) slot_of_row[r] = -1;
-    std::vector<int> present, rcv;  // slots of originals / recovery blocks, array order
+    int rcv[256], e = 0;  // slots of the recovery blocks, array order
     for (int i = 0; i < k; ++i) {
         const int r = blocks[i].row;
         if (r >= k + m || slot_of_row[r] >= 0) return -1;
         slot_of_row[r] = i;
-        (r < k ? present : rcv).push_back(i);
+        if (r >= k) rcv[e++] = i;
     }
-    const int e = (int)rcv.size();
-    std::vector<int> erased;  // missing original rows, ascending (sort_blocks, :538-570)
-    for (int x = 0; x < k && (int)erased.size() < e; ++x)
-        if (slot_of_row[x] < 0) erased.push_back(x);
-    const std::vector<uint8_t> G = generator_matrix(k, m);
+    int erased[256], ne = 0;  // missing original rows, ascending (sort_blocks, :538-570)
+    for (int x = 0; x < k && ne < e; ++x)
+        if (slot_of_row[x] < 0) erased[ne++] = x;
+    const ShapeCache::Entry &S = shape(k, m);
+    const uint8_t *G = S.G.data();
     // A[j][i] = G[row of recovery j - k][erased i]; Gauss-Jordan for A^-1.
-    std::vector<uint8_t> A((size_t)e * e), I((size_t)e * e, 0);
+    thread_local std::vector<uint8_t> AI;
+    AI.assign((size_t)2 * e * e, 0);
+    uint8_t *A = AI.data(), *I = A + (size_t)e * e;
     for (int j = 0; j < e; ++j) {
         I[(size_t)j * e + j] = 1;
         for (int i = 0; i < e; ++i) A[(size_t)j * e + i] = G[(size_t)(blocks[rcv[j]].row - k) * k + erased[i]];
@@ -301,30 +326,29 @@ int decode(int k, int m, Block *blocks, int bytes) {
             }
         }
     }
-    // D_E = A^-1 (R - G_p D_p): coefficients over the k received blocks in array order.
-    // Inputs: present originals (coefficient -(A^-1 G[rcv rows][x]) = A^-1 G, char 2) and
-    // recovery blocks (coefficient A^-1).
     const int sub = bytes / 8;
-    std::vector<uint8_t> C((size_t)e * k, 0);
-    for (int i = 0; i < e; ++i) {
-        for (int jj = 0; jj < e; ++jj) C[(size_t)i * k + rcv[jj]] = I[(size_t)i * e + jj];
-        for (int s : present) {
-            const int x = blocks[s].row;
-            uint8_t acc = 0;
-            for (int jj = 0; jj < e; ++jj)
-                acc ^= F.mul(I[(size_t)i * e + jj], G[(size_t)(blocks[rcv[jj]].row - k) * k + x]);
-            C[(size_t)i * k + s] = acc;
-        }
+    // Phase A into a scratch V (e blocks); erased columns read a zero block.
+    thread_local std::vector<uint8_t> zero, V;
+    if (zero.size() < (size_t)bytes) zero.assign((size_t)bytes, 0);
+    if (V.size() < (size_t)e * bytes) V.resize((size_t)e * bytes);
+    const uint8_t *src[256 * 8];
+    for (int x = 0; x < k; ++x) {
+        const uint8_t *d = slot_of_row[x] >= 0 ? blocks[slot_of_row[x]].data : zero.data();
+        for (int b = 0; b < 8; ++b) src[8 * x + b] = d + (size_t)b * sub;
     }
-    Terms T;
-    build_terms(C.data(), e, k, &T);
-    std::vector<const uint8_t *> src((size_t)k * 8);
-    for (int s = 0; s < k; ++s)
-        for (int b = 0; b < 8; ++b) src[(size_t)8 * s + b] = blocks[s].data + (size_t)b * sub;
-    std::vector<uint8_t *> dst((size_t)e * 8);
-    for (int i = 0; i < e; ++i)  // recovery slot i (array order) receives erased row i
-        for (int y = 0; y < 8; ++y) dst[(size_t)8 * i + y] = blocks[rcv[i]].data + (size_t)y * sub;
-    apply(T, src.data(), dst.data(), sub);
+    thread_local std::vector<OutRow> rows;
+    rows.resize((size_t)8 * e);
+    for (int j = 0; j < e; ++j)
+        term_rows(S.T, blocks[rcv[j]].row - k, V.data() + (size_t)j * bytes, sub, blocks[rcv[j]].data, sub,
+                  rows.data() + 8 * j);
+    apply(rows.data(), 8 * e, src, sub);
+    // Phase B: recovery slot i (array order) receives erased row i.
+    thread_local Terms TB;
+    build_terms(I, e, e, &TB);
+    for (int j = 0; j < e; ++j)  // phase A's inputs are consumed: src now names V's sub-blocks
+        for (int b = 0; b < 8; ++b) src[8 * j + b] = V.data() + (size_t)j * bytes + (size_t)b * sub;
+    for (int i = 0; i < e; ++i) term_rows(TB, i, blocks[rcv[i]].data, sub, nullptr, 0, rows.data() + 8 * i);
+    apply(rows.data(), 8 * e, src, sub);
     for (int i = 0; i < e; ++i) blocks[rcv[i]].row = (unsigned char)erased[i];
     return 0;
 }
