@@ -795,17 +795,98 @@ __device__ __forceinline__ bool lh_fused_plan(const lh_lane &l, int c, int sl, u
     return true;
 }
 
+#ifndef LH_SOLVE_GJ
+#define LH_SOLVE_GJ 0  // fused planner: Gauss-Jordan instead of the adjugate inverse (A/B knob)
+#endif
+
+// Permutations of n <= 3 elements, for the cofactor expansion below.
+template <int n> struct lh_perms;
+template <> struct lh_perms<0> { static constexpr int cnt = 1; static constexpr int p[1][1] = {{0}}; };
+template <> struct lh_perms<1> { static constexpr int cnt = 1; static constexpr int p[1][1] = {{0}}; };
+template <> struct lh_perms<2> { static constexpr int cnt = 2; static constexpr int p[2][2] = {{0, 1}, {1, 0}}; };
+template <> struct lh_perms<3> {
+    static constexpr int cnt = 6;
+    static constexpr int p[6][3] = {{0, 1, 2}, {0, 2, 1}, {1, 0, 2}, {1, 2, 0}, {2, 0, 1}, {2, 1, 0}};
+};
+
+// A^-1 = adj(A) / det(A) for the N x N GF(256) matrix A (N = LH_EMAX <= 4; characteristic
+// 2, so no signs).  Every cofactor is a sum of products of N - 1 elements, each product one
+// exp lookup of a sum of logs, so the inverse costs a handful of dependent LDS round trips
+// (logs of A; all cofactor terms; logs of the cofactors and det; the quotients) where
+// Gauss-Jordan needs one chain of lookups per elimination step.  gexp has 1024 entries
+// (exp of any sum of up to four logs without a modulo).
+template <int N>
+__device__ __forceinline__ void lh_inv_adj(const unsigned int (&A)[N][N], unsigned int (&Ainv)[N][N],
+                                           const unsigned char *gexp, const short *glog) {
+    int L[N][N];
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int j = 0; j < N; ++j) L[i][j] = glog[A[i][j]];
+    constexpr int M = N - 1;
+    unsigned int C[N][N];  // cofactors
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        // One cofactor row at a time: the logs pass through an empty asm that also takes
+        // the previous row's cofactors, so at most N * (N-1)! lookups are in flight (all 96
+        // at once held ~25 more VGPRs than the rest of the kernel needs).
+        if (i > 0) {
+#pragma unroll
+            for (int j = 0; j < N; ++j) asm volatile("" : "+v"(C[i - 1][j]));
+#pragma unroll
+            for (int r = 0; r < N; ++r)
+#pragma unroll
+                for (int c = 0; c < N; ++c) asm volatile("" : "+v"(L[r][c]));
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            unsigned int c = 0;
+#pragma unroll
+            for (int q = 0; q < lh_perms<M>::cnt; ++q) {
+                int sum = 0;
+                bool zero = false;
+#pragma unroll
+                for (int t = 0; t < M; ++t) {
+                    const int r = t < i ? t : t + 1;
+                    const int cc0 = lh_perms<M>::p[q][t];
+                    const int cc = cc0 < j ? cc0 : cc0 + 1;
+                    sum += L[r][cc];
+                    zero = zero || A[r][cc] == 0u;
+                }
+                c ^= zero ? 0u : (unsigned int)gexp[sum];
+            }
+            C[i][j] = c;
+        }
+    }
+    int LC[N][N];
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int j = 0; j < N; ++j) LC[i][j] = glog[C[i][j]];
+    unsigned int det = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) det ^= (A[0][j] && C[0][j]) ? (unsigned int)gexp[L[0][j] + LC[0][j]] : 0u;
+    const int ninv = 255 - glog[det];  // det != 0: A is a square sub-matrix of an MDS code
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int j = 0; j < N; ++j) Ainv[i][j] = C[j][i] ? (unsigned int)gexp[LC[j][i] + ninv] : 0u;
+}
+
 __device__ __forceinline__ void lh_fused_solve::operator()(lh_plan_regs &pr) const {
     const int nr = pr.e;
-    // Gauss-Jordan on A = G[rr_i][er_j], identity-padded to LH_EMAX.
+    // A = G[rr_i][er_j], identity-padded to LH_EMAX; I = A^-1.
     unsigned int A[LH_EMAX][LH_EMAX], I[LH_EMAX][LH_EMAX];
 #pragma unroll
     for (int i = 0; i < LH_EMAX; ++i)
 #pragma unroll
-        for (int j = 0; j < LH_EMAX; ++j) {
+        for (int j = 0; j < LH_EMAX; ++j)
             A[i][j] = (i < nr && j < nr) ? LH_GRAW[rr[i]][er[j]] : (i == j ? 1u : 0u);
-            I[i][j] = (i == j) ? 1u : 0u;
-        }
+#if LH_SOLVE_GJ  // Gauss-Jordan (round 1): one dependent chain of table lookups per step
+#pragma unroll
+    for (int i = 0; i < LH_EMAX; ++i)
+#pragma unroll
+        for (int j = 0; j < LH_EMAX; ++j) I[i][j] = (i == j) ? 1u : 0u;
 #pragma unroll
     for (int cc = 0; cc < LH_EMAX; ++cc) {
         int p = cc;
@@ -830,6 +911,13 @@ __device__ __forceinline__ void lh_fused_solve::operator()(lh_plan_regs &pr) con
             for (int j = 0; j < LH_EMAX; ++j) { A[r][j] ^= lh_gmul(gexp, glog, f, A[cc][j]); I[r][j] ^= lh_gmul(gexp, glog, f, I[cc][j]); }
         }
     }
+#else
+    lh_inv_adj<LH_EMAX>(A, I, gexp, glog);
+#endif
+#pragma unroll
+    for (int i = 0; i < LH_EMAX; ++i)
+#pragma unroll
+        for (int j = 0; j < LH_EMAX; ++j) asm volatile("" : "+v"(I[i][j]));  // inverse complete here
     // Pack: coef[i][r] = Ainv[i][j] for the recovery row r = rr[j]; out slots; maps.
 #pragma unroll
     for (int q = 0; q < LH_NCOEF; ++q) pr.coefw[q] = 0;
@@ -868,12 +956,12 @@ extern "C" __global__ void __launch_bounds__(256, LH_DEC_LB)
 lh_jit_decode_fused(unsigned char *__restrict__ blocks, long long stripe_stride, unsigned char *__restrict__ rows,
                     signed char *__restrict__ status, const unsigned char *__restrict__ zero_page,
                     const unsigned char *__restrict__ gf_exp, const short *__restrict__ gf_log, int stripes) {
-    __shared__ unsigned char gexp[512];
+    __shared__ unsigned char gexp[1024];  // exp(i mod 255) for i < 1024 (lh_inv_adj)
     __shared__ short glog[256];
     __shared__ __attribute__((aligned(16))) unsigned char scratch[4][LH_SPW > 0 ? LH_SPW : 1][LH_SR];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-        gexp[i] = gf_exp[i];
-        gexp[i + 256] = gf_exp[i + 256];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gexp[i + 256 * q] = gf_exp[(i + 256 * q) % 255];
         glog[i] = gf_log[i];
     }
     __syncthreads();

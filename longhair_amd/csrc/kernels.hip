@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "kernels.hpp"
 
 namespace {
@@ -611,7 +613,11 @@ hipError_t launch_plan(const PlanArgs &a, hipStream_t st) {
     // Few stripes (latency-bound: one workgroup per stripe cannot fill the chip): four
     // waves per stripe split the elimination's columns; many stripes: one wave each.
     const size_t lds = (size_t)2 * a.e_max * (a.e_max > 64 ? 128 : 64);
-    const unsigned threads = (a.stripes <= 4096 && a.e_max > 8) ? 256u : 64u;
+    unsigned threads = (a.stripes <= 4096 && a.e_max > 8) ? 256u : 64u;
+    if (const char *t = std::getenv("LONGHAIR_AMD_PLAN_THREADS")) {  // tuning knob: 64, 128 or 256
+        const int v = std::atoi(t);
+        if (v == 64 || v == 128 || v == 256) threads = (unsigned)v;
+    }
     hipLaunchKernelGGL(lh_plan_kernel, dim3((unsigned)a.stripes), dim3(threads), lds, st, a);
     return hipGetLastError();
 }

@@ -23,7 +23,7 @@ VARIANTS = [
     ("nofused", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1"}),
 ]
 KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID", "LONGHAIR_AMD_NO_FUSED_PLAN",
-         "LONGHAIR_AMD_DEC_PIPE",
+         "LONGHAIR_AMD_PLAN_THREADS",
          "LONGHAIR_AMD_WIN_ROWS", "LONGHAIR_AMD_WIN_PF", "LONGHAIR_AMD_WIN_LDS"]
 # Large-m (windowed) variants: rows per wave and columns in flight.
 VARIANTS_WIN = [
