@@ -601,12 +601,13 @@ static std::atomic<long long> g_host_max_work{[] {
     return e ? std::atoll(e) : (4ll << 20);
 }()};
 
-// XOR work of one call in bytes (terms x sub-block bytes): encode = the generator's ones
-// plus the row-0 XOR; decode ~ half of the e x k x 64 bit-matrix entries.
+// Estimated XOR work of one call in bytes (terms x sub-block bytes), from the average
+// density of a bit-matrix (32 of 64 bits): encode = rows 1..m-1 plus the row-0 XOR;
+// decode = phase A over the k columns for e rows plus the e x e phase B.
 static long long host_work(int k, int m, int e, int bytes, bool decode) {
     const long long sub = bytes / 8;
-    if (!decode) return (generator_ones(k, m) - 8ll * k + k) * sub;
-    return 32ll * e * k * sub;
+    if (!decode) return (32ll * k * (m - 1) + k) * sub;
+    return 32ll * e * (k + e) * sub;
 }
 
 static bool want_host(long long work) {
