@@ -368,3 +368,46 @@ def test_frame_unframe_decode(lh, k, m, nbytes, stripes):
     assert int((status != 0).sum()) == 0
     order = rows.long().argsort(dim=1)
     assert torch.equal(torch.gather(blocks, 1, order.unsqueeze(-1).expand(-1, -1, nbytes)), data)
+
+
+# ------------------------------------------------------------------- hipGraph capture
+
+
+@pytest.mark.parametrize("k,m,nbytes,stripes", [(29, 4, 1296, 4096), (128, 32, 8192, 64)])
+def test_batch_calls_capture_in_a_graph(lh, k, m, nbytes, stripes):
+    """The batched calls only enqueue stream-ordered work (no device-wide synchronisation,
+    no allocation once the shape is prepared), so an encode + decode step captures into a
+    hipGraph (torch.cuda.graph) and replays with the same results."""
+    import torch
+    lh.prepare(k, m, nbytes, stripes)
+    g = torch.Generator(device="cuda").manual_seed(k)
+    data = torch.randint(0, 256, (stripes, k, nbytes), dtype=torch.uint8, device="cuda", generator=g)
+    perm = torch.argsort(torch.rand(stripes, k, device="cuda", generator=g), dim=1)
+    keep = perm[:, : k - m]
+    blocks = torch.empty_like(data)
+    blocks[:, : k - m] = torch.gather(data, 1, keep.unsqueeze(-1).expand(-1, -1, nbytes))
+    rows0 = torch.cat([keep, torch.arange(k, k + m, device="cuda").expand(stripes, m)], dim=1).to(torch.uint8)
+    rows = rows0.clone()
+    status = torch.empty((stripes,), dtype=torch.int8, device="cuda")
+    rec_view = blocks[:, k - m:]
+
+    def step():
+        lh.encode_batch(data, m, recovery=rec_view)
+        rows.copy_(rows0)
+        lh.decode_batch(blocks, rows, m, status=status)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()  # warm-up on the capture stream (workspaces, zero page)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):  # the warmed-up stream: its workspace exists
+        step()
+    blocks[:, k - m:].zero_()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert int((status != 0).sum()) == 0
+    order = rows.long().argsort(dim=1)
+    assert torch.equal(torch.gather(blocks, 1, order.unsqueeze(-1).expand(-1, -1, nbytes)), data)
