@@ -108,7 +108,9 @@ struct Device {
     std::mutex mu;                       // guards maps below and the drop-in staging
     uint8_t *gf_exp = nullptr;           // 512 B
     int16_t *gf_log = nullptr;           // 256 x int16
-    std::map<std::pair<int, int>, uint8_t *> generators;  // (k, m) -> m x k on device
+    // (k, m) -> m x k generator on device, followed by the Cauchy points X'[k], Y'[m]
+    // when the generator has that form (second: points present).
+    std::map<std::pair<int, int>, std::pair<uint8_t *, bool>> generators;
     DevBuf zero;                         // zero page (>= block bytes)
     std::vector<uint8_t *> retired;      // outgrown zero pages (never freed: see zero_page)
     std::map<hipStream_t, Workspace> ws;
@@ -151,17 +153,24 @@ static int current_device(Device **out) {
     return kOk;
 }
 
-static int device_generator(Device *d, int k, int m, const uint8_t **out) {
+static int device_generator(Device *d, int k, int m, const uint8_t **out, const uint8_t **points = nullptr) {
     std::lock_guard<std::mutex> g(d->mu);
     auto it = d->generators.find({k, m});
     if (it == d->generators.end()) {
-        const std::vector<uint8_t> G = generator_matrix(k, m);
+        std::vector<uint8_t> G = generator_matrix(k, m);
+        std::vector<uint8_t> xs, ys;
+        const bool pts = cauchy_points(k, m, xs, ys);
+        if (pts) {
+            G.insert(G.end(), xs.begin(), xs.end());
+            G.insert(G.end(), ys.begin(), ys.end());
+        }
         uint8_t *p = nullptr;
         LH_HIP(hipMalloc(&p, G.size()));
         LH_HIP(hipMemcpy(p, G.data(), G.size(), hipMemcpyHostToDevice));
-        it = d->generators.emplace(std::make_pair(k, m), p).first;
+        it = d->generators.emplace(std::make_pair(k, m), std::make_pair(p, pts)).first;
     }
-    *out = it->second;
+    *out = it->second.first;
+    if (points) *points = it->second.second ? it->second.first + (size_t)k * m : nullptr;
     return kOk;
 }
 
@@ -352,8 +361,8 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
     const size_t work_bytes = (generic && !wk) ? (size_t)stripes * e_max * bytes : 0;
     Workspace *w = nullptr;
     if (int rc = workspace(d, st, (size_t)stripes * plan_stride, work_bytes, &w)) return rc;
-    const uint8_t *G = nullptr;
-    if (int rc = device_generator(d, k, m, &G)) return rc;
+    const uint8_t *G = nullptr, *points = nullptr;
+    if (int rc = device_generator(d, k, m, &G, &points)) return rc;
 
     PlanArgs pa{};
     pa.rows = d_rows;
@@ -361,6 +370,7 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
     pa.plan = w->plan.ptr;
     pa.plan_stride = plan_stride;
     pa.G = G;
+    pa.points = std::getenv("LONGHAIR_AMD_PLAN_GJ") ? nullptr : points;  // knob: Gauss-Jordan always
     pa.gf_exp = d->gf_exp;
     pa.gf_log = d->gf_log;
     pa.k = k;

@@ -59,4 +59,28 @@ std::vector<uint8_t> generator_matrix(int k, int m) {
     return g;
 }
 
+// Cauchy points of the m >= 7 generators: element(r, x) = X_x / (X_x + Y'_r) with
+// X_0 = 1, Y'_0 = 0 (the all-ones row) and Y'_r = Y_{r-1}.  The decode planner inverts
+// e x e submatrices of this form in closed form.  Checked against the generator itself;
+// false (no closed form) for m < 7, whose rows are tabulated (cauchy_256.cpp:428-444).
+bool cauchy_points(int k, int m, std::vector<uint8_t> &xs, std::vector<uint8_t> &ys) {
+    if (m < 7 || k < 1) return false;
+    const unsigned char *Y = lh_cauchy_tables_blob + 3770;
+    const unsigned char *Xall = lh_cauchy_tables_blob + 4026;
+    const int n = m - 7;
+    const unsigned char *X = Xall + n * 249 - n * (n + 1) / 2;
+    xs.assign((size_t)k, 1);
+    ys.assign((size_t)m, 0);
+    for (int x = 1; x < k; ++x) xs[x] = X[x - 1];
+    for (int r = 1; r < m; ++r) ys[r] = Y[r - 1];
+    const Field &F = Field::get();
+    const std::vector<uint8_t> g = generator_matrix(k, m);
+    for (int r = 0; r < m; ++r)
+        for (int x = 0; x < k; ++x) {
+            const uint8_t d = (uint8_t)(xs[x] ^ ys[r]);
+            if (!xs[x] || !d || g[(size_t)r * k + x] != F.div(xs[x], d)) return false;
+        }
+    return true;
+}
+
 }  // namespace lh

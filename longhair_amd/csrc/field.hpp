@@ -32,6 +32,7 @@ struct Field {
 // data, cauchy_256.cpp:1511-1516), rows 1..m-1 are the reference's Cauchy rows
 // (cauchy_matrix, cauchy_256.cpp:423-481).  Preconditions: k >= 1, m >= 1, k + m <= 256.
 std::vector<uint8_t> generator_matrix(int k, int m);
+bool cauchy_points(int k, int m, std::vector<uint8_t> &xs, std::vector<uint8_t> &ys);
 
 // Expanded 8x8 GF(2) bit-matrix of element e, one byte per bit-row: row y = e * 2^y.
 // Bit b of row y set <=> data sub-block b contributes to output sub-block y.

@@ -202,6 +202,13 @@ __global__ void __launch_bounds__(256) lh_scatter_kernel(lh::ScatterArgs a) {
 //    consecutive bytes; the pivot of column c is the lowest unused row with a non-zero
 //    entry (one ballot).  [A | I] reduces to [P | M] with row p_c of the permutation P
 //    holding the 1 of column c, so A^-1[c][:] = M[p_c][:].
+//  * Closed form instead, whenever the generator is a Cauchy matrix (every m >= 7, so every
+//    e > 8 this kernel sees): A[i][j] = x_j / (x_j + y_i) with x_j = X'[E_j], y_i =
+//    Y'[r_i] (field.cpp cauchy_points), and over GF(2^8)
+//        A^-1[j][i] = P_j Q_i / ((x_j + y_i) C_j D_i x_j),
+//    P_j = prod_k (x_j + y_k), Q_i = prod_k (x_k + y_i), C_j = prod_{k!=j} (x_j + x_k),
+//    D_i = prod_{k!=i} (y_i + y_k): O(e^2) table lookups in the log domain instead of the
+//    O(e^3) elimination (the inverse is unique, so the bytes are the same).
 // LDS: GF tables, maps, and 2 e_max x RC bytes (RC = 64 or 128 rows).
 __global__ void __launch_bounds__(256) lh_plan_kernel(lh::PlanArgs a) {
     const int s = blockIdx.x;
@@ -285,6 +292,40 @@ __global__ void __launch_bounds__(256) lh_plan_kernel(lh::PlanArgs a) {
     }
     if (e == 0) return;
 
+    if (a.points) {
+        __shared__ uint8_t cx[128], cy[128];  // x_j, y_i
+        __shared__ int16_t al[128], be[128];  // log(P_j / (C_j x_j)), log(Q_i / D_i), in [0, 255)
+        for (int t = tid; t < e; t += nth) {
+            cx[t] = a.points[erasure[t]];
+            cy[t] = a.points[k + rcv_row[t]];
+        }
+        __syncthreads();
+        for (int t = tid; t < e; t += nth) {
+            const int x = cx[t], y = cy[t];
+            int pc = -glog[x], qd = 0;
+            for (int u = 0; u < e; ++u) {
+                const int xu = cx[u], yu = cy[u];
+                pc += glog[x ^ yu];
+                qd += glog[xu ^ y];
+                if (u != t) {
+                    pc -= glog[x ^ xu];
+                    qd -= glog[y ^ yu];
+                }
+            }
+            al[t] = (int16_t)((pc % 255 + 255) % 255);
+            be[t] = (int16_t)((qd % 255 + 255) % 255);
+        }
+        __syncthreads();
+        // A^-1[i][j] lands where the elimination would leave it: aug[e + j][p_i], p_i = i.
+        for (int q = tid; q < e * e; q += nth) {
+            const int i = q / e, j = q - i * e;
+            int v = al[i] + be[j] - glog[cx[i] ^ cy[j]];
+            v += v < 0 ? 255 : 0;
+            aug[(e + j) * RC + i] = gexp[v];
+        }
+        for (int i = tid; i < e; i += nth) piv_row[i] = (uint8_t)i;
+        __syncthreads();
+    } else {
     // [A | I]: A[i][j] = G[r_i][E_j] (r_i = recovery row of the i-th recovery slot,
     // E_j = j-th missing original).
     const int w2 = 2 * e;
@@ -355,6 +396,7 @@ __global__ void __launch_bounds__(256) lh_plan_kernel(lh::PlanArgs a) {
             }
         }
         __syncthreads();
+    }
     }
     // A^-1[c][j] = aug[e + j][p_c].  Emit: out slots, src/rec slot maps, coef (e x m over
     // recovery rows) and W (e x k over slots).

@@ -81,6 +81,7 @@ struct PlanArgs {
     uint8_t *plan;
     long long plan_stride;
     const uint8_t *G;             // m x k generator (row 0 = ones)
+    const uint8_t *points;        // Cauchy points X'[k], Y'[m] of G, or null (no closed form)
     const uint8_t *gf_exp;        // 512
     const int16_t *gf_log;        // 256
     int k, m, e_max, stripes;

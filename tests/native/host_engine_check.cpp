@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <vector>
 
+#include "field.hpp"
 #include "host_codec.hpp"
 
 typedef int (*enc_t)(int, int, const unsigned char *const *, unsigned char *, int);
@@ -30,6 +31,49 @@ int main(int argc, char **argv) {
     const dec_t odec = (dec_t)dlsym(h, "lho_decode");
     srand(12345);
     int bad = 0, n = 0;
+    // The decode planner's closed-form inverse (kernels.hip lh_plan_kernel): every m >= 7
+    // generator must expose its Cauchy points, and A^-1[j][i] = P_j Q_i / ((x_j + y_i) C_j
+    // D_i x_j) must invert random e x e submatrices (checked here by A * A^-1 = I).
+    {
+        const lh::Field &F = lh::Field::get();
+        for (int m = 7; m <= 128; m += 11)
+            for (int k : {1, 2, 9, 64, 256 - m}) {
+                std::vector<uint8_t> xs, ys;
+                ++n;
+                if (!lh::cauchy_points(k, m, xs, ys)) {
+                    printf("no Cauchy points k=%d m=%d\n", k, m);
+                    ++bad;
+                    continue;
+                }
+                const std::vector<uint8_t> G = lh::generator_matrix(k, m);
+                const int e = 1 + rand() % std::min(k, m);
+                std::vector<int> E, R;
+                for (int x = 0; x < k && (int)E.size() < e; ++x) if (rand() % 3 == 0 || k - x == e - (int)E.size()) E.push_back(x);
+                for (int r = 0; r < m && (int)R.size() < e; ++r) if (rand() % 3 == 0 || m - r == e - (int)R.size()) R.push_back(r);
+                std::vector<uint8_t> inv((size_t)e * e);
+                for (int j = 0; j < e; ++j)
+                    for (int i = 0; i < e; ++i) {
+                        const uint8_t x = xs[E[j]], y = ys[R[i]];
+                        int lg = -F.log[x] - F.log[x ^ y];
+                        for (int u = 0; u < e; ++u) {
+                            lg += F.log[x ^ ys[R[u]]] + F.log[xs[E[u]] ^ y];
+                            if (u != j) lg -= F.log[x ^ xs[E[u]]];
+                            if (u != i) lg -= F.log[y ^ ys[R[u]]];
+                        }
+                        inv[(size_t)j * e + i] = F.exp[(lg % 255 + 255) % 255];
+                    }
+                for (int i = 0; i < e; ++i)
+                    for (int c = 0; c < e; ++c) {
+                        uint8_t acc = 0;
+                        for (int j = 0; j < e; ++j) acc ^= F.mul(G[(size_t)R[i] * k + E[j]], inv[(size_t)j * e + c]);
+                        if (acc != (i == c)) {
+                            printf("closed-form inverse wrong k=%d m=%d e=%d\n", k, m, e);
+                            ++bad;
+                            i = c = e;
+                        }
+                    }
+            }
+    }
     const int shapes[][3] = {{29, 4, 1296}, {29, 1, 1296}, {2, 2, 8},     {17, 6, 520},   {128, 32, 8192},
                              {10, 6, 24},   {250, 6, 16},  {1, 3, 16},    {29, 4, 1304},  {64, 4, 4096},
                              {5, 3, 8},     {200, 56, 2048}, {29, 3, 12}, {200, 57, 16},  {3, 2, 520}};

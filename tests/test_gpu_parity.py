@@ -411,3 +411,65 @@ def test_batch_calls_capture_in_a_graph(lh, k, m, nbytes, stripes):
     assert int((status != 0).sum()) == 0
     order = rows.long().argsort(dim=1)
     assert torch.equal(torch.gather(blocks, 1, order.unsqueeze(-1).expand(-1, -1, nbytes)), data)
+
+
+def test_huge_stripe_stride_uses_a_safe_path(lh, oracle):
+    """The specialised kernels address a wave's stripes through one 32-bit buffer range;
+    strides beyond it (here 800 MB between stripes) must take a path without that limit
+    and still give the oracle's bytes (encode and in-place decode)."""
+    import torch
+    k, m, nbytes, stripes, stride = 29, 4, 1296, 4, 800 << 20
+    buf = torch.zeros(stride * (stripes - 1) + k * nbytes, dtype=torch.uint8, device="cuda")
+    view = torch.as_strided(buf, (stripes, k, nbytes), (stride, nbytes, 1))
+    host = lhutil.fill(31, stripes * k * nbytes).reshape(stripes, k, nbytes)
+    view.copy_(torch.from_numpy(host))
+    rec = lh.encode_batch(view, m)
+    torch.cuda.synchronize()
+    for s in range(stripes):
+        rc, exp = oracle.encode(k, m, host[s], nbytes)
+        assert rec[s].cpu().numpy().tobytes() == exp.tobytes(), s
+    # decode in place: erase originals 0..3, recovery blocks in their slots
+    for s in range(stripes):
+        view[s, :m] = rec[s]
+    rows = torch.tensor([[k + r for r in range(m)] + list(range(m, k))] * stripes, dtype=torch.uint8, device="cuda")
+    status = lh.decode_batch(view, rows, m)
+    torch.cuda.synchronize()
+    assert (status.cpu() == 0).all()
+    assert torch.equal(view.cpu(), torch.from_numpy(host))
+    assert rows.cpu().tolist() == [list(range(k))] * stripes
+    del buf
+
+
+@pytest.mark.parametrize("k,m,nbytes,stripes", [
+    (128, 32, 1024, 64), (200, 56, 256, 32), (128, 128, 64, 12), (60, 12, 512, 100), (9, 200, 64, 40),
+    (128, 32, 8192, 16),  # wide decode (precompiled module)
+])
+def test_planner_closed_form_matches_elimination(lh, oracle, monkeypatch, k, m, nbytes, stripes):
+    """The decode planner inverts e x e Cauchy submatrices in closed form (every m >= 7);
+    LONGHAIR_AMD_PLAN_GJ forces the Gauss-Jordan elimination it replaced.  Both must give
+    the oracle's bytes and rows, at random erasure counts up to e = min(k, m) (here up to
+    128: two rows per lane), through the wide decode and the generic path (m > 64)."""
+    import torch
+    data = lhutil.fill(k * 7 + m, stripes * k * nbytes).reshape(stripes, k, nbytes)
+    slots, rows = _decode_scenarios(k, m, nbytes, stripes, seed=k * m)
+    blocks = np.zeros((stripes, k, nbytes), dtype=np.uint8)
+    for s in range(stripes):
+        rec = oracle.encode(k, m, data[s], nbytes)[1].reshape(m, nbytes)
+        for i, (kind, x) in enumerate(slots[s]):
+            blocks[s, i] = data[s, x] if kind == "d" else rec[x]
+    outs = []
+    for gj in (False, True):
+        if gj:
+            monkeypatch.setenv("LONGHAIR_AMD_PLAN_GJ", "1")
+        d_blocks = _gpu_tensor(blocks)
+        d_rows = _gpu_tensor(np.array(rows, dtype=np.uint8))
+        status = lh.decode_batch(d_blocks, d_rows, m)
+        torch.cuda.synchronize()
+        assert (status.cpu() == 0).all()
+        outs.append((d_blocks.cpu().numpy(), d_rows.cpu().numpy()))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    for s in range(min(stripes, 8)):
+        bufs = [blocks[s, i].copy() for i in range(k)]
+        rc, exp_rows = oracle.decode(k, m, bufs, list(rows[s]), nbytes)
+        assert rc == 0 and list(outs[0][1][s]) == exp_rows
+        assert all(outs[0][0][s, i].tobytes() == bufs[i].tobytes() for i in range(k)), s
