@@ -154,6 +154,85 @@ __global__ void __launch_bounds__(256) pattern_enc_buf(const uint8_t *__restrict
     for (int b = 0; b < 8; ++b) __builtin_nontemporal_store(acc[b] ^ u32x2{(uint32_t)r, 0}, (u32x2 *)(o + r * BYTES + b * SUB));
 }
 
+// Encode pattern with the columns staged by LDS-DMA: per column, the wave's three
+// stripe-columns (3 x 1296 contiguous bytes) arrive as 16-B chunks in consecutive lanes
+// (global_load_lds_dwordx4, fully coalesced: 4 wave instructions instead of 8 scattered
+// 8-B loads), D columns in flight in a per-wave LDS ring; each lane then reads its 8
+// sub-block words from LDS (2-byte aligned ds_read_b64).
+template <int D>
+__global__ void __launch_bounds__(256) pattern_enc_dma(const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
+                                                       long long in_stride, long long out_stride, int stripes) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[4][D][4096];
+  const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, sl = lane / NCH, c = lane - sl * NCH;
+  const long long s0 = __builtin_amdgcn_readfirstlane((int)wave) * (long long)SPW;
+  if (s0 >= stripes) return;
+  const int ns = (int)min((long long)SPW, stripes - s0);
+  const int p = c == NCH - 1 ? SUB - 8 : c * 8;
+  const uint8_t *src[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = min(i * 64 + lane, SPW * 81 - 1);
+    src[i] = in + (s0 + min(j / 81, ns - 1)) * in_stride + (j % 81) * 16;
+  }
+  auto issue = [&](int x, int slot) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src[i] + x * BYTES),
+                                       (__attribute__((address_space(3))) void *)&ring[w][slot][i * 1024], 16, 0, 2);
+  };
+#pragma unroll
+  for (int q = 0; q < D; ++q) issue(q, q);
+  u32x2 acc[8];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) acc[b] = u32x2{0, 0};
+  const int lo = min(sl, SPW - 1) * BYTES + p;
+#pragma unroll
+  for (int x = 0; x < K; ++x) {
+    const int left = min(D - 1, K - 1 - x);  // columns issued after x
+    if (left == 2) __builtin_amdgcn_s_waitcnt((8 & 15) | ((8 >> 4) << 14) | (7 << 4) | (15 << 8));
+    else if (left == 1) __builtin_amdgcn_s_waitcnt(4 | (7 << 4) | (15 << 8));
+    else if (left == 3) __builtin_amdgcn_s_waitcnt(12 | (7 << 4) | (15 << 8));
+    else __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (15 << 8));
+    const uint8_t *t = &ring[w][x % D][lo];
+    u32x2 v[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) v[b] = *(const u32x2 *)(t + b * SUB);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[b] ^= v[b];
+    if (x + D < K) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      issue(x + D, x % D);
+    }
+  }
+  if (sl >= SPW || s0 + sl >= stripes) return;
+  uint8_t *o = out + (s0 + sl) * out_stride + p;
+#pragma unroll
+  for (int r = 0; r < M; ++r)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) __builtin_nontemporal_store(acc[b] ^ u32x2{(uint32_t)r, 0}, (u32x2 *)(o + r * BYTES + b * SUB));
+}
+
+// The floor for the encode's bytes: read the input and write the output as flat arrays,
+// 16 B per lane, fully coalesced, grid-stride (no stripe structure at all).
+template <int U>
+__global__ void __launch_bounds__(256) pattern_stream(const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
+                                                      long long in_bytes, long long out_bytes) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const long long n = in_bytes / 16, no = out_bytes / 16, tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long nt = (long long)gridDim.x * blockDim.x;
+  u32x4 acc = {0, 0, 0, 0};
+  for (long long i = tid; i < n; i += U * nt) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = i + u * nt < n ? __builtin_nontemporal_load((const u32x4 *)in + i + u * nt) : u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u];
+  }
+  for (long long i = tid; i < no; i += nt) __builtin_nontemporal_store(acc ^ u32x4{(uint32_t)i, 0, 0, 0}, (u32x4 *)out + i);
+}
+
 int main() {
   const int stripes = 65536;
   const size_t in_bytes = (size_t)stripes * K * BYTES;
@@ -247,6 +326,38 @@ int main() {
       printf("%-22s %7.4f ms  %7.1f GB/s input\n", name, ms / 10, in_bytes / (ms / 10 * 1e-3) / 1e9);
     };
     run_enc("enc buf nt", pattern_enc_buf<2>);
+    {  // the DMA variant must produce the buffer variant's bytes
+      const size_t ob = (size_t)stripes * M * BYTES;
+      std::vector<uint8_t> h(ob);
+      for (size_t i = 0; i < in_bytes; i += 4096) CK(hipMemset(din + i, (int)((i * 2654435761u) >> 24), std::min<size_t>(4096, in_bytes - i)));
+      pattern_enc_buf<2><<<grid, 256>>>(din, dout, (long long)K * BYTES, (long long)M * BYTES, stripes);
+      CK(hipMemcpy(h.data(), dout, ob, hipMemcpyDeviceToHost));
+      CK(hipMemset(dout, 0, ob));
+      pattern_enc_dma<3><<<grid, 256>>>(din, dout, (long long)K * BYTES, (long long)M * BYTES, stripes);
+      std::vector<uint8_t> h2(ob);
+      CK(hipMemcpy(h2.data(), dout, ob, hipMemcpyDeviceToHost));
+      printf("enc dma bytes %s\n", h == h2 ? "match" : "DIFFER");
+    }
+    run_enc("enc dma D=2", pattern_enc_dma<2>);
+    run_enc("enc dma D=3", pattern_enc_dma<3>);
+    run_enc("enc dma D=4", pattern_enc_dma<4>);
+    for (int g : {2048, 8192, 32768})
+      for (int u : {4, 8}) {
+        const long long ob = (long long)stripes * M * BYTES;
+        auto launch = [&] {
+          if (u == 4) pattern_stream<4><<<g, 256>>>(din, dout, (long long)in_bytes, ob);
+          else pattern_stream<8><<<g, 256>>>(din, dout, (long long)in_bytes, ob);
+        };
+        for (int i = 0; i < 3; ++i) launch();
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0));
+        for (int i = 0; i < 10; ++i) launch();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("flat stream r+w g=%-5d U=%d %7.4f ms  %7.1f GB/s input\n", g, u, ms / 10, in_bytes / (ms / 10 * 1e-3) / 1e9);
+      }
     run_enc("enc buf def", pattern_enc_buf<0>);
     run("buf zero-page nt/nt", pattern_buf<2, 2, false>);
     run("buf oob nt/nt", pattern_buf<2, 2, true>);
