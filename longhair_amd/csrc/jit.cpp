@@ -417,10 +417,17 @@ static std::string win_source_for(const JitConfig &c) {
         for (int q = 0; q <= c.win_pf; ++q)
             os << "__shared__ __attribute__((aligned(16))) unsigned char tile" << q << "[2048];\n";
     // LH_PINn: keep the accumulators in registers between columns (no re-association).
+    // One asm statement per row (8 operands): every volatile asm is a memory side effect
+    // to LLVM, and the IR sinking pass's cost grows with their number times the loads of
+    // the block -- one statement per accumulator made hiprtc spend 387 of the 451 s of the
+    // k200/m56 encode module in "Code sinking" (grouped: 85 s, 221 -> 217 VGPRs).
     for (int n = 1; n <= R; ++n) {
         os << "#define LH_PIN" << n << " do {";
-        for (int r = 0; r < n; ++r)
-            for (int y = 0; y < 8; ++y) os << " asm volatile(\"\" : \"+v\"(a" << r << "_" << y << "));";
+        for (int r = 0; r < n; ++r) {
+            os << " asm volatile(\"\" :";
+            for (int y = 0; y < 8; ++y) os << (y ? ", " : " ") << "\"+v\"(a" << r << "_" << y << ")";
+            os << ");";
+        }
         os << " } while (0)\n";
     }
     if (c.win == 2) {

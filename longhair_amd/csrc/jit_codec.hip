@@ -272,13 +272,30 @@ __device__ __forceinline__ long long lh_block_id() {
 
 // Keeps the accumulators in registers between columns: stops the compiler from
 // re-associating XORs across columns (which lengthens live ranges past the register file).
+// One asm statement per 8 (NW <= 3) or 4 words: each volatile asm is a memory side effect
+// to LLVM, and the IR sinking pass's cost grows with their number (jit.cpp LH_PIN).
+#if LH_NW == 1
+#define LH_OPS(w) "+v"((w).v[0])
+#elif LH_NW == 2
+#define LH_OPS(w) "+v"((w).v[0]), "+v"((w).v[1])
+#elif LH_NW == 3
+#define LH_OPS(w) "+v"((w).v[0]), "+v"((w).v[1]), "+v"((w).v[2])
+#else
+#define LH_OPS(w) "+v"((w).v[0]), "+v"((w).v[1]), "+v"((w).v[2]), "+v"((w).v[3])
+#endif
+__device__ __forceinline__ void lh_pin8(lh_word (&a)[8]) {
+#if LH_NW <= 3
+    asm volatile("" : LH_OPS(a[0]), LH_OPS(a[1]), LH_OPS(a[2]), LH_OPS(a[3]), LH_OPS(a[4]), LH_OPS(a[5]),
+                 LH_OPS(a[6]), LH_OPS(a[7]));
+#else
+    asm volatile("" : LH_OPS(a[0]), LH_OPS(a[1]), LH_OPS(a[2]), LH_OPS(a[3]));
+    asm volatile("" : LH_OPS(a[4]), LH_OPS(a[5]), LH_OPS(a[6]), LH_OPS(a[7]));
+#endif
+}
+
 __device__ __forceinline__ void lh_opaque(lh_word (&acc)[LH_M][8]) {
 #pragma unroll
-    for (int r = 0; r < LH_M; ++r)
-#pragma unroll
-        for (int y = 0; y < 8; ++y)
-#pragma unroll
-            for (int i = 0; i < LH_NW; ++i) asm volatile("" : "+v"(acc[r][y].v[i]));
+    for (int r = 0; r < LH_M; ++r) lh_pin8(acc[r]);
 }
 
 // Encode column source of a lane: with LH_BUF one buffer resource over the wave's stripes
@@ -598,10 +615,7 @@ __device__ __forceinline__ void lh_dec_phase_b(const lh_word (&v)[LH_M][8], cons
 #pragma unroll
                         for (int q = 0; q < LH_NW; ++q) o[y].v[q] = lh_xand(o[y].v[q], v[r][y].v[q], mask);
                 }
-#pragma unroll
-                for (int y = 0; y < 8; ++y)
-#pragma unroll
-                    for (int q = 0; q < LH_NW; ++q) asm volatile("" : "+v"(o[y].v[q]));
+                lh_pin8(o);
             }
             unsigned char *dst = base + (long long)LH_BYTE(outw, i) * LH_BYTES;
 #pragma unroll
