@@ -231,7 +231,9 @@ def kernel_names(k, m, block_bytes):
     dec = {"generic": ["lh_plan_kernel", "lh_apply_generic_kernel", "lh_scatter_kernel"],
            "jit": ["lh_plan_small_kernel" if min(k, m) <= 8 else "lh_plan_kernel", "lh_jit_decode"],
            "jit-fused": ["lh_jit_decode_fused"],
-           "jit-wide": ["lh_plan_kernel", "lh_jit_decode_wide"]}[batch_path(k, m, block_bytes, True)]
+           "jit-wide": ["lh_plan_kernel", "lh_jit_decode_wide"]
+           + ([] if os.environ.get("LONGHAIR_AMD_WIN_SPLIT") == "0" else ["lh_inverse_kernel"]),
+           }[batch_path(k, m, block_bytes, True)]
     if m == 1 or k == 1:
         enc, dec = ["lh_xor_reduce_kernel"], ["lh_plan_kernel", "lh_xor_reduce_kernel"]
     return enc, dec

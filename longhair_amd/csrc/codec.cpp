@@ -349,8 +349,9 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         LH_HIP(hipModuleLaunchKernel(fn, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr));
         return kOk;
     }
-    // Large m (<= 64): the fused windowed decode (phase A into LDS, phase B from LDS) after
-    // the planner; sub % (64 W) == 0.
+    // Large m (<= 64), sub % (64 W) == 0, after the planner: the windowed phase-A kernel
+    // (V_r in place of R_r) and lh_inverse_kernel (phase B), or the fused windowed decode
+    // (phase A into an LDS tile, phase B from it; LONGHAIR_AMD_WIN_SPLIT=0).
     JitConfig wcfg;
     const JitKernels *wk = nullptr;
     if (generic && jit_win_config_for(k, m, bytes, &wcfg, true)) {
@@ -422,6 +423,19 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         int n = stripes;
         void *args[] = {(void *)&d_blocks, &s1, (void *)&plan, &s2, (void *)&zero, &n};
         LH_HIP(hipModuleLaunchKernel(wk->decode_wide, (unsigned)blocks, 1, 1, threads, 1, 1, 0, st, args, nullptr));
+        if (wk->cfg.win_split) {  // phase A left V_r in the recovery slots: phase B
+            InverseArgs ia{};
+            ia.blocks = d_blocks;
+            ia.stride = stride;
+            ia.plan = plan;
+            ia.plan_stride = plan_stride;
+            ia.k = k;
+            ia.m = m;
+            ia.e_max = e_max;
+            ia.bytes = bytes;
+            ia.stripes = stripes;
+            LH_HIP(launch_inverse(ia, st));
+        }
         return kOk;
     }
     // Generic: recovered originals into the workspace, then into their slots.

@@ -107,17 +107,20 @@ bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
     cfg->spw = 0;
     cfg->wps = (cfg->nch + 63) / 64;
     cfg->win = decode ? 2 : 1;
-    // Rows per wave: 16 for encode (half the redundant column loads and nibble tables of
-    // 8: k128/m32 encode 4.21 -> 3.00 ms); 8 for the fused decode, whose V tile in LDS
-    // (m x 2 KiB per workgroup) caps the workgroups per CU, so it needs more waves each.
-    cfg->rows_per_wave = decode ? 8 : 16;
+    // Rows per wave: 16 (half the redundant column loads and nibble tables of 8: k128/m32
+    // encode 4.21 -> 3.00 ms; split decode phase A: k128/m32 decode 4.24 -> 4.14 ms,
+    // k200/m56 0.87 -> 0.79); 8 for the fused decode, whose V tile in LDS (m x 2 KiB per
+    // workgroup) caps the workgroups per CU, so it needs more waves each.
+    cfg->win_split = decode ? 1 : 0;
+    if (const char *sp = std::getenv("LONGHAIR_AMD_WIN_SPLIT")) cfg->win_split = decode && std::atoi(sp) ? 1 : 0;
+    cfg->rows_per_wave = (decode && !cfg->win_split) ? 8 : 16;
     if (const char *r = std::getenv("LONGHAIR_AMD_WIN_ROWS")) cfg->rows_per_wave = std::atoi(r);
     cfg->win_pf = 3;
     if (const char *f = std::getenv("LONGHAIR_AMD_WIN_PF")) cfg->win_pf = std::max(1, std::atoi(f));
     cfg->win_lds = 1;
     if (const char *l = std::getenv("LONGHAIR_AMD_WIN_LDS")) cfg->win_lds = std::atoi(l) ? 1 : 0;
     if ((m + cfg->rows_per_wave - 1) / cfg->rows_per_wave > 16) return false;  // <= 1024 threads
-    if (decode && m > 64) return false;  // the fused decode keeps m x 2 KiB of V in LDS
+    if (decode && m > 64) return false;  // the plan's used-row mask is one 64-lane ballot
     cfg->defines.clear();
     if (const char *d = std::getenv("LONGHAIR_AMD_JIT_DEFINES")) cfg->defines = d;
     return true;
@@ -149,7 +152,8 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
     const bool lds = c.win_lds != 0;
     const int NG = (m + R - 1) / R, D = PF + 1;
     const int ndma = NG == 1 ? 2 : (g < 2 ? 1 : 0);  // DMA instructions per column, this wave
-    os << "__device__ __forceinline__ void lh_wg" << g << "(const unsigned char *__restrict__ base, "
+    const bool split = elim && c.win_split;  // V_r goes back in place of R_r (lh_inverse_kernel follows)
+    os << "__device__ __forceinline__ void lh_wg" << g << "(" << (split ? "" : "const ") << "unsigned char *__restrict__ base, "
        << (elim ? "const unsigned char *__restrict__ zero, const unsigned int (&slv)[LH_NQ], unsigned int *__restrict__ lv"
                 : "unsigned char *__restrict__ o")
        << (lds ? ", const unsigned char *__restrict__ sb, const unsigned char *__restrict__ zb" : "")
@@ -190,14 +194,19 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
             if (ndma) os << "    lh_wait_vm(" << ndma * ahead << ");\n";
             os << "    __builtin_amdgcn_s_barrier();\n";
             if (x + PF < k) dma(x + PF, "    ");
-            for (int b = 0; b < 8; ++b)
-                os << "    const unsigned int d0_" << b << " = ((const unsigned int *)(tile" << x % D << " + " << b * 256
-                   << "))[lane];\n";
         } else if (x + PF < k) {
             os << "    const unsigned char *cn = " << col(x + PF) << ";\n";
             for (int b = 0; b < 8; ++b)
                 os << "    const unsigned int n" << b << " = lh_ld(cn + " << b * c.sub << ");\n";
         }
+        // Decode: an erased original contributes nothing -- skip its tables and XORs (a
+        // wave-uniform branch; the column's DMA / ring slot bookkeeping above still runs).
+        if (elim)
+            os << "    if (__builtin_amdgcn_readlane((int)slv[" << x / 64 << "], " << x % 64 << ") != 0xFF) {\n";
+        if (lds)
+            for (int b = 0; b < 8; ++b)
+                os << "    const unsigned int d0_" << b << " = ((const unsigned int *)(tile" << x % D << " + " << b * 256
+                   << "))[lane];\n";
         // Which nibble-table entries (lo: sub-blocks 0..3, hi: 4..7) this group needs.
         bool need[2][16] = {};
         for (int r = r0; r < r1; ++r) {
@@ -233,11 +242,23 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
             }
         }
         os << "    LH_PIN" << (r1 - r0) << ";\n";
+        if (elim) os << "    }\n";
         if (!lds && x + PF < k)
             for (int b = 0; b < 8; ++b) os << "    d" << slot << "_" << b << " = n" << b << ";\n";
         os << "  }\n";
     }
-    if (elim) {  // V_r = R_r + sum_x ...: XOR the recovery row r (zero page if absent)
+    if (split) {  // V_r = R_r + sum_x ...: read R_r, store V_r over it (absent rows: nothing)
+        for (int r = r0; r < r1; ++r) {
+            os << "  {\n    const unsigned int s = (unsigned int)__builtin_amdgcn_readlane((int)slv[" << (k + r) / 64
+               << "], " << (k + r) % 64 << ");\n    if (s != 0xFFu) {\n"
+               << "      unsigned char *rp = base + (long long)s * " << c.bytes << ";\n";
+            for (int y = 0; y < 8; ++y)
+                os << "      const unsigned int r" << y << " = lh_ld(rp + " << y * c.sub << ");\n";
+            for (int y = 0; y < 8; ++y)
+                os << "      lh_st(rp + " << y * c.sub << ", a" << (r - r0) << "_" << y << " ^ r" << y << ");\n";
+            os << "    }\n  }\n";
+        }
+    } else if (elim) {  // V_r = R_r + sum_x ...: XOR the recovery row r (zero page if absent)
         for (int r = r0; r < r1; ++r) {
             os << "  {\n    const unsigned char *rp = lh_slot(slv, " << k + r << ", base, zero);\n";
             for (int y = 0; y < 8; ++y)
@@ -271,12 +292,60 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
        << "  const unsigned int s = (unsigned int)__builtin_amdgcn_readlane((int)slv[i / 64], i % 64);\n"
        << "  return s == 0xFFu ? zero : base + (long long)s * " << c.bytes << ";\n}\n";
     for (int g = 0; g < NG; ++g) emit_win_group(os, c, G, g);
+    if (c.win_split) {
+        // Phase A only: every present recovery block R_r becomes V_r in place; phase B is
+        // lh_inverse_kernel (kernels.hip), launched after this kernel on the same stream.
+        // No V tile in LDS: the workgroup holds only the column-tile ring, so occupancy is
+        // set by registers, not by m x 2 KiB of LDS.
+        os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
+           << "lh_jit_decode_wide(unsigned char *__restrict__ blocks, long long stride,\n"
+           << "                   const unsigned char *__restrict__ plan, long long plan_stride,\n"
+           << "                   const unsigned char *__restrict__ zero_page, int stripes) {\n"
+           << "  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
+           << "  const int lane = threadIdx.x & 63;\n"
+           << "  const long long stripe = blockIdx.x / " << CPS << ";\n"
+           << "  if (stripe >= stripes) return;\n"
+           << "  const unsigned char *pl = plan + stripe * plan_stride;\n"
+           << "  if (pl[0] == 0) return;\n"
+           << "  unsigned int slv[LH_NQ];\n"
+           << "#pragma unroll\n  for (int q = 0; q < LH_NQ; ++q) {\n"
+           << "    const int i = q * 64 + lane;\n"
+           << "    slv[q] = i < " << km << " ? (unsigned int)pl[" << 16 + e_max << " + i] : 0xFFu;\n"
+           << "  }\n"
+           << "  const int chunk = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << ";\n"
+           << "  unsigned char *b = blocks + stripe * stride + chunk + lane * " << c.W << ";\n"
+           << "  const unsigned char *z = zero_page + chunk + lane * " << c.W << ";\n";
+        const char *dargs = "(b, z, slv, nullptr)";
+        if (c.win_lds) {
+            os << "  const unsigned char *sb = blocks + stripe * stride + chunk;\n"
+               << "  const unsigned char *zb = zero_page + chunk;\n";
+            dargs = "(b, z, slv, nullptr, sb, zb)";
+        }
+        for (int g = 0; g < NG; ++g) os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << dargs << ";\n";
+        os << "}\n";
+        return;
+    }
     // Phase B: coefficients are workgroup-uniform, so each coefficient bit is a scalar
     // branch and only set bits cost XORs; V_r is doubled in place (B(2) in bit-sliced
     // form: (v1..v7, v0^v1^v2^v7)).  (A nibble-windowed variant -- a 16-way uniform switch
     // per output and nibble with XOR3-paired cases -- measured 1.2-1.3x slower.)
     os << "#ifndef LH_PB_MASK  // masks: k128/m32 decode 7.0 ms against 6.5 ms with branches\n#define LH_PB_MASK 0\n#endif\n";
     os << "#ifndef LH_PB_PAIR  // bits in pairs, XOR3 when both set: 7.2 ms against 6.2 (k128/m32 decode)\n#define LH_PB_PAIR 0\n#endif\n";
+    // LH_PB_FR: no per-bit branches.  Per used row, the 16-entry XOR tables of V_r's
+    // sub-rows 0..3 and 4..7 sit in registers; output sub-row y of B(c) V_r is
+    // tl[lo_y] ^ th[hi_y], where (lo_y, hi_y) are the nibbles of byte y of the bit-matrix
+    // of c (from lh_bmtab, read per lane once per output group, then v_readlane).  The
+    // wave-uniform table index becomes a VGPR-indexed move (s_set_gpr_idx_on / v_mov /
+    // off): 3 VALU + 4 SALU per output sub-row, 74 instructions per (output, row) against
+    // ~52 for the branches.  Measured slower: k128/m32 decode 5.89 against 5.57 ms,
+    // k200/m56 1.41 against 1.14 ms (profiles/r2_tune_pb_fr.txt).
+    os << "#ifndef LH_PB_FR\n#define LH_PB_FR 0\n#endif\n#if LH_PB_FR\n";
+    os << "__device__ const unsigned int lh_bmtab[512] = {";
+    for (int c = 0; c < 256; ++c) {
+        const uint64_t bm = bitmatrix((uint8_t)c);
+        os << (unsigned)(bm & 0xFFFFFFFFu) << "u," << (unsigned)(bm >> 32) << "u" << (c < 255 ? "," : "");
+    }
+    os << "};\n#endif\n";
     // The coefficients of the wave's 8 outputs for used row j sit packed in lane j
     // (cpk0: outputs 0..3, cpk1: 4..7) and come back as SGPRs through v_readlane, and the
     // next row's V is read from LDS while the current row is applied, so no LDS round
@@ -293,6 +362,13 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
        << "        cpk0 |= (i0 + i < e ? (unsigned int)cf[(i0 + i) * " << c.m << " + ur] : 0u) << (8 * i);\n"
        << "        cpk1 |= (i0 + 4 + i < e ? (unsigned int)cf[(i0 + 4 + i) * " << c.m << " + ur] : 0u) << (8 * i);\n"
        << "      }\n    }\n"
+       << "#if LH_PB_FR  // bit-matrices of the wave's 8 coefficients of used row `lane`\n"
+       << "    unsigned int bmv[8][2];\n"
+       << "#pragma unroll\n    for (int i = 0; i < 8; ++i) {\n"
+       << "      const unsigned int c = (i < 4 ? cpk0 >> (8 * i) : cpk1 >> (8 * (i - 4))) & 0xFFu;\n"
+       << "      bmv[i][0] = lh_bmtab[2 * c];\n      bmv[i][1] = lh_bmtab[2 * c + 1];\n"
+       << "    }\n"
+       << "#endif\n"
        << "    unsigned int acc[8][8];\n"
        << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n#pragma unroll\n      for (int y = 0; y < 8; ++y) acc[i][y] = 0;\n"
        << "    unsigned int v[8], vn[8];\n"
@@ -306,7 +382,23 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
        << "      }\n"
        << "      const unsigned int c0 = (unsigned int)__builtin_amdgcn_readlane((int)cpk0, j);\n"
        << "      const unsigned int c1 = (unsigned int)__builtin_amdgcn_readlane((int)cpk1, j);\n"
-       << "#if LH_PB_PAIR  // bits (2q, 2q + 1) of a coefficient together: both set -> one XOR3\n"
+       << "#if LH_PB_FR\n"
+       << "      unsigned int tl[16], th[16];\n"
+       << "      tl[0] = 0u;\n      th[0] = 0u;\n"
+       << "#pragma unroll\n      for (int n = 1; n < 16; ++n) {\n"
+       << "        const int low = __builtin_ctz(n), pre = n & (n - 1);\n"
+       << "        tl[n] = pre ? (tl[pre] ^ v[low]) : v[low];\n"
+       << "        th[n] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];\n"
+       << "      }\n"
+       << "#pragma unroll\n      for (int i = 0; i < 8; ++i) {\n"
+       << "        if (i0 + i >= e) continue;\n"
+       << "        const unsigned int b0 = (unsigned int)__builtin_amdgcn_readlane((int)bmv[i][0], j);\n"
+       << "        const unsigned int b1 = (unsigned int)__builtin_amdgcn_readlane((int)bmv[i][1], j);\n"
+       << "#pragma unroll\n        for (int y = 0; y < 8; ++y) {\n"
+       << "          const unsigned int s = ((y < 4 ? b0 : b1) >> (8 * (y & 3))) & 0xFFu;\n"
+       << "          acc[i][y] = __builtin_amdgcn_bitop3_b32(acc[i][y], tl[s & 15u], th[s >> 4], 0x96);\n"
+       << "        }\n      }\n"
+       << "#elif LH_PB_PAIR  // bits (2q, 2q + 1) of a coefficient together: both set -> one XOR3\n"
        << "#pragma unroll\n      for (int q = 0; q < 4; ++q) {\n"
        << "        unsigned int w[8];  // w = B(2) v: the ladder entry of bit 2q + 1\n"
        << "        {\n          const unsigned int t7 = __builtin_amdgcn_bitop3_b32(v[0], v[1], v[2], 0x96) ^ v[7];\n"
@@ -514,7 +606,7 @@ std::string jit_source_for(const JitConfig &c) {
 
 const JitKernels *JitCache::peek(const JitConfig &cfg) {
     std::lock_guard<std::mutex> g(mu_);
-    auto it = cache_.find(Key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines, cfg.win * 100000 + cfg.win_lds * 10000 + cfg.rows_per_wave * 100 + cfg.win_pf));
+    auto it = cache_.find(Key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines, cfg.win_split * 1000000 + cfg.win * 100000 + cfg.win_lds * 10000 + cfg.rows_per_wave * 100 + cfg.win_pf));
     return it == cache_.end() ? nullptr : &it->second;
 }
 
@@ -628,7 +720,7 @@ bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::str
 
 const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err) {
     std::lock_guard<std::mutex> g(mu_);
-    const Key key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines, cfg.win * 100000 + cfg.win_lds * 10000 + cfg.rows_per_wave * 100 + cfg.win_pf);
+    const Key key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines, cfg.win_split * 1000000 + cfg.win * 100000 + cfg.win_lds * 10000 + cfg.rows_per_wave * 100 + cfg.win_pf);
     auto it = cache_.find(key);
     if (it != cache_.end()) return &it->second;
 

@@ -611,6 +611,128 @@ __global__ void __launch_bounds__(256) lh_frame_kernel(lh::FrameArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ large-m decode, phase B
+// After the windowed phase-A kernel (jit.cpp, split modules) has replaced every present
+// recovery block R_r by V_r = R_r + sum_{x present} B(G[r][x]) D_x in place:
+// D_{E_i} = sum_r B(coef[i][r]) V_r (the reference's back-substitution,
+// cauchy_256.cpp:1083-1247; same unique solution).  One workgroup per (stripe, 256-byte
+// chunk of every sub-block), nw = ceil(e_max / 8) waves; wave g recovers outputs g,
+// g + nw, ... (at most 8) of the stripe's e.  For each used recovery row r (ascending:
+// the plan's coefficient columns) the wave reads V_r's chunk (one dword per lane and
+// sub-block, two rows ahead, from L2 after the first wave) and adds B(coef[i][r]) V_r to
+// every output by Horner over the coefficient bits: coefficients are wave-uniform, so a
+// bit is a scalar branch and only set bits cost XORs; V is doubled in place
+// (B(2) v = (v1..v7, v0^v1^v2^v7)).  Every wave has read every V row before any output is
+// written (workgroup barrier): the outputs go to the recovery blocks' slots, where V is.
+// No LDS and ~100 VGPRs: several waves per SIMD hide the branch latency that the fused
+// kernel (an m x 2 KiB V tile per workgroup, 2 waves per SIMD) could not.
+__device__ __forceinline__ void lh_inv_load(uint32_t (&d)[8], const uint8_t *base, uint32_t rslot,
+                                            unsigned long long mk, int bytes, int sub) {
+    const int r = __builtin_ctzll(mk);
+    const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)rslot, r);
+    const uint8_t *p = base + (long long)slot * bytes;
+#pragma unroll
+    for (int y = 0; y < 8; ++y) d[y] = *(const uint32_t *)(p + (long long)y * sub);
+}
+
+template <int OPW, int NO>
+__device__ __forceinline__ void lh_inv_rows(uint32_t (&acc)[OPW][8], const uint8_t *base, uint32_t rslot,
+                                            unsigned long long used, uint32_t cpk0, uint32_t cpk1, int bytes,
+                                            int sub) {
+    uint32_t n0[8], n1[8];
+    unsigned long long pf = used;  // rows not yet loaded
+    lh_inv_load(n0, base, rslot, pf, bytes, sub);
+    pf &= pf - 1;
+    if (pf) {
+        lh_inv_load(n1, base, rslot, pf, bytes, sub);
+        pf &= pf - 1;
+    }
+    for (unsigned long long rest = used; rest; rest &= rest - 1) {
+        const int r = __builtin_ctzll(rest);
+        uint32_t v[8];
+#pragma unroll
+        for (int y = 0; y < 8; ++y) {
+            v[y] = n0[y];
+            n0[y] = n1[y];
+        }
+        if (pf) {
+            lh_inv_load(n1, base, rslot, pf, bytes, sub);
+            pf &= pf - 1;
+        }
+        const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)cpk0, r);
+        const uint32_t c1 = OPW > 4 ? (uint32_t)__builtin_amdgcn_readlane((int)cpk1, r) : 0u;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+#pragma unroll
+            for (int i = 0; i < NO; ++i) {
+                if (__builtin_expect(((i < 4 ? c0 : c1) >> (8 * (i & 3) + t)) & 1u, 1))
+#pragma unroll
+                    for (int y = 0; y < 8; ++y) acc[i][y] ^= v[y];
+            }
+            if (t < 7) {
+                const uint32_t t7 = __builtin_amdgcn_bitop3_b32(v[0], v[1], v[2], 0x96) ^ v[7];
+#pragma unroll
+                for (int y = 0; y < 7; ++y) v[y] = v[y + 1];
+                v[7] = t7;
+            }
+        }
+    }
+}
+
+// OPW: outputs per wave (8, or 4: twice the waves, half the accumulators).
+template <int OPW>
+__global__ void __launch_bounds__(1024) lh_inverse_kernel(lh::InverseArgs a) {
+    const int nw = (int)(blockDim.x >> 6);
+    const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = (int)(threadIdx.x & 63);
+    const int cps = a.bytes >> 11;  // 256-byte chunks per sub-block
+    const long long stripe = blockIdx.x / cps;
+    if (stripe >= a.stripes) return;  // workgroup-uniform
+    const uint8_t *pl = a.plan + stripe * a.plan_stride;
+    const int e = pl[0];
+    if (e == 0) return;  // workgroup-uniform: nothing to recover, or invalid rows
+    const int m = a.m, sub = a.bytes >> 3;
+    const lh::PlanView pv(pl, a.k, m, a.e_max);
+    const uint32_t rslot = lane < m ? (uint32_t)pv.rec_slot(lane) : 0xFFu;
+    const unsigned long long used = __ballot(rslot != 0xFFu);
+    const int nout = g < e ? (e - g + nw - 1) / nw : 0;  // outputs g, g + nw, ... < e
+    uint32_t cpk0 = 0, cpk1 = 0;  // lane r: coefficients of this wave's outputs for row r
+    if (rslot != 0xFFu) {
+        const uint8_t *cf = pv.coef_ptr();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (i < nout) cpk0 |= (uint32_t)cf[(g + i * nw) * m + lane] << (8 * i);
+            if (OPW > 4 && i + 4 < nout) cpk1 |= (uint32_t)cf[(g + (i + 4) * nw) * m + lane] << (8 * i);
+        }
+    }
+    uint8_t *base = a.blocks + stripe * a.stride + (int)(blockIdx.x % cps) * 256 + lane * 4;
+    uint32_t acc[OPW][8];
+#pragma unroll
+    for (int i = 0; i < OPW; ++i)
+#pragma unroll
+        for (int y = 0; y < 8; ++y) acc[i][y] = 0;
+    switch (nout) {  // wave-uniform
+        case 0: break;
+        case 1: lh_inv_rows<OPW, 1>(acc, base, rslot, used, cpk0, cpk1, a.bytes, sub); break;
+        case 2: lh_inv_rows<OPW, 2>(acc, base, rslot, used, cpk0, cpk1, a.bytes, sub); break;
+        case 3: lh_inv_rows<OPW, 3>(acc, base, rslot, used, cpk0, cpk1, a.bytes, sub); break;
+        case 4: lh_inv_rows<OPW, 4>(acc, base, rslot, used, cpk0, cpk1, a.bytes, sub); break;
+        case 5: lh_inv_rows<OPW, (OPW > 4 ? 5 : 4)>(acc, base, rslot, used, cpk0, cpk1, a.bytes, sub); break;
+        case 6: lh_inv_rows<OPW, (OPW > 4 ? 6 : 4)>(acc, base, rslot, used, cpk0, cpk1, a.bytes, sub); break;
+        case 7: lh_inv_rows<OPW, (OPW > 4 ? 7 : 4)>(acc, base, rslot, used, cpk0, cpk1, a.bytes, sub); break;
+        default: lh_inv_rows<OPW, OPW>(acc, base, rslot, used, cpk0, cpk1, a.bytes, sub); break;
+    }
+    __syncthreads();  // every V row read by every wave before the outputs overwrite them
+#pragma unroll
+    for (int i = 0; i < OPW; ++i) {
+        if (i < nout) {
+            uint8_t *dst = base + (long long)pv.out_slot(g + i * nw) * a.bytes;
+#pragma unroll
+            for (int y = 0; y < 8; ++y) __builtin_nontemporal_store(acc[i][y], (uint32_t *)(dst + (long long)y * sub));
+        }
+    }
+}
+
 // ------------------------------------------------------------------ host launchers
 namespace lh {
 
@@ -623,6 +745,25 @@ hipError_t launch_apply_generic(const ApplyArgs &a, int W, hipStream_t st) {
         case 4: hipLaunchKernelGGL(lh_apply_generic_kernel<4>, grid, dim3(256), 0, st, a); break;
         default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
+    // sub-blocks in 256-byte chunks (the windowed configurations: sub % 256 == 0)
+    if (a.bytes % 2048 != 0 || a.e_max < 1 || a.e_max > 64 || a.m > 64) return hipErrorInvalidValue;
+    const long long blocks = (long long)a.stripes * (a.bytes / 2048);
+    if (blocks <= 0) return hipSuccess;
+    if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+    // Outputs per wave: 4 (default; LONGHAIR_AMD_INV_OPW=8: half the waves, twice the
+    // accumulators: k128/m32 decode 4.24 against 4.12 ms).  (Rows taken in pairs, XOR3 when both
+    // coefficient bits are set, 25 % fewer XORs behind nested branches: 5.90 against 4.12 ms.)
+    const char *o = std::getenv("LONGHAIR_AMD_INV_OPW");
+    const int opw = (o && std::atoi(o) == 8) ? 8 : 4;
+    const unsigned threads = 64u * (unsigned)((a.e_max + opw - 1) / opw);
+    if (threads > 1024) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)blocks), block(threads);
+    if (opw == 4) hipLaunchKernelGGL(lh_inverse_kernel<4>, grid, block, 0, st, a);
+    else hipLaunchKernelGGL(lh_inverse_kernel<8>, grid, block, 0, st, a);
     return hipGetLastError();
 }
 

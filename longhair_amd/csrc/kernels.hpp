@@ -101,6 +101,17 @@ struct FrameArgs {
     int k, m, bytes, stripes, npk, unframe;
 };
 
+// Phase B of the large-m decode (after the windowed phase-A kernel replaced every present
+// recovery block R_r by V_r in place): D_{E_i} = sum_r B(coef[i][r]) V_r into out_slot(i).
+struct InverseArgs {
+    uint8_t *blocks;              // stripe s, slot j: blocks + s*stride + j*bytes
+    long long stride;
+    const uint8_t *plan;          // PlanView records
+    long long plan_stride;
+    int k, m, e_max, bytes, stripes;
+};
+
+hipError_t launch_inverse(const InverseArgs &a, hipStream_t st);
 hipError_t launch_apply_generic(const ApplyArgs &a, int W, hipStream_t st);
 hipError_t launch_frame(const FrameArgs &a, hipStream_t st);
 hipError_t launch_xor_reduce(const XorArgs &a, hipStream_t st);
