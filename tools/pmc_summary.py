@@ -13,10 +13,16 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
+def short(name):
+    """'void lh_inverse_kernel<4>(lh::InverseArgs)' -> 'lh_inverse_kernel'."""
+    name = name[5:] if name.startswith("void ") else name
+    return name.split("(")[0].split("<")[0]
+
+
 def per_kernel(path, counter):
     vals = {}
     for row in csv.DictReader(open(path)):
-        if row["Counter_Name"] == counter and row["Kernel_Name"].lstrip("void ").startswith("lh_"):
+        if row["Counter_Name"] == counter and short(row["Kernel_Name"]).startswith("lh_"):
             vals.setdefault(row["Kernel_Name"], []).append(float(row["Counter_Value"]))
     return {k: statistics.median(v) for k, v in vals.items()}
 
@@ -35,18 +41,17 @@ def main():
            "algorithmic_bytes_per_launch": alg, "kernels": {}}
     for name in sorted(set(f) | set(w)):
         fb, wb = f.get(name, 0.0) * 2048, w.get(name, 0.0) * 1024
-        res["kernels"][name] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb}
+        res["kernels"][short(name)] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb}
 
-    def pick(words):
-        for name, v in res["kernels"].items():
-            if any(wd in name for wd in words):
-                return name, v
-        return None, None
-    for role, words in (("encode", ["lh_jit_encode_win", "lh_jit_encode", "lh_apply_generic"]),
-                        ("decode", ["lh_jit_decode_fused", "lh_jit_decode_wide", "lh_jit_decode", "lh_apply_generic"])):
-        name, v = pick(words)
-        if v:
-            res[role] = dict(v, kernel=name, ratio_to_algorithmic=v["hbm_bytes_per_launch"] / alg[role])
+    # Each phase's traffic: the sum over the kernels one encode_batch / decode_batch launches
+    # (the large-m decode is planner + phase A + lh_inverse_kernel).
+    import longhair_amd as lh
+    for role, names in zip(("encode", "decode"), lh.kernel_names(k, m, nbytes)):
+        got = [res["kernels"][n] for n in names if n in res["kernels"]]
+        if got:
+            tot = {key: sum(v[key] for v in got) for key in ("fetch_bytes", "write_bytes", "hbm_bytes_per_launch")}
+            res[role] = dict(tot, kernel="+".join(n for n in names if n in res["kernels"]),
+                             ratio_to_algorithmic=tot["hbm_bytes_per_launch"] / alg[role])
     path = os.path.join(REPO, "profiles", f"pmc_{cfg}.json")
     json.dump(res, open(path, "w"), indent=1)
     print(json.dumps(res, indent=1))

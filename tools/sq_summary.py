@@ -12,12 +12,18 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def short(name):
+    """'void lh_inverse_kernel<4>(lh::InverseArgs)' -> 'lh_inverse_kernel'."""
+    name = name[5:] if name.startswith("void ") else name
+    return name.split("(")[0].split("<")[0]
+
+
 def main():
     path, cfg = sys.argv[1], sys.argv[2]
     per = {}
     for row in csv.DictReader(open(path)):
         name = row["Kernel_Name"]
-        if not name.lstrip("void ").startswith("lh_"):
+        if not short(name).startswith("lh_"):
             continue
         per.setdefault(name, {}).setdefault((row["Dispatch_Id"]), {})[row["Counter_Name"]] = float(row["Counter_Value"])
     out = {"config": cfg, "source": f"rocprofv3 --pmc SQ_* --kernel-trace of tools/prof_kernels.py {cfg}",
@@ -30,7 +36,7 @@ def main():
         if agg.get("SQ_WAVE_CYCLES"):
             agg["wait_any_frac"] = round(agg.get("SQ_WAIT_ANY", 0) / agg["SQ_WAVE_CYCLES"], 4)
         agg["dispatches"] = len(disp)
-        out["kernels"][name.split("(")[0]] = agg
+        out["kernels"][short(name)] = agg
     dst = os.path.join(REPO, "profiles", f"sq_{cfg}.json")
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
