@@ -123,7 +123,7 @@ struct Device {
     // host-batch pipeline: per ring slot a stream, device buffers and an event
     std::mutex pipe_mu;
     hipStream_t pipe_stream[3] = {nullptr, nullptr, nullptr};
-    DevBuf pipe_blocks[3], pipe_out[3], pipe_rows[3], pipe_status[3];
+    DevBuf pipe_blocks[3], pipe_out[3], pipe_rows[3], pipe_rows0[3], pipe_status[3];
 };
 
 static std::mutex g_devices_mu;
@@ -558,21 +558,33 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
     PipeDrain drain{d};
     const long long sz = (long long)k * bytes;
     chunk = auto_chunk(sz, stripes, chunk);
+    // Only the slots decode can write travel back: the recovery slots (for m == 1 the
+    // last one, or slot 0 when there is none: cauchy_decode_m1's quirk).  For k, m > 1 a
+    // kernel writes exactly those blocks into the caller's pinned buffer through its
+    // device mapping (lh_writeback_kernel); otherwise -- or when the buffer has no device
+    // mapping, or LONGHAIR_AMD_PIPE_WRITEBACK=range -- one 2-D copy per chunk covers the
+    // range [lo, hi] of such slots over the chunk's stripes (per-slot copies of small
+    // blocks would be dominated by per-call overhead), which with recovery blocks spread
+    // over the slots is most of the stripe.
+    uint8_t *h_dev = nullptr;
+    bool kernel_wb = k > 1 && m > 1;
+    if (const char *e = std::getenv("LONGHAIR_AMD_PIPE_WRITEBACK")) kernel_wb = kernel_wb && std::string(e) != "range";
+    if (kernel_wb && hipHostGetDevicePointer((void **)&h_dev, h_blocks, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        kernel_wb = false;
+    }
     for (int i = 0; i < 3; ++i) {
         LH_HIP(d->pipe_blocks[i].reserve((size_t)chunk * sz));
         LH_HIP(d->pipe_rows[i].reserve((size_t)chunk * k));
+        if (kernel_wb) LH_HIP(d->pipe_rows0[i].reserve((size_t)chunk * k));
         LH_HIP(d->pipe_status[i].reserve((size_t)chunk));
     }
-    // Only the slots decode can write travel back: the recovery slots (for m == 1 the
-    // last one, or slot 0 when there is none: cauchy_decode_m1's quirk).  One 2-D copy per
-    // chunk covers the range [lo, hi] of such slots over the chunk's stripes (per-slot
-    // copies of small blocks would be dominated by per-call overhead).
     for (int s0 = 0, c = 0; s0 < stripes; s0 += chunk, ++c) {
         const int n = stripes - s0 < chunk ? stripes - s0 : chunk;
         const int i = c % 3;
         hipStream_t st = d->pipe_stream[i];
         int lo = k, hi = -1;  // slot range [lo, hi] decode may write in this chunk
-        if (k > 1) {
+        if (k > 1 && !kernel_wb) {
             for (int s = s0; s < s0 + n; ++s) {
                 const uint8_t *r = h_rows + (long long)s * k;
                 int first = -1, last = -1;  // first / last recovery slot of the stripe
@@ -590,10 +602,23 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
         LH_HIP(hipMemcpy2DAsync(d->pipe_blocks[i].ptr, sz, h_blocks + (long long)s0 * stride, stride, sz, n,
                                 hipMemcpyHostToDevice, st));
         LH_HIP(hipMemcpyAsync(d->pipe_rows[i].ptr, h_rows + (long long)s0 * k, (size_t)n * k, hipMemcpyHostToDevice, st));
+        if (kernel_wb)
+            LH_HIP(hipMemcpyAsync(d->pipe_rows0[i].ptr, d->pipe_rows[i].ptr, (size_t)n * k, hipMemcpyDeviceToDevice, st));
         const int rc = decode_batch(k, m, bytes, n, d->pipe_blocks[i].ptr, sz, d->pipe_rows[i].ptr,
                                     (int8_t *)d->pipe_status[i].ptr, st, true);
         if (rc != kOk) return rc;
-        if (hi >= lo) {
+        if (kernel_wb) {
+            WritebackArgs wa{};
+            wa.blocks = d->pipe_blocks[i].ptr;
+            wa.stride = sz;
+            wa.host = h_dev + (long long)s0 * stride;
+            wa.host_stride = stride;
+            wa.rows_orig = d->pipe_rows0[i].ptr;
+            wa.k = k;
+            wa.bytes = bytes;
+            wa.stripes = n;
+            LH_HIP(launch_writeback(wa, st));
+        } else if (hi >= lo) {
             const long long off = (long long)lo * bytes, w = (long long)(hi - lo + 1) * bytes;
             LH_HIP(hipMemcpy2DAsync(h_blocks + (long long)s0 * stride + off, stride, d->pipe_blocks[i].ptr + off, sz, w,
                                     n, hipMemcpyDeviceToHost, st));

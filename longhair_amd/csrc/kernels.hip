@@ -733,6 +733,31 @@ __global__ void __launch_bounds__(1024) lh_inverse_kernel(lh::InverseArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ pinned-host write-back
+// One workgroup per stripe: the slots whose row was a recovery row before the decode are
+// the slots decode may have written (its outputs; an invalid stripe is untouched, so the
+// copy is the host's own bytes).  16 B per lane when the block size allows, else 8 B
+// (bytes % 8 == 0 for m > 1).  Vector stores over PCIe into the mapped host buffer.
+__global__ void __launch_bounds__(256) lh_writeback_kernel(lh::WritebackArgs a) {
+    const long long s = blockIdx.x;
+    if (s >= a.stripes) return;
+    const uint8_t *rows = a.rows_orig + s * a.k;
+    const uint8_t *src = a.blocks + s * a.stride;
+    uint8_t *dst = a.host + s * a.host_stride;
+    const bool wide = (a.bytes & 15) == 0;
+    for (int j = 0; j < a.k; ++j) {
+        if (rows[j] < a.k) continue;  // workgroup-uniform
+        const long long off = (long long)j * a.bytes;
+        if (wide) {
+            for (int q = threadIdx.x; q < (a.bytes >> 4); q += blockDim.x)
+                ((uint4 *)(dst + off))[q] = ((const uint4 *)(src + off))[q];
+        } else {
+            for (int q = threadIdx.x; q < (a.bytes >> 3); q += blockDim.x)
+                ((uint2 *)(dst + off))[q] = ((const uint2 *)(src + off))[q];
+        }
+    }
+}
+
 // ------------------------------------------------------------------ host launchers
 namespace lh {
 
@@ -764,6 +789,13 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     const dim3 grid((unsigned)blocks), block(threads);
     if (opw == 4) hipLaunchKernelGGL(lh_inverse_kernel<4>, grid, block, 0, st, a);
     else hipLaunchKernelGGL(lh_inverse_kernel<8>, grid, block, 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_writeback(const WritebackArgs &a, hipStream_t st) {
+    if (a.stripes <= 0) return hipSuccess;
+    if (a.bytes % 8 != 0 || a.k < 1 || a.k > 255) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(lh_writeback_kernel, dim3((unsigned)a.stripes), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

@@ -112,6 +112,20 @@ struct InverseArgs {
 };
 
 hipError_t launch_inverse(const InverseArgs &a, hipStream_t st);
+
+// Pinned-host decode pipeline: write every slot that held a recovery block before the
+// decode (rows_orig >= k: the only slots decode writes) straight into the caller's pinned
+// host buffer (device-mapped pointer), so only the recovered blocks cross PCIe back.
+struct WritebackArgs {
+    const uint8_t *blocks;        // device chunk: stripe s, slot j at blocks + s*stride + j*bytes
+    long long stride;
+    uint8_t *host;                // device-mapped pinned host buffer of the chunk
+    long long host_stride;
+    const uint8_t *rows_orig;     // the chunk's Block.row bytes before the decode, stripes x k
+    int k, bytes, stripes;
+};
+
+hipError_t launch_writeback(const WritebackArgs &a, hipStream_t st);
 hipError_t launch_apply_generic(const ApplyArgs &a, int W, hipStream_t st);
 hipError_t launch_frame(const FrameArgs &a, hipStream_t st);
 hipError_t launch_xor_reduce(const XorArgs &a, hipStream_t st);

@@ -315,10 +315,14 @@ def test_baseline_scale_roundtrip(lh):
 # ------------------------------------------------------------- host-batch pipeline
 
 
+@pytest.mark.parametrize("writeback", ["kernel", "range"])
 @pytest.mark.parametrize("k,m,nbytes,stripes,chunk", [(29, 4, 1296, 1000, 96), (17, 6, 520, 77, 0),
                                                       (29, 1, 1296, 50, 8), (128, 32, 8192, 5, 2)])
-def test_host_batch_pipeline(lh, oracle, k, m, nbytes, stripes, chunk):
+def test_host_batch_pipeline(lh, oracle, k, m, nbytes, stripes, chunk, writeback, monkeypatch):
+    """Pinned-host pipeline against the oracle, with the recovered blocks written back by
+    lh_writeback_kernel (default) or by the per-chunk slot-range copy."""
     import torch
+    monkeypatch.setenv("LONGHAIR_AMD_PIPE_WRITEBACK", writeback)
     data = lhutil.fill(k * 3 + m, stripes * k * nbytes).reshape(stripes, k, nbytes)
     pinned = torch.from_numpy(data).pin_memory()
     rec = lh.encode_host_batch(pinned.numpy(), m, chunk_stripes=chunk)
@@ -343,6 +347,12 @@ def test_host_batch_pipeline(lh, oracle, k, m, nbytes, stripes, chunk):
     assert (status == 0).all()
     assert np.array_equal(pr, exp_rows)
     assert np.array_equal(pb, exp_blocks)
+    if writeback == "kernel" and m > 1:
+        # pageable buffers have no device mapping: the range copy takes over
+        blocks2, rows2 = blocks.copy(), rows.copy()
+        status = lh.decode_host_batch(blocks2, rows2, m, chunk_stripes=chunk)
+        assert (status == 0).all()
+        assert np.array_equal(rows2, exp_rows) and np.array_equal(blocks2, exp_blocks)
 
 
 # ------------------------------------------------------------------- packet framing
