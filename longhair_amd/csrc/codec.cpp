@@ -5,6 +5,7 @@
 // byte of encode/decode output is produced by GPU kernels (kernels.hip, jit_codec.hip).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -504,9 +505,18 @@ struct PipeDrain {
     }
 };
 
-static int auto_chunk(long long stripe_bytes, int stripes, int chunk) {
+// Stripes per pipeline chunk: ~64 MiB for the encode; the decode's three kernels need
+// larger launches to fill the GPU, so up to 256 MiB while keeping >= 4 chunks in flight
+// (tools/pcie_bench.py PCIE_CHUNK sweep, shuffled slots: k200/m56 decode 39.1 GB/s at 5
+// stripes per chunk, 43.3 at 10, 45.4 at 16; k29/m4 46.7 at 2048, 48.4 at 8192).
+static int auto_chunk(long long stripe_bytes, int stripes, int chunk, bool decode = false) {
     if (chunk > 0) return chunk < stripes ? chunk : stripes;
-    long long c = (64ll << 20) / (stripe_bytes > 0 ? stripe_bytes : 1);  // ~64 MiB per chunk
+    const long long sb = stripe_bytes > 0 ? stripe_bytes : 1;
+    long long c = (64ll << 20) / sb;
+    if (decode) {
+        const long long big = (256ll << 20) / sb, quarter = ((long long)stripes + 3) / 4;
+        c = std::max(c, std::min(big, quarter));
+    }
     if (c < 1) c = 1;
     return (int)(c < stripes ? c : stripes);
 }
@@ -557,7 +567,7 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
     if (int rc = pipe_streams(d)) return rc;
     PipeDrain drain{d};
     const long long sz = (long long)k * bytes;
-    chunk = auto_chunk(sz, stripes, chunk);
+    chunk = auto_chunk(sz, stripes, chunk, true);
     // Only the slots decode can write travel back: the recovery slots (for m == 1 the
     // last one, or slot 0 when there is none: cauchy_decode_m1's quirk).  For k, m > 1 a
     // kernel writes exactly those blocks into the caller's pinned buffer through its
