@@ -450,10 +450,13 @@ struct lh_dsrc {
         return slot == 0xFFu ? (int)0x80000000 : lbase + (int)slot * LH_BYTES;
     }
 };
+// NT: non-temporal loads for this column.  LH_NT_DEC == 2: data columns non-temporal (read
+// once, never written), recovery rows -- the slots the outputs overwrite -- default policy.
+template <bool NT = (LH_NT_DEC == 1)>
 __device__ __forceinline__ void lh_load_col(lh_word (&d)[8], const lh_dsrc &S, unsigned int slot) {
     const int off = S.col(slot);
 #pragma unroll
-    for (int b = 0; b < 8; ++b) d[b] = lh_load_buf<LH_NT_DEC ? 2 : 0>(S.rs, off + b * LH_SUB);
+    for (int b = 0; b < 8; ++b) d[b] = lh_load_buf<NT ? 2 : 0>(S.rs, off + b * LH_SUB);
 }
 #else
 // Column source of a lane: its stripe's chunk pointer and the zero page.
@@ -510,7 +513,12 @@ struct lh_unroll_decode {
                                                const unsigned int (&recw)[LH_NREC]) {
         if (X + LH_PF_DEC < LH_DCOLS) {
             lh_word nxt[8];
+#if LH_BUF
+            lh_load_col<LH_NT_DEC == 1 || (LH_NT_DEC == 2 && X + LH_PF_DEC < LH_K)>(
+                nxt, S, lh_dcol_slot<(X + LH_PF_DEC < LH_DCOLS ? X + LH_PF_DEC : 0)>(srcw, recw));
+#else
             lh_load_col(nxt, S, lh_dcol_slot<(X + LH_PF_DEC < LH_DCOLS ? X + LH_PF_DEC : 0)>(srcw, recw));
+#endif
             lh_dcombine<X>(acc, ring[X % LH_PF_DEC]);
             lh_opaque(acc);
 #pragma unroll
@@ -550,7 +558,11 @@ __device__ __forceinline__ void lh_dec_issue(lh_word (&ring)[LH_PF_DEC][8], cons
                                 : (q == 1) ? lh_dcol_slot<1>(pr.srcw, pr.recw)
                                 : (q == 2) ? lh_dcol_slot<2>(pr.srcw, pr.recw)
                                            : lh_dcol_slot<3>(pr.srcw, pr.recw);
+#if LH_BUF
+        lh_load_col<LH_NT_DEC != 0>(ring[q], S, slot);  // the first columns are data columns
+#else
         lh_load_col(ring[q], S, slot);
+#endif
     }
 }
 

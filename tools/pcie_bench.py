@@ -68,7 +68,7 @@ def run(name, reps=3):
             "encode_GBps_pcie_inclusive": round(inb / enc / 1e9, 2),
             "decode_GBps_pcie_inclusive": round(inb / dec / 1e9, 2),
             "encode_s": round(enc, 5), "decode_s": round(dec, 5),
-            "slots": "shuffled" if SHUFFLE else "recovery blocks last", "chunk_stripes": CHUNK or "auto (~64 MiB)",
+            "slots": "shuffled" if SHUFFLE else "recovery blocks last", "chunk_stripes": CHUNK or "auto (encode ~64 MiB, decode <= 256 MiB)",
             "writeback": os.environ.get("LONGHAIR_AMD_PIPE_WRITEBACK", "kernel"),
             "note": "pinned host in/out, 3-stream chunked pipeline, input GB/s (1e9)"}
 
