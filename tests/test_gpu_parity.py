@@ -237,6 +237,20 @@ def _decode_scenarios(k, m, nbytes, stripes, seed, e=None):
     (100, 16, 2048, 12, None), (40, 20, 4096, 8, None), (250, 6, 2048, 8, None),
 ])
 def test_decode_batch_vs_oracle(lh, oracle, path, k, m, nbytes, stripes, e):
+    _decode_batch_vs_oracle(lh, oracle, k, m, nbytes, stripes, e)
+
+
+@pytest.mark.parametrize("knob,value", [("LONGHAIR_AMD_WIN_SPLIT", "0"), ("LONGHAIR_AMD_INV_OPW", "8")])
+@pytest.mark.parametrize("k,m,nbytes,stripes", [(40, 20, 4096, 8), (100, 16, 2048, 6)])
+def test_wide_decode_variants(lh, oracle, monkeypatch, knob, value, k, m, nbytes, stripes):
+    """Large-m decode with the non-default kernels: the fused phase A + B kernel
+    (LONGHAIR_AMD_WIN_SPLIT=0) and lh_inverse_kernel with 8 outputs per wave."""
+    monkeypatch.setenv(knob, value)
+    assert lh.batch_path(k, m, nbytes, True) == "jit-wide"
+    _decode_batch_vs_oracle(lh, oracle, k, m, nbytes, stripes, None)
+
+
+def _decode_batch_vs_oracle(lh, oracle, k, m, nbytes, stripes, e):
     import torch
     data = lhutil.fill(k + m + nbytes, stripes * k * nbytes).reshape(stripes, k, nbytes)
     slots, rows = _decode_scenarios(k, m, nbytes, stripes, seed=nbytes + k, e=e)
