@@ -17,6 +17,8 @@ TESTS = [(29, 2, 1296), (29, 3, 1296), (29, 8, 1296), (4, 2, 16), (10, 6, 8), (1
          (3, 250, 24), (2, 2, 8), (29, 4, 1304), (9, 7, 72), (29, 2, 16), (10, 8, 24),
          (128, 32, 1024), (5, 3, 8), (100, 16, 2048), (40, 20, 4096), (250, 6, 2048), (10, 6, 24), (3, 2, 8),
          (64, 4, 4096), (64, 3, 4096), (64, 2, 8192)]
+# Shapes whose fused large-m decode (LONGHAIR_AMD_WIN_SPLIT=0) the GPU tests run.
+VARIANT_SHAPES = [(40, 20, 4096), (100, 16, 2048)]
 
 
 def main():
@@ -43,10 +45,15 @@ def main():
             # the large-m shapes' encode and decode modules compile in separate processes
             jobs_list = [(s, part) for s in slow[:2] for part in ("dec", "enc")]
             jobs_list += [(s, None) for s in slow[2:] + [s for s in DEFAULT + TESTS if s not in slow]]
+            # non-default kernels the GPU tests also run (test_wide_decode_variants)
+            jobs_list += [(s, ("dec", {"LONGHAIR_AMD_WIN_SPLIT": "0"})) for s in VARIANT_SHAPES]
 
             def run(job):
                 shape, part = job
                 env = dict(os.environ)
+                if isinstance(part, tuple):
+                    part, extra = part
+                    env.update(extra)
                 if part:
                     env["LONGHAIR_AMD_PRECOMPILE_PART"] = part
                 return subprocess.run(cmd + [str(v) for v in shape], env=env)
