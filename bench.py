@@ -494,6 +494,13 @@ def main():
                                    "valu_insts_per_launch": insts, "valu_source": f"profiles/sq_{args.config}.json",
                                    "hbm": hbm}
         out["kernels"] = roof
+        if args.config == "k29m4":
+            # BASELINE north star: >= 70 % of the HBM-read roofline on the k29/m4 encode
+            # (input bytes read per second by the encode kernel / HBM peak).
+            enc_in = k * nbytes * stripes / (enc_ms * 1e-3) / 1e9
+            out["north_star"] = {"kernel": "+".join(enc_k), "input_read_GBps": round(enc_in, 1),
+                                 "frac_of_hbm_peak": round(enc_in / HBM_PEAK_GBS, 4), "target": 0.70,
+                                 "frac_of_measured_read_ceiling": round(enc_in / HBM_CEILING_GBS, 4)}
     if rank == 0 and world == 1 and not dry:
         calls = args.dropin_calls if args.dropin_calls >= 0 else max(10, min(2000, int(4e7 / (k * nbytes))))
         if calls:

@@ -579,6 +579,7 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
     uint8_t *h_dev = nullptr;
     bool kernel_wb = k > 1 && m > 1;
     if (const char *e = std::getenv("LONGHAIR_AMD_PIPE_WRITEBACK")) kernel_wb = kernel_wb && std::string(e) != "range";
+    if (((uintptr_t)h_blocks | (uintptr_t)stride | (uintptr_t)bytes) & 7) kernel_wb = false;  // 8-byte lanes
     if (kernel_wb && hipHostGetDevicePointer((void **)&h_dev, h_blocks, 0) != hipSuccess) {
         (void)hipGetLastError();
         kernel_wb = false;

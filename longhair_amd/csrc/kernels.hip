@@ -744,7 +744,7 @@ __global__ void __launch_bounds__(256) lh_writeback_kernel(lh::WritebackArgs a) 
     const uint8_t *rows = a.rows_orig + s * a.k;
     const uint8_t *src = a.blocks + s * a.stride;
     uint8_t *dst = a.host + s * a.host_stride;
-    const bool wide = (a.bytes & 15) == 0;
+    const bool wide = ((a.bytes | a.host_stride | (long long)(uintptr_t)a.host) & 15) == 0;
     for (int j = 0; j < a.k; ++j) {
         if (rows[j] < a.k) continue;  // workgroup-uniform
         const long long off = (long long)j * a.bytes;
@@ -794,7 +794,9 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
 
 hipError_t launch_writeback(const WritebackArgs &a, hipStream_t st) {
     if (a.stripes <= 0) return hipSuccess;
-    if (a.bytes % 8 != 0 || a.k < 1 || a.k > 255) return hipErrorInvalidValue;
+    // 8-byte lanes need 8-byte aligned blocks on the host side (16-byte lanes when aligned)
+    if (((a.bytes | a.host_stride | (long long)(uintptr_t)a.host) & 7) != 0 || a.k < 1 || a.k > 255)
+        return hipErrorInvalidValue;
     hipLaunchKernelGGL(lh_writeback_kernel, dim3((unsigned)a.stripes), dim3(256), 0, st, a);
     return hipGetLastError();
 }
