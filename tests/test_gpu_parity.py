@@ -369,6 +369,38 @@ def test_host_batch_pipeline(lh, oracle, k, m, nbytes, stripes, chunk, writeback
         assert np.array_equal(rows2, exp_rows) and np.array_equal(blocks2, exp_blocks)
 
 
+@pytest.mark.parametrize("offset", [8, 4])
+def test_host_batch_unaligned(lh, oracle, offset):
+    """Pinned blocks at an 8-byte (write-back kernel, 8-byte lanes) and a 4-byte offset
+    (range copy) from a 16-byte boundary."""
+    import torch
+    k, m, nbytes, stripes = 29, 4, 1296, 40
+    data = lhutil.fill(offset + 77, stripes * k * nbytes).reshape(stripes, k, nbytes)
+    rec = np.stack([oracle.encode(k, m, data[s], nbytes)[1].reshape(m, nbytes) for s in range(stripes)])
+    slots, rws = _decode_scenarios(k, m, nbytes, stripes, seed=offset)
+    blocks = np.zeros_like(data)
+    for s in range(stripes):
+        for i, (kind, x) in enumerate(slots[s]):
+            blocks[s, i] = data[s, x] if kind == "d" else rec[s, x]
+    rows = np.array(rws, dtype=np.uint8)
+    exp_blocks, exp_rows = blocks.copy(), rows.copy()
+    for s in range(stripes):
+        bufs = [exp_blocks[s, i].copy() for i in range(k)]
+        rc, r = oracle.decode(k, m, bufs, list(exp_rows[s]), nbytes)
+        exp_blocks[s] = np.stack(bufs)
+        exp_rows[s] = r
+    raw = torch.empty(blocks.nbytes + 64, dtype=torch.uint8).pin_memory().numpy()
+    base = (-raw.ctypes.data) % 16 + offset
+    pb = raw[base:base + blocks.nbytes].reshape(blocks.shape)
+    assert pb.ctypes.data % 16 == offset
+    pb[:] = blocks
+    pr = torch.from_numpy(rows).pin_memory().numpy()
+    status = lh.decode_host_batch(pb, pr, m, chunk_stripes=16)
+    assert (status == 0).all()
+    assert np.array_equal(pr, exp_rows)
+    assert np.array_equal(pb, exp_blocks)
+
+
 # ------------------------------------------------------------------- packet framing
 
 
