@@ -40,11 +40,13 @@ int cauchy_256_decode_batch(int k, int m, int block_bytes, int stripes,
                             unsigned char *d_rows, signed char *d_status, void *stream);
 
 /* Host-memory batches: the same operations on stripes that live
- * in host memory, pipelined in chunks of `chunk_stripes` (0 = about 64 MiB) over three
- * streams so the PCIe copies overlap the kernels.  Host buffers should be pinned
- * (hipHostMalloc / hipHostRegister).  Synchronous: returns when the results are in
- * host memory.  Decode copies back the slots decode can write (the recovery slots of each
- * chunk's stripes) and the rewritten rows. */
+ * in host memory, pipelined in chunks of `chunk_stripes` (0 = about 64 MiB for encode,
+ * up to 256 MiB with at least 4 chunks for decode) over three streams so the PCIe copies
+ * overlap the kernels.  Host buffers should be pinned (hipHostMalloc / hipHostRegister).
+ * Synchronous: returns when the results are in host memory.  Decode writes back only the
+ * slots decode can write (each stripe's recovery slots) and the rewritten rows: for k, m > 1
+ * with pinned, 8-byte-aligned blocks a kernel stores exactly those blocks through the
+ * buffer's device mapping; otherwise one copy per chunk covers their slot range. */
 int cauchy_256_encode_host_batch(int k, int m, int block_bytes, int stripes,
                                  const void *h_data, long long data_stride,
                                  void *h_recovery, long long recovery_stride, int chunk_stripes);
