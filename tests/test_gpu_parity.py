@@ -401,6 +401,39 @@ def test_host_batch_unaligned(lh, oracle, offset):
     assert np.array_equal(pb, exp_blocks)
 
 
+@pytest.mark.parametrize("writeback", ["kernel", "range"])
+def test_host_batch_padded_stride(lh, oracle, monkeypatch, writeback):
+    """Pinned stripes with a padded stripe stride through the C ABI: the write-back kernel
+    and the range copy honour the stride, and the padding is never written."""
+    import torch
+    monkeypatch.setenv("LONGHAIR_AMD_PIPE_WRITEBACK", writeback)
+    k, m, nbytes, stripes, pad = 17, 6, 520, 30, 72
+    stride = k * nbytes + pad
+    data = lhutil.fill(pad + 5, stripes * k * nbytes).reshape(stripes, k, nbytes)
+    slots, rws = _decode_scenarios(k, m, nbytes, stripes, seed=pad)
+    raw = torch.full((stripes * stride,), 0xA5, dtype=torch.uint8).pin_memory().numpy()
+    view = raw.reshape(stripes, stride)
+    exp = view.copy()
+    rows = np.array(rws, dtype=np.uint8)
+    exp_rows = rows.copy()
+    for s in range(stripes):
+        rc, rec = oracle.encode(k, m, data[s], nbytes)
+        rec = rec.reshape(m, nbytes)
+        blk = np.stack([data[s, x] if kind == "d" else rec[x] for kind, x in slots[s]])
+        view[s, :k * nbytes] = blk.reshape(-1)
+        bufs = [blk[i].copy() for i in range(k)]
+        rc, r = oracle.decode(k, m, bufs, list(exp_rows[s]), nbytes)
+        exp[s, :k * nbytes] = np.stack(bufs).reshape(-1)
+        exp_rows[s] = r
+    pr = torch.from_numpy(rows).pin_memory().numpy()
+    status = np.zeros(stripes, dtype=np.int8)
+    rc = lh.lib().cauchy_256_decode_host_batch(k, m, nbytes, stripes, raw.ctypes.data, stride, pr.ctypes.data,
+                                               status.ctypes.data, 8)
+    assert rc == 0 and (status == 0).all()
+    assert np.array_equal(pr, exp_rows)
+    assert np.array_equal(view, exp)
+
+
 # ------------------------------------------------------------------- packet framing
 
 
