@@ -340,21 +340,9 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
     // per output and nibble with XOR3-paired cases -- measured 1.2-1.3x slower.)
     os << "#ifndef LH_PB_MASK  // masks: k128/m32 decode 7.0 ms against 6.5 ms with branches\n#define LH_PB_MASK 0\n#endif\n";
     os << "#ifndef LH_PB_PAIR  // bits in pairs, XOR3 when both set: 7.2 ms against 6.2 (k128/m32 decode)\n#define LH_PB_PAIR 0\n#endif\n";
-    // LH_PB_FR: no per-bit branches.  Per used row, the 16-entry XOR tables of V_r's
-    // sub-rows 0..3 and 4..7 sit in registers; output sub-row y of B(c) V_r is
-    // tl[lo_y] ^ th[hi_y], where (lo_y, hi_y) are the nibbles of byte y of the bit-matrix
-    // of c (from lh_bmtab, read per lane once per output group, then v_readlane).  The
-    // wave-uniform table index becomes a VGPR-indexed move (s_set_gpr_idx_on / v_mov /
-    // off): 3 VALU + 4 SALU per output sub-row, 74 instructions per (output, row) against
-    // ~52 for the branches.  Measured slower: k128/m32 decode 5.89 against 5.57 ms,
-    // k200/m56 1.41 against 1.14 ms (profiles/r2_tune_pb_fr.txt).
-    os << "#ifndef LH_PB_FR\n#define LH_PB_FR 0\n#endif\n#if LH_PB_FR\n";
-    os << "__device__ const unsigned int lh_bmtab[512] = {";
-    for (int c = 0; c < 256; ++c) {
-        const uint64_t bm = bitmatrix((uint8_t)c);
-        os << (unsigned)(bm & 0xFFFFFFFFu) << "u," << (unsigned)(bm >> 32) << "u" << (c < 255 ? "," : "");
-    }
-    os << "};\n#endif\n";
+    // (Register tables per V row indexed at run time -- s_set_gpr_idx_on / v_mov / off,
+    // 74 instructions per (output, row) -- measured slower: k128/m32 decode 5.89 vs 5.57 ms,
+    // profiles/r2_tune_pb_fr.txt.)
     // The coefficients of the wave's 8 outputs for used row j sit packed in lane j
     // (cpk0: outputs 0..3, cpk1: 4..7) and come back as SGPRs through v_readlane, and the
     // next row's V is read from LDS while the current row is applied, so no LDS round
@@ -371,13 +359,6 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
        << "        cpk0 |= (i0 + i < e ? (unsigned int)cf[(i0 + i) * " << c.m << " + ur] : 0u) << (8 * i);\n"
        << "        cpk1 |= (i0 + 4 + i < e ? (unsigned int)cf[(i0 + 4 + i) * " << c.m << " + ur] : 0u) << (8 * i);\n"
        << "      }\n    }\n"
-       << "#if LH_PB_FR  // bit-matrices of the wave's 8 coefficients of used row `lane`\n"
-       << "    unsigned int bmv[8][2];\n"
-       << "#pragma unroll\n    for (int i = 0; i < 8; ++i) {\n"
-       << "      const unsigned int c = (i < 4 ? cpk0 >> (8 * i) : cpk1 >> (8 * (i - 4))) & 0xFFu;\n"
-       << "      bmv[i][0] = lh_bmtab[2 * c];\n      bmv[i][1] = lh_bmtab[2 * c + 1];\n"
-       << "    }\n"
-       << "#endif\n"
        << "    unsigned int acc[8][8];\n"
        << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n#pragma unroll\n      for (int y = 0; y < 8; ++y) acc[i][y] = 0;\n"
        << "    unsigned int v[8], vn[8];\n"
@@ -391,23 +372,7 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
        << "      }\n"
        << "      const unsigned int c0 = (unsigned int)__builtin_amdgcn_readlane((int)cpk0, j);\n"
        << "      const unsigned int c1 = (unsigned int)__builtin_amdgcn_readlane((int)cpk1, j);\n"
-       << "#if LH_PB_FR\n"
-       << "      unsigned int tl[16], th[16];\n"
-       << "      tl[0] = 0u;\n      th[0] = 0u;\n"
-       << "#pragma unroll\n      for (int n = 1; n < 16; ++n) {\n"
-       << "        const int low = __builtin_ctz(n), pre = n & (n - 1);\n"
-       << "        tl[n] = pre ? (tl[pre] ^ v[low]) : v[low];\n"
-       << "        th[n] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];\n"
-       << "      }\n"
-       << "#pragma unroll\n      for (int i = 0; i < 8; ++i) {\n"
-       << "        if (i0 + i >= e) continue;\n"
-       << "        const unsigned int b0 = (unsigned int)__builtin_amdgcn_readlane((int)bmv[i][0], j);\n"
-       << "        const unsigned int b1 = (unsigned int)__builtin_amdgcn_readlane((int)bmv[i][1], j);\n"
-       << "#pragma unroll\n        for (int y = 0; y < 8; ++y) {\n"
-       << "          const unsigned int s = ((y < 4 ? b0 : b1) >> (8 * (y & 3))) & 0xFFu;\n"
-       << "          acc[i][y] = __builtin_amdgcn_bitop3_b32(acc[i][y], tl[s & 15u], th[s >> 4], 0x96);\n"
-       << "        }\n      }\n"
-       << "#elif LH_PB_PAIR  // bits (2q, 2q + 1) of a coefficient together: both set -> one XOR3\n"
+       << "#if LH_PB_PAIR  // bits (2q, 2q + 1) of a coefficient together: both set -> one XOR3\n"
        << "#pragma unroll\n      for (int q = 0; q < 4; ++q) {\n"
        << "        unsigned int w[8];  // w = B(2) v: the ladder entry of bit 2q + 1\n"
        << "        {\n          const unsigned int t7 = __builtin_amdgcn_bitop3_b32(v[0], v[1], v[2], 0x96) ^ v[7];\n"
