@@ -224,6 +224,14 @@ def batch_path(k, m, block_bytes, decode=False):
     return {0: "generic", 1: "jit", 2: "jit-fused", 3: "jit-win", 4: "jit-wide"}[code]
 
 
+def _phase_b_kernel(k, m):
+    """Phase-B kernel of the split large-m decode (kernels.hip launch_inverse)."""
+    if os.environ.get("LONGHAIR_AMD_WIN_SPLIT") == "0":
+        return []
+    jump = os.environ.get("LONGHAIR_AMD_INV_JUMP", "4")
+    return ["lh_inverse_jt_kernel" if jump != "0" and min(k, m) <= 32 else "lh_inverse_kernel"]
+
+
 def kernel_names(k, m, block_bytes):
     """Names of the kernels one encode_batch / decode_batch launches for this shape."""
     enc = {"generic": ["lh_apply_generic_kernel"], "jit": ["lh_jit_encode"],
@@ -231,8 +239,7 @@ def kernel_names(k, m, block_bytes):
     dec = {"generic": ["lh_plan_kernel", "lh_apply_generic_kernel", "lh_scatter_kernel"],
            "jit": ["lh_plan_small_kernel" if min(k, m) <= 8 else "lh_plan_kernel", "lh_jit_decode"],
            "jit-fused": ["lh_jit_decode_fused"],
-           "jit-wide": ["lh_plan_kernel", "lh_jit_decode_wide"]
-           + ([] if os.environ.get("LONGHAIR_AMD_WIN_SPLIT") == "0" else ["lh_inverse_kernel"]),
+           "jit-wide": ["lh_plan_kernel", "lh_jit_decode_wide"] + _phase_b_kernel(k, m),
            }[batch_path(k, m, block_bytes, True)]
     if m == 1 or k == 1:
         enc, dec = ["lh_xor_reduce_kernel"], ["lh_plan_kernel", "lh_xor_reduce_kernel"]

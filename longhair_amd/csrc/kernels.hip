@@ -679,6 +679,106 @@ __device__ __forceinline__ void lh_inv_rows(uint32_t (&acc)[OPW][8], const uint8
     }
 }
 
+// ---- phase B by a computed jump on the coefficient value (LONGHAIR_AMD_INV_JUMP=1,
+// e_max <= 32).  The V rows of the chunk are staged in LDS once per workgroup (e x 2 KiB;
+// after that barrier the recovery slots may be overwritten).  Per used row a wave builds
+// the 16-entry XOR tables of V_r's sub-blocks 0..3 (tl) and 4..7 (th) in registers; a
+// multiply by c is then, for every output sub-row y, one XOR3 of two table entries whose
+// indices are the nibbles of c * 2^y.  Those are compile-time constants of 256 fixed-size
+// bodies (8 v_bitop3 + s_branch = 68 bytes, inv_jump.inc, tools/gen_inv_jump.py); the
+// wave jumps to body c with s_setpc_b64 (c is wave-uniform): 8 VALU per (output, row)
+// against the Horner form's 8 bit branches and ~32 XORs.  Two outputs per wave: the two
+// jump tables (35 KiB) stay within the instruction cache.
+#include "inv_jump.inc"
+
+__device__ __forceinline__ void lh_mul_jump(unsigned c, uint32_t (&a)[8], const uint32_t (&tl)[16],
+                                            const uint32_t (&th)[16]) {
+    asm volatile(LH_INV_JUMP_ASM
+                 : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7])
+                 : "s"(c), "v"(tl[0]), "v"(tl[1]), "v"(tl[2]), "v"(tl[3]), "v"(tl[4]), "v"(tl[5]), "v"(tl[6]),
+                   "v"(tl[7]), "v"(tl[8]), "v"(tl[9]), "v"(tl[10]), "v"(tl[11]), "v"(tl[12]), "v"(tl[13]),
+                   "v"(tl[14]), "v"(tl[15]), "v"(th[0]), "v"(th[1]), "v"(th[2]), "v"(th[3]), "v"(th[4]),
+                   "v"(th[5]), "v"(th[6]), "v"(th[7]), "v"(th[8]), "v"(th[9]), "v"(th[10]), "v"(th[11]),
+                   "v"(th[12]), "v"(th[13]), "v"(th[14]), "v"(th[15])
+                 : "s96", "s97", "s98", "scc");
+}
+
+template <int JO>
+__global__ void __launch_bounds__(1024) lh_inverse_jt_kernel(lh::InverseArgs a) {
+    static_assert(JO >= 1 && JO <= 4, "one coefficient byte per output in a 32-bit word");
+    __shared__ uint32_t lv[32 * 8 * 64];  // V rows of the chunk, [used row][sub-block][lane]
+    const int nw = (int)(blockDim.x >> 6);
+    const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = (int)(threadIdx.x & 63);
+    const int cps = a.bytes >> 11;
+    const long long stripe = blockIdx.x / cps;
+    if (stripe >= a.stripes) return;  // workgroup-uniform
+    const uint8_t *pl = a.plan + stripe * a.plan_stride;
+    const int e = pl[0];
+    if (e == 0) return;  // workgroup-uniform
+    const int m = a.m, sub = a.bytes >> 3;
+    const lh::PlanView pv(pl, a.k, m, a.e_max);
+    const uint32_t rslot = lane < m ? (uint32_t)pv.rec_slot(lane) : 0xFFu;
+    const unsigned long long used = __ballot(rslot != 0xFFu);
+    uint8_t *base = a.blocks + stripe * a.stride + (int)(blockIdx.x % cps) * 256 + lane * 4;
+    {  // stage: wave g copies used rows g, g + nw, ... (j-th set bit of `used`) into lv[j]
+        unsigned long long rest = used;
+        for (int j = 0; rest; ++j, rest &= rest - 1) {
+            if (j % nw != g) continue;
+            const int r = __builtin_ctzll(rest);
+            const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)rslot, r);
+            const uint8_t *p = base + (long long)slot * a.bytes;
+            uint32_t v[8];
+#pragma unroll
+            for (int y = 0; y < 8; ++y) v[y] = *(const uint32_t *)(p + (long long)y * sub);
+#pragma unroll
+            for (int y = 0; y < 8; ++y) lv[(j * 8 + y) * 64 + lane] = v[y];
+        }
+    }
+    __syncthreads();  // every V row is in LDS: the recovery slots may now be overwritten
+    const int nout = g < e ? (e - g + nw - 1) / nw : 0;  // outputs g, g + nw, ... (<= JO)
+    if (nout == 0) return;
+    uint32_t cpk = 0;  // lane r: this wave's coefficients for recovery row r
+    if (rslot != 0xFFu) {
+        const uint8_t *cf = pv.coef_ptr();
+#pragma unroll
+        for (int i = 0; i < JO; ++i)
+            if (i < nout) cpk |= (uint32_t)cf[(g + i * nw) * m + lane] << (8 * i);
+    }
+    uint32_t acc[JO][8];
+#pragma unroll
+    for (int i = 0; i < JO; ++i)
+#pragma unroll
+        for (int y = 0; y < 8; ++y) acc[i][y] = 0;
+    unsigned long long rest = used;
+    for (int j = 0; rest; ++j, rest &= rest - 1) {
+        const int r = __builtin_ctzll(rest);
+        uint32_t v[8];
+#pragma unroll
+        for (int y = 0; y < 8; ++y) v[y] = lv[(j * 8 + y) * 64 + lane];
+        uint32_t tl[16], th[16];
+        tl[0] = th[0] = 0;
+#pragma unroll
+        for (int q = 1; q < 16; ++q) {
+            const int low = __builtin_ctz(q), pre = q & (q - 1);
+            tl[q] = pre ? (tl[pre] ^ v[low]) : v[low];
+            th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];
+        }
+        const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane((int)cpk, r);
+#pragma unroll
+        for (int i = 0; i < JO; ++i)
+            if (i < nout) lh_mul_jump((cw >> (8 * i)) & 0xFFu, acc[i], tl, th);
+    }
+#pragma unroll
+    for (int i = 0; i < JO; ++i) {
+        if (i < nout) {
+            uint8_t *dst = base + (long long)pv.out_slot(g + i * nw) * a.bytes;
+#pragma unroll
+            for (int y = 0; y < 8; ++y) __builtin_nontemporal_store(acc[i][y], (uint32_t *)(dst + (long long)y * sub));
+        }
+    }
+}
+
 // OPW: outputs per wave (8, or 4: twice the waves, half the accumulators).
 template <int OPW>
 __global__ void __launch_bounds__(1024) lh_inverse_kernel(lh::InverseArgs a) {
@@ -784,6 +884,20 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     // coefficient bits are set, 25 % fewer XORs behind nested branches: 5.90 against 4.12 ms.)
     const char *o = std::getenv("LONGHAIR_AMD_INV_OPW");
     const int opw = (o && std::atoi(o) == 8) ? 8 : 4;
+    // e_max <= 32: the computed-jump kernel with 4 outputs per wave (default;
+    // LONGHAIR_AMD_INV_JUMP=0 selects the Horner kernel, =2 two outputs per wave).
+    // k128/m32 decode 4.14 -> 3.94 ms (profiles/r2_tune_split_decode.txt).
+    const char *jpe = std::getenv("LONGHAIR_AMD_INV_JUMP");
+    const int jp = jpe ? std::atoi(jpe) : 4;
+    if (jp != 0 && a.e_max <= 32) {
+        if (jp == 4)
+            hipLaunchKernelGGL(lh_inverse_jt_kernel<4>, dim3((unsigned)blocks),
+                               dim3(64u * (unsigned)((a.e_max + 3) / 4)), 0, st, a);
+        else
+            hipLaunchKernelGGL(lh_inverse_jt_kernel<2>, dim3((unsigned)blocks),
+                               dim3(64u * (unsigned)((a.e_max + 1) / 2)), 0, st, a);
+        return hipGetLastError();
+    }
     const unsigned threads = 64u * (unsigned)((a.e_max + opw - 1) / opw);
     if (threads > 1024) return hipErrorInvalidValue;
     const dim3 grid((unsigned)blocks), block(threads);
