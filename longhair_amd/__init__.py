@@ -229,7 +229,8 @@ def _phase_b_kernel(k, m):
     if os.environ.get("LONGHAIR_AMD_WIN_SPLIT") == "0":
         return []
     jump = os.environ.get("LONGHAIR_AMD_INV_JUMP", "4")
-    return ["lh_inverse_jt_kernel" if jump != "0" and min(k, m) <= 32 else "lh_inverse_kernel"]
+    horner = jump == "0" or (jump == "2" and min(k, m) > 32)
+    return ["lh_inverse_kernel" if horner else "lh_inverse_jt_kernel"]
 
 
 def kernel_names(k, m, block_bytes):

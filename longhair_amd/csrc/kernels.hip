@@ -703,10 +703,10 @@ __device__ __forceinline__ void lh_mul_jump(unsigned c, uint32_t (&a)[8], const 
                  : "s96", "s97", "s98", "scc");
 }
 
-template <int JO>
+template <int JO, int MAXE>
 __global__ void __launch_bounds__(1024) lh_inverse_jt_kernel(lh::InverseArgs a) {
     static_assert(JO >= 1 && JO <= 4, "one coefficient byte per output in a 32-bit word");
-    __shared__ uint32_t lv[32 * 8 * 64];  // V rows of the chunk, [used row][sub-block][lane]
+    __shared__ uint32_t lv[MAXE * 8 * 64];  // V rows of the chunk, [used row][sub-block][lane]
     const int nw = (int)(blockDim.x >> 6);
     const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = (int)(threadIdx.x & 63);
@@ -884,19 +884,21 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     // coefficient bits are set, 25 % fewer XORs behind nested branches: 5.90 against 4.12 ms.)
     const char *o = std::getenv("LONGHAIR_AMD_INV_OPW");
     const int opw = (o && std::atoi(o) == 8) ? 8 : 4;
-    // e_max <= 32: the computed-jump kernel with 4 outputs per wave (default;
-    // LONGHAIR_AMD_INV_JUMP=0 selects the Horner kernel, =2 two outputs per wave).
-    // k128/m32 decode 4.14 -> 3.94 ms (profiles/r2_tune_split_decode.txt).
+    // The computed-jump kernel with 4 outputs per wave (default; its V tile is 64 KiB for
+    // e_max <= 32, else 128 KiB; LONGHAIR_AMD_INV_JUMP=0 selects the Horner kernel, =2 two
+    // outputs per wave for e_max <= 32).  k128/m32 decode 4.15 -> 3.98 ms
+    // (profiles/r2_tune_split_decode.txt).
+    bool jt_done = true;
     const char *jpe = std::getenv("LONGHAIR_AMD_INV_JUMP");
     const int jp = jpe ? std::atoi(jpe) : 4;
-    if (jp != 0 && a.e_max <= 32) {
-        if (jp == 4)
-            hipLaunchKernelGGL(lh_inverse_jt_kernel<4>, dim3((unsigned)blocks),
-                               dim3(64u * (unsigned)((a.e_max + 3) / 4)), 0, st, a);
-        else
-            hipLaunchKernelGGL(lh_inverse_jt_kernel<2>, dim3((unsigned)blocks),
-                               dim3(64u * (unsigned)((a.e_max + 1) / 2)), 0, st, a);
-        return hipGetLastError();
+    if (jp != 0) {
+        const unsigned jt = 64u * (unsigned)((a.e_max + (jp == 2 ? 1 : 3)) / (jp == 2 ? 2 : 4));
+        const dim3 grid((unsigned)blocks);
+        if (jp == 2 && a.e_max <= 32) hipLaunchKernelGGL((lh_inverse_jt_kernel<2, 32>), grid, dim3(jt), 0, st, a);
+        else if (a.e_max <= 32) hipLaunchKernelGGL((lh_inverse_jt_kernel<4, 32>), grid, dim3(jt), 0, st, a);
+        else if (jp != 2) hipLaunchKernelGGL((lh_inverse_jt_kernel<4, 64>), grid, dim3(jt), 0, st, a);
+        else jt_done = false;
+        if (jt_done) return hipGetLastError();
     }
     const unsigned threads = 64u * (unsigned)((a.e_max + opw - 1) / opw);
     if (threads > 1024) return hipErrorInvalidValue;
