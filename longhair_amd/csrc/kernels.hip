@@ -13,6 +13,12 @@
 //   lh_xor_reduce_kernel    out = XOR of n inputs for any block size (m == 1 encode
 //                           :1511-1522, k <= 1 copies :1501-1509, m == 1 decode :487-535).
 //   lh_scatter_kernel       moves recovered blocks from the workspace into their slots.
+//   lh_inverse_jt_kernel    large-m decode phase B (after the windowed phase A left V_r in
+//                           the recovery slots): D_E = A^-1 V by a computed jump into 256
+//                           fixed multiply-by-c bodies (default); lh_inverse_kernel is the
+//                           Horner form (back-substitution :1083-1247, same solution).
+//   lh_writeback_kernel     pinned-host decode pipeline: recovered blocks straight into
+//                           the caller's pinned buffer.
 //
 // Lanes own W-byte columns of a stripe's sub-blocks: a lane loads the same byte range of
 // all 8 sub-blocks of a block and produces the same range of all 8 output sub-blocks, so
