@@ -709,10 +709,14 @@ __device__ __forceinline__ void lh_mul_jump(unsigned c, uint32_t (&a)[8], const 
                  : "s96", "s97", "s98", "scc");
 }
 
-template <int JO, int MAXE>
+// BLK > 0: the V rows are staged BLK at a time (a BLK x 2 KiB tile, more workgroups per
+// CU; a barrier after each block's compute before the next staging, and the outputs are
+// stored once every row has been staged).  BLK == 0: all rows at once (MAXE x 2 KiB).
+template <int JO, int MAXE, int BLK>
 __global__ void __launch_bounds__(1024) lh_inverse_jt_kernel(lh::InverseArgs a) {
     static_assert(JO >= 1 && JO <= 4, "one coefficient byte per output in a 32-bit word");
-    __shared__ uint32_t lv[MAXE * 8 * 64];  // V rows of the chunk, [used row][sub-block][lane]
+    constexpr int TILE = BLK > 0 ? BLK : MAXE;
+    __shared__ uint32_t lv[TILE * 8 * 64];  // V rows, [row in tile][sub-block][lane]
     const int nw = (int)(blockDim.x >> 6);
     const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = (int)(threadIdx.x & 63);
@@ -727,23 +731,7 @@ __global__ void __launch_bounds__(1024) lh_inverse_jt_kernel(lh::InverseArgs a) 
     const uint32_t rslot = lane < m ? (uint32_t)pv.rec_slot(lane) : 0xFFu;
     const unsigned long long used = __ballot(rslot != 0xFFu);
     uint8_t *base = a.blocks + stripe * a.stride + (int)(blockIdx.x % cps) * 256 + lane * 4;
-    {  // stage: wave g copies used rows g, g + nw, ... (j-th set bit of `used`) into lv[j]
-        unsigned long long rest = used;
-        for (int j = 0; rest; ++j, rest &= rest - 1) {
-            if (j % nw != g) continue;
-            const int r = __builtin_ctzll(rest);
-            const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)rslot, r);
-            const uint8_t *p = base + (long long)slot * a.bytes;
-            uint32_t v[8];
-#pragma unroll
-            for (int y = 0; y < 8; ++y) v[y] = *(const uint32_t *)(p + (long long)y * sub);
-#pragma unroll
-            for (int y = 0; y < 8; ++y) lv[(j * 8 + y) * 64 + lane] = v[y];
-        }
-    }
-    __syncthreads();  // every V row is in LDS: the recovery slots may now be overwritten
     const int nout = g < e ? (e - g + nw - 1) / nw : 0;  // outputs g, g + nw, ... (<= JO)
-    if (nout == 0) return;
     uint32_t cpk = 0;  // lane r: this wave's coefficients for recovery row r
     if (rslot != 0xFFu) {
         const uint8_t *cf = pv.coef_ptr();
@@ -756,25 +744,46 @@ __global__ void __launch_bounds__(1024) lh_inverse_jt_kernel(lh::InverseArgs a) 
     for (int i = 0; i < JO; ++i)
 #pragma unroll
         for (int y = 0; y < 8; ++y) acc[i][y] = 0;
-    unsigned long long rest = used;
-    for (int j = 0; rest; ++j, rest &= rest - 1) {
-        const int r = __builtin_ctzll(rest);
-        uint32_t v[8];
+    unsigned long long todo = used;  // rows not yet staged
+    while (todo) {  // workgroup-uniform
+        {  // stage the next TILE used rows: wave g copies tile rows g, g + nw, ...
+            unsigned long long rest = todo;
+            for (int j = 0; rest && j < TILE; ++j, rest &= rest - 1) {
+                if (j % nw != g) continue;
+                const int r = __builtin_ctzll(rest);
+                const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)rslot, r);
+                const uint8_t *p = base + (long long)slot * a.bytes;
+                uint32_t v[8];
 #pragma unroll
-        for (int y = 0; y < 8; ++y) v[y] = lv[(j * 8 + y) * 64 + lane];
-        uint32_t tl[16], th[16];
-        tl[0] = th[0] = 0;
+                for (int y = 0; y < 8; ++y) v[y] = *(const uint32_t *)(p + (long long)y * sub);
 #pragma unroll
-        for (int q = 1; q < 16; ++q) {
-            const int low = __builtin_ctz(q), pre = q & (q - 1);
-            tl[q] = pre ? (tl[pre] ^ v[low]) : v[low];
-            th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];
+                for (int y = 0; y < 8; ++y) lv[(j * 8 + y) * 64 + lane] = v[y];
+            }
         }
-        const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane((int)cpk, r);
+        __syncthreads();  // this tile is in LDS
+        for (int j = 0; todo && j < TILE; ++j, todo &= todo - 1) {
+            if (nout == 0) continue;
+            const int r = __builtin_ctzll(todo);
+            uint32_t v[8];
 #pragma unroll
-        for (int i = 0; i < JO; ++i)
-            if (i < nout) lh_mul_jump((cw >> (8 * i)) & 0xFFu, acc[i], tl, th);
+            for (int y = 0; y < 8; ++y) v[y] = lv[(j * 8 + y) * 64 + lane];
+            uint32_t tl[16], th[16];
+            tl[0] = th[0] = 0;
+#pragma unroll
+            for (int q = 1; q < 16; ++q) {
+                const int low = __builtin_ctz(q), pre = q & (q - 1);
+                tl[q] = pre ? (tl[pre] ^ v[low]) : v[low];
+                th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];
+            }
+            const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane((int)cpk, r);
+#pragma unroll
+            for (int i = 0; i < JO; ++i)
+                if (i < nout) lh_mul_jump((cw >> (8 * i)) & 0xFFu, acc[i], tl, th);
+        }
+        if (todo) __syncthreads();  // the tile is consumed before the next staging
     }
+    // Every row was staged (read) before the last tile's barrier: the recovery slots may be
+    // overwritten.
 #pragma unroll
     for (int i = 0; i < JO; ++i) {
         if (i < nout) {
@@ -890,19 +899,22 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     // coefficient bits are set, 25 % fewer XORs behind nested branches: 5.90 against 4.12 ms.)
     const char *o = std::getenv("LONGHAIR_AMD_INV_OPW");
     const int opw = (o && std::atoi(o) == 8) ? 8 : 4;
-    // The computed-jump kernel with 4 outputs per wave (default; its V tile is 64 KiB for
-    // e_max <= 32, else 128 KiB; LONGHAIR_AMD_INV_JUMP=0 selects the Horner kernel, =2 two
-    // outputs per wave for e_max <= 32).  k128/m32 decode 4.15 -> 3.98 ms
-    // (profiles/r2_tune_split_decode.txt).
+    // The computed-jump kernel with 4 outputs per wave (default): for e_max <= 32 the V rows
+    // are staged 16 at a time (32 KiB tile; k128/m32 decode 4.10 -> 3.84 ms against all 32
+    // at once), above that all at once (128 KiB; 16-row staging measured 2 % slower for
+    // k200/m56).  LONGHAIR_AMD_INV_JUMP=0: the Horner kernel; =2: two outputs per wave
+    // (e_max <= 32); =40: e_max <= 32 staged at once (profiles/r2_tune_split_decode.txt).
     bool jt_done = true;
     const char *jpe = std::getenv("LONGHAIR_AMD_INV_JUMP");
     const int jp = jpe ? std::atoi(jpe) : 4;
     if (jp != 0) {
         const unsigned jt = 64u * (unsigned)((a.e_max + (jp == 2 ? 1 : 3)) / (jp == 2 ? 2 : 4));
         const dim3 grid((unsigned)blocks);
-        if (jp == 2 && a.e_max <= 32) hipLaunchKernelGGL((lh_inverse_jt_kernel<2, 32>), grid, dim3(jt), 0, st, a);
-        else if (a.e_max <= 32) hipLaunchKernelGGL((lh_inverse_jt_kernel<4, 32>), grid, dim3(jt), 0, st, a);
-        else if (jp != 2) hipLaunchKernelGGL((lh_inverse_jt_kernel<4, 64>), grid, dim3(jt), 0, st, a);
+        if (jp == 2 && a.e_max <= 32) hipLaunchKernelGGL((lh_inverse_jt_kernel<2, 32, 0>), grid, dim3(jt), 0, st, a);
+        else if (jp == 40 && a.e_max <= 32)  // (A/B) all rows staged at once
+            hipLaunchKernelGGL((lh_inverse_jt_kernel<4, 32, 0>), grid, dim3(jt), 0, st, a);
+        else if (a.e_max <= 32) hipLaunchKernelGGL((lh_inverse_jt_kernel<4, 32, 16>), grid, dim3(jt), 0, st, a);
+        else if (jp != 2) hipLaunchKernelGGL((lh_inverse_jt_kernel<4, 64, 0>), grid, dim3(jt), 0, st, a);
         else jt_done = false;
         if (jt_done) return hipGetLastError();
     }
