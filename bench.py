@@ -18,8 +18,15 @@ per GPU.  Multi-GPU (one process per GPU, no collective on the data path):
 With --gpus N > 1 and no torchrun environment, this process starts
 `torch.distributed.run --nproc-per-node N` on itself before touching any GPU and exits
 with its code; under torchrun (WORLD_SIZE set) it must see WORLD_SIZE == N.
-`--dry-run` replaces the HIP work with a CPU stand-in over the gloo backend (tests the
-launcher and the aggregation on a machine without a GPU).
+The process group is always gloo: the codec needs no collective (stripes are independent),
+so the group only carries the barriers around the timed region and the per-rank timing
+reduction -- the same code path with or without a GPU.  `--dry-run` replaces the HIP work
+with a CPU stand-in (tests the launcher and the aggregation on a machine without a GPU).
+
+Legs besides the device-resident steps (rank 0 unless noted): the PCIe-inclusive rate from
+pinned host memory (every rank at once, `--pcie`, default on), the per-call latency of the
+drop-in entry points, and the reference CPU codec on the host cores (`cpu_baseline`) over
+the same erasure patterns as the GPU workload.
 
 Prints one JSON line (rank 0).  See DESIGN.md for the roofline and cpu_baseline definitions.
 """
@@ -50,6 +57,10 @@ HBM_CEILING_SRC = "profiles/r2_ubench_ceiling.txt (dwordx4 non-temporal stream r
 VALU_PEAK_GINSTR = 256 * 4 * 2.4e9 / 2 / 1e9
 # Measured v_bitop3_b32 issue rate at 8 waves/SIMD (profiles/r2_ubench_ceiling.txt).
 VALU_CEILING_GINSTR = 761.5
+# k29/m4 x 65536: the encode's 2.46 GB read + 0.34 GB written as flat, fully coalesced
+# 16-byte-lane streams (trivial compute, best of 6 grid / unroll settings).
+FLAT_FLOOR_MS = 0.538
+FLAT_FLOOR_SRC = "profiles/r2_ubench_pattern_floor.txt (tools/ubench_pattern.hip, flat read+write)"
 
 
 def parse(argv=None):
@@ -65,6 +76,10 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="wall-time budget of the CPU baseline leg")
     ap.add_argument("--dropin-calls", type=int, default=-1,
                     help="per-call drop-in latency leg (host pointers, one stripe per call); 0 = off")
+    ap.add_argument("--pcie", default="on", choices=["on", "off"],
+                    help="PCIe-inclusive leg: cauchy_256_*_host_batch from pinned host memory on every rank")
+    ap.add_argument("--pcie-stripes", type=int, default=0,
+                    help="stripes per rank in the PCIe leg (default: the workload, capped at ~640 MB)")
     ap.add_argument("--dry-run", action="store_true", help="no HIP work: CPU stand-in step over gloo")
     return ap.parse_args(argv)
 
@@ -88,6 +103,8 @@ def launch(args):
 
 
 def setup_dist(dry):
+    """One process per GPU.  The group is gloo in every run: no data-path collective exists
+    (SURVEY 8e), so it carries only host-side barriers and the timing reduction."""
     import torch
     import torch.distributed as dist
     from longhair_amd.shard import world_info
@@ -95,32 +112,32 @@ def setup_dist(dry):
     if not dry:
         torch.cuda.set_device(local)
     if world > 1:
-        if dry:
-            dist.init_process_group(backend="gloo")
-        else:
-            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group(backend="gloo")
     return world, rank, local
 
 
 def barrier(world, dry):
+    """Device idle on every rank, then all ranks meet, then the device again."""
     import torch
     import torch.distributed as dist
+    if not dry:
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     if not dry:
         torch.cuda.synchronize()
 
 
-def per_rank(world, rank, value, dry):
-    """Every rank's `value`, in rank order (one all-reduce of a one-hot vector)."""
+def per_rank(world, rank, value, dry=False):
+    """Every rank's `value`, in rank order (one gloo all-reduce of a one-hot CPU vector)."""
     if world == 1:
         return [float(value)]
     import torch
     import torch.distributed as dist
-    t = torch.zeros(world, dtype=torch.float64, device="cpu" if dry else "cuda")
+    t = torch.zeros(world, dtype=torch.float64)
     t[rank] = float(value)
     dist.all_reduce(t)
-    return [float(v) for v in t.cpu().tolist()]
+    return [float(v) for v in t.tolist()]
 
 
 # ------------------------------------------------------------------------ workload
@@ -241,36 +258,65 @@ def dropin_blocks(k, m, nbytes, data, erased_rows=None):
     return make
 
 
-def cpu_baseline(k, m, nbytes, budget_s, stripes):
+def erasure_patterns(rows, k):
+    """From Block.row bytes [n, k] of decode slots: (erased originals [n, e_max], erasures
+    per stripe [n], recovery rows used [n, e_max]) for lhb_run_pattern."""
+    import numpy as np
+    n = rows.shape[0]
+    e_of = (rows >= k).sum(axis=1).astype(np.uint8)
+    e_max = max(1, int(e_of.max()))
+    erased = np.zeros((n, e_max), dtype=np.uint8)
+    rec = np.zeros((n, e_max), dtype=np.uint8)
+    for s in range(n):
+        miss = np.setdiff1d(np.arange(k), rows[s][rows[s] < k])[: e_of[s]]
+        erased[s, : len(miss)] = miss
+        rr = np.sort(rows[s][rows[s] >= k]) - k
+        rec[s, : len(rr)] = rr
+    return erased, e_of, rec, e_max
+
+
+def cpu_baseline(k, m, nbytes, budget_s, stripes, patterns=None):
     """Reference codec (oracle/_ref, compiled from the reference sources) -- or, if that
     build is absent, the oracle restatement -- on the host cores, same step definition,
     a bounded sample of stripes: all granted cores, then one thread; plus the per-call
-    latency of one-stripe encode / decode (the reference API shape)."""
+    latency of one-stripe encode / decode (the reference API shape).  `patterns`: the
+    Block.row bytes of the GPU workload's first decode stripes, so the reference decodes
+    the same erasure counts and recovery rows as the line it is reported beside."""
     import numpy as np
     import lhutil
     bench_so = os.path.join(REPO, "oracle", "liblh_cpubench.so")
     if not os.path.exists(bench_so):
         return None
     hb = ctypes.CDLL(bench_so)
-    hb.lhb_run.restype = ctypes.c_double
+    hb.lhb_run_pattern.restype = ctypes.c_double
     if os.path.exists(lhutil.REF_SO):
         lib, kind = lhutil.RefLib(), "reference"
         enc, dec = lib.lib.cauchy_256_encode, lib.lib.cauchy_256_decode
     else:
         lib, kind = lhutil.Oracle(), "port"
         enc, dec = lib.lib.lho_encode, lib.lib.lho_decode
-    e = min(k, m)
     data = lhutil.fill(99, stripes * k * nbytes)
-    rng = np.random.Generator(np.random.PCG64(5))
-    erased = np.stack([rng.choice(k, size=e, replace=False) for _ in range(stripes)]).astype(np.uint8)
+    if patterns is None:
+        e = min(k, m)
+        rng = np.random.Generator(np.random.PCG64(5))
+        erased = np.stack([rng.choice(k, size=e, replace=False) for _ in range(stripes)]).astype(np.uint8)
+        e_of = np.full(stripes, e, dtype=np.uint8)
+        rec_rows = np.tile(np.arange(e, dtype=np.uint8), (stripes, 1))
+    else:
+        idx = np.arange(stripes) % patterns.shape[0]
+        erased, e_of, rec_rows, e = erasure_patterns(np.ascontiguousarray(patterns[idx]), k)
+    erased, e_of, rec_rows = (np.ascontiguousarray(a) for a in (erased, e_of, rec_rows))
+    e_mean = float(e_of.mean())
     threads, aff, quota = effective_cpus()
     ok = ctypes.c_int(0)
     cpu_s = ctypes.c_double(0.0)
+    vp = ctypes.c_void_p
 
     def run(nstripes, nthreads, passes):
-        t = hb.lhb_run(ctypes.cast(enc, ctypes.c_void_p), ctypes.cast(dec, ctypes.c_void_p), k, m, nbytes,
-                       nstripes, data.ctypes.data_as(ctypes.c_void_p), erased.ctypes.data_as(ctypes.c_void_p), e,
-                       nthreads, passes, ctypes.byref(ok), ctypes.byref(cpu_s))
+        t = hb.lhb_run_pattern(ctypes.cast(enc, vp), ctypes.cast(dec, vp), k, m, nbytes, nstripes,
+                               data.ctypes.data_as(vp), erased.ctypes.data_as(vp), e_of.ctypes.data_as(vp),
+                               rec_rows.ctypes.data_as(vp), e, nthreads, passes, ctypes.byref(ok),
+                               ctypes.byref(cpu_s))
         return t, cpu_s.value, bool(ok.value)
 
     t1, _, good = run(stripes, threads, 1)  # warm-up + correctness pass
@@ -285,7 +331,9 @@ def cpu_baseline(k, m, nbytes, budget_s, stripes):
     tb, cs1, good1 = run(s1, 1, p1)
     gbs1 = 2.0 * k * nbytes * s1 * p1 / tb / 1e9
     out = {"value": round(gbs, 3), "unit": "GB/s", "cores": threads, "kind": kind,
-           "sample": f"{stripes} stripes x {passes} passes of encode+decode (e={e}), {threads} threads: "
+           "sample": f"{stripes} stripes x {passes} passes of encode+decode "
+                     f"({'the GPU workload' + chr(39) + 's erasure patterns, ' if patterns is not None else ''}"
+                     f"mean e {e_mean:.1f}), {threads} threads: "
                      f"{t:.1f} s wall, {cs:.1f} s CPU measured; 1 thread: {s1} stripes x {p1} passes, "
                      f"{tb:.1f} s wall",
            "value_1thread": round(gbs1, 3), "cpu_seconds": round(cs, 2), "wall_seconds": round(t, 2),
@@ -306,14 +354,15 @@ def dropin_leg(lh, k, m, nbytes, calls):
     import lhutil
     lib = lh.lib()
     d0 = lhutil.fill(7, k * nbytes)
-    prev = lh.set_dispatch("gpu")
+    # top level: the library's default policy, i.e. what an unchanged reference caller gets
     out = per_call_us(lib.cauchy_256_encode, lib.cauchy_256_decode, k, m, nbytes, calls, d0,
                       dropin_blocks(k, m, nbytes, d0))
-    # the same calls under the AUTO dispatch policy (include/cauchy_256_dispatch.h)
-    lh.set_dispatch("auto")
-    out["auto"] = per_call_us(lib.cauchy_256_encode, lib.cauchy_256_decode, k, m, nbytes, calls, d0,
-                              dropin_blocks(k, m, nbytes, d0))
-    out["auto"]["host_isa"] = lh.host_isa()
+    out["policy"] = lh.dispatch_policy()
+    out["host_isa"] = lh.host_isa()
+    # the same calls forced onto the GPU (include/cauchy_256_dispatch.h)
+    prev = lh.set_dispatch("gpu")
+    out["gpu"] = per_call_us(lib.cauchy_256_encode, lib.cauchy_256_decode, k, m, nbytes, calls, d0,
+                             dropin_blocks(k, m, nbytes, d0))
     lh.set_dispatch(prev)
     # the recovered blocks of the last decoded array must equal the erased originals
     ref = lhutil.fill(7, k * nbytes).reshape(k, nbytes)
@@ -333,8 +382,62 @@ def dropin_leg(lh, k, m, nbytes, calls):
     for _ in range(calls):
         noop()
     out["ctypes_overhead_us"] = round((time.perf_counter() - t0) / calls * 1e6, 2)
-    out["dispatch"] = "gpu (top level) / auto (out['auto'])"
+    out["dispatch"] = f"{out['policy']} (default, top level) / gpu (out['gpu'])"
     return out
+
+
+def pcie_leg(lh, args, k, m, nbytes, X, D, rows0, rec_view, rec_index, world, rank, reps=3):
+    """PCIe-inclusive rate: the workload's first stripes copied to pinned host
+    memory, then cauchy_256_encode_host_batch and cauchy_256_decode_host_batch (H2D, kernels
+    and D2H pipelined over three streams), every rank at the same time.  Input GB/s per rank
+    and for the node (all ranks' input bytes / the slowest rank's time)."""
+    import numpy as np
+    import torch
+    n = args.pcie_stripes or min(X.shape[0], max(1, (640 << 20) // (k * nbytes)))
+    n = min(n, X.shape[0])
+    # decode input: the recovery blocks back in their slots (the timed steps decoded them)
+    lh.encode_batch(X, m, recovery=rec_view)
+    if rec_index is not None:
+        D.view(-1, nbytes).index_copy_(0, rec_index[0], rec_view.reshape(-1, nbytes).index_select(0, rec_index[1]))
+    torch.cuda.synchronize()
+    hx = X[:n].cpu().pin_memory()
+    hb0 = D[:n].cpu()
+    hb = hb0.clone().pin_memory()
+    hr0 = rows0[:n].cpu()
+    hr = hr0.clone().pin_memory()
+    hrec = torch.empty((n, m, nbytes), dtype=torch.uint8).pin_memory()
+    xn, bn, rn, recn = hx.numpy(), hb.numpy(), hr.numpy(), hrec.numpy()
+    lh.encode_host_batch(xn, m, recovery=recn)           # warm-up: buffers, streams
+    lh.decode_host_batch(bn, rn, m)
+    order = np.argsort(rn, axis=1)
+    ok = bool(np.array_equal(np.take_along_axis(bn, order[:, :, None], axis=1), xn))
+    te = td = 0.0
+    for _ in range(reps):
+        barrier(world, False)
+        t0 = time.perf_counter()
+        lh.encode_host_batch(xn, m, recovery=recn)
+        te += time.perf_counter() - t0
+        bn[:] = hb0.numpy()
+        rn[:] = hr0.numpy()
+        barrier(world, False)
+        t0 = time.perf_counter()
+        lh.decode_host_batch(bn, rn, m)
+        td += time.perf_counter() - t0
+    te, td = te / reps, td / reps
+    inb = float(k * nbytes * n)
+    enc_r = per_rank(world, rank, inb / te / 1e9)
+    dec_r = per_rank(world, rank, inb / td / 1e9)
+    te_max, td_max = max(per_rank(world, rank, te)), max(per_rank(world, rank, td))
+    ok_all = min(per_rank(world, rank, 1.0 if ok else 0.0)) == 1.0
+    return {"stripes_per_rank": n, "input_MB_per_rank": round(inb / 1e6, 1),
+            "encode_GBps_per_rank": [round(v, 2) for v in enc_r],
+            "decode_GBps_per_rank": [round(v, 2) for v in dec_r],
+            "node_encode_GBps": round(inb * world / te_max / 1e9, 2),
+            "node_decode_GBps": round(inb * world / td_max / 1e9, 2),
+            "ok": ok_all,
+            "what": "input GB/s incl. host-to-device and device-to-host copies: pinned host stripes, "
+                    "cauchy_256_{encode,decode}_host_batch, every rank at once, mean of "
+                    f"{reps} (decode: the workload's erasure patterns, recovered blocks written back)"}
 
 
 def load_profile(name):
@@ -387,11 +490,13 @@ def main():
             Dflat, Rflat = D.view(-1, nbytes), R.view(-1, nbytes)
         rows = rows0.clone()
         stream = torch.cuda.current_stream()  # every kernel below is launched on this stream
+        traces = {}
 
         def step(ev=None):
             if ev is not None:
                 ev[0].record(stream)
             lh.encode_batch(X, m, recovery=rec_view, stream=stream)
+            traces.setdefault("encode", lh.last_launch())
             if ev is not None:
                 ev[1].record(stream)
             if rec_index is not None:   # deliver the received recovery blocks to their slots
@@ -400,6 +505,7 @@ def main():
             if ev is not None:
                 ev[2].record(stream)
             lh.decode_batch(D, rows, m, stream=stream)
+            traces.setdefault("decode", lh.last_launch())
             if ev is not None:
                 ev[3].record(stream)
 
@@ -460,7 +566,9 @@ def main():
         dec_ms = sum(ev[2].elapsed_time(ev[3]) for ev in evs) / args.steps
         enc_alg = float(k + m) * nbytes * stripes           # read k, write m blocks per stripe
         dec_alg = (k + e_mean) * nbytes * stripes           # read k slots, write e blocks
-        enc_k, dec_k = lh.kernel_names(k, m, nbytes)
+        # the kernels the batch calls really launched (cauchy_256_last_launch)
+        enc_k, dec_k = traces.get("encode") or lh.kernel_names(k, m, nbytes)[0], \
+            traces.get("decode") or lh.kernel_names(k, m, nbytes)[1]
         roof = {
             "encode": {"kernel": "+".join(enc_k), "ms": round(enc_ms, 4),
                        "achieved": round(enc_alg / (enc_ms * 1e-3) / 1e9, 1)},
@@ -501,13 +609,28 @@ def main():
             out["north_star"] = {"kernel": "+".join(enc_k), "input_read_GBps": round(enc_in, 1),
                                  "frac_of_hbm_peak": round(enc_in / HBM_PEAK_GBS, 4), "target": 0.70,
                                  "frac_of_measured_read_ceiling": round(enc_in / HBM_CEILING_GBS, 4)}
-    if rank == 0 and world == 1 and not dry:
+            if stripes == CONFIGS[args.config][3]:
+                # the same bytes as flat, fully coalesced read + write streams (the best of
+                # 6 grid / unroll settings, trivial compute): the floor this layout allows
+                out["north_star"].update({
+                    "measured_floor_ms": FLAT_FLOOR_MS, "floor_source": FLAT_FLOOR_SRC,
+                    "frac_of_measured_floor": round(FLAT_FLOOR_MS / enc_ms, 4),
+                    "floor_frac_of_hbm_peak": round(k * nbytes * stripes / (FLAT_FLOOR_MS * 1e-3) / 1e9
+                                                    / HBM_PEAK_GBS, 4)})
+    if not dry and args.pcie == "on":
+        # every rank at once: the node's host links and memory are shared
+        out["pcie"] = pcie_leg(lh, args, k, m, nbytes, X, D, rows0, rec_view, rec_index, world, rank)
+    if rank == 0 and not dry:
         calls = args.dropin_calls if args.dropin_calls >= 0 else max(10, min(2000, int(4e7 / (k * nbytes))))
         if calls:
             out["dropin_per_call"] = dropin_leg(lh, k, m, nbytes, calls)
         if args.cpu_baseline != "off":
-            out["cpu_baseline"] = cpu_baseline(k, m, nbytes, args.cpu_seconds,
-                                               stripes=max(2, min(4096, (256 << 20) // (k * nbytes))))
+            n_cpu = min(stripes, max(64, (256 << 20) // (k * nbytes)), 4096)
+            out["cpu_baseline"] = cpu_baseline(k, m, nbytes, args.cpu_seconds, stripes=n_cpu,
+                                               patterns=rows0[:n_cpu].cpu().numpy())
+            if world > 1:
+                out["cpu_baseline"]["note"] = (f"rank 0's host, after the {world}-rank timed region "
+                                               "(the other ranks idle)")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -32,7 +32,8 @@ int cauchy_256_encode_batch(int k, int m, int block_bytes, int stripes,
 
 /* Decode every stripe in place (as cauchy_256_decode applied to the k slots of each
  * stripe in array order).  d_status, if not NULL, receives one signed byte per stripe:
- * 0 = ok, -1 = the stripe's rows are invalid (duplicate or >= k + m); such a stripe is
+ * 0 = ok, -1 = the stripe's rows are invalid (duplicate or >= k + m; m > 1 only: for
+ * m == 1 every row is accepted, as by the reference's cauchy_decode_m1); such a stripe is
  * left untouched.  Returns -1 (nothing done) when m > 1 and k + m > 256 or
  * block_bytes % 8 != 0. */
 int cauchy_256_decode_batch(int k, int m, int block_bytes, int stripes,
@@ -58,6 +59,18 @@ int cauchy_256_decode_host_batch(int k, int m, int block_bytes, int stripes,
  * `max_stripes` stripes of this shape ahead of time (e.g. before hipGraph capture or
  * a timed region).  Synchronous.  Returns 0 or an error code. */
 int cauchy_256_batch_prepare(int k, int m, int block_bytes, int max_stripes);
+
+/* As cauchy_256_batch_prepare, reserving the decode workspace of `stream` (workspaces are
+ * per stream).  A batch call made while its stream is being captured into a graph never
+ * allocates: if the stream's workspace (or the device's zero page or generator) would
+ * have to grow, the call returns -3 without enqueuing anything.  Prepare the capture
+ * stream first. */
+int cauchy_256_batch_prepare_stream(int k, int m, int block_bytes, int max_stripes, void *stream);
+
+/* Diagnostics: comma-separated names of the kernels the calling thread's last entry-point
+ * call (drop-in or batch) enqueued, each once, in launch order (empty when it ran none,
+ * e.g. on the host engine). */
+const char *cauchy_256_last_launch(void);
 
 /* Which kernel family serves this shape: 0 = generic coefficient-driven kernels,
  * 1 = run-time specialised (JIT) network, 2 (decode only) = specialised network with the

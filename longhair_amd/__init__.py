@@ -192,8 +192,8 @@ _POLICIES = {"gpu": 0, "auto": 1, "host": 2}
 
 
 def set_dispatch(policy, host_max_work=-1):
-    """Drop-in dispatch policy (include/cauchy_256_dispatch.h): 'gpu' (default), 'auto'
-    (small all-host-memory calls on the host SIMD engine) or 'host'.  Returns the
+    """Drop-in dispatch policy (include/cauchy_256_dispatch.h): 'auto' (default: small
+    all-host-memory calls on the host SIMD engine), 'gpu' or 'host'.  Returns the
     previous policy name.  The library needs a GPU under every policy."""
     prev = lib().cauchy_256_set_dispatch(_POLICIES[policy], host_max_work)
     if prev < 0:
@@ -210,11 +210,20 @@ def host_isa():
     return lib().cauchy_256_host_isa().decode()
 
 
-def prepare(k, m, block_bytes, max_stripes=0):
-    """Compile the specialised kernels / reserve workspace for a shape (synchronous)."""
-    rc = lib().cauchy_256_batch_prepare(k, m, block_bytes, max_stripes)
+def prepare(k, m, block_bytes, max_stripes=0, stream=None):
+    """Compile the specialised kernels / reserve workspace for a shape (synchronous).
+    Workspaces are per stream: prepare the stream a graph will be captured on."""
+    rc = lib().cauchy_256_batch_prepare_stream(k, m, block_bytes, max_stripes,
+                                               ctypes.c_void_p(_stream_handle(stream)))
     if rc != 0:
-        raise LonghairError(rc, "cauchy_256_batch_prepare")
+        raise LonghairError(rc, "cauchy_256_batch_prepare_stream")
+
+
+def last_launch():
+    """Kernels this thread's last entry-point call enqueued (cauchy_256_last_launch), in
+    launch order; [] when it ran on the host engine or launched nothing."""
+    s = lib().cauchy_256_last_launch().decode()
+    return s.split(",") if s else []
 
 
 def batch_path(k, m, block_bytes, decode=False):

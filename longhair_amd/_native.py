@@ -30,6 +30,9 @@ EXPORTS = {
                                                     ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_int]),
     "cauchy_256_batch_prepare": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "cauchy_256_batch_prepare_stream": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                       ctypes.c_void_p]),
+    "cauchy_256_last_launch": (ctypes.c_char_p, []),
     "cauchy_256_batch_path": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "cauchy_256_jit_precompile": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "cauchy_256_frame_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,

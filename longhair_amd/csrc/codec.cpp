@@ -28,11 +28,31 @@ namespace lh {
 enum { kOk = 0, kInvalid = -1, kNoDevice = -2, kHipError = -3 };
 
 thread_local std::string g_last_error;
+thread_local std::string g_last_launch;  // kernels enqueued by this thread's last call
 
 static int fail(int code, const std::string &msg) {
     g_last_error = msg;
     return code;
 }
+
+void note_launch(const char *kernel) {
+    const std::string k(kernel);
+    // each kernel once, in order of first launch (the host-batch pipeline repeats them per chunk)
+    size_t pos = 0;
+    while ((pos = g_last_launch.find(k, pos)) != std::string::npos) {
+        const size_t end = pos + k.size();
+        if ((pos == 0 || g_last_launch[pos - 1] == ',') && (end == g_last_launch.size() || g_last_launch[end] == ','))
+            return;
+        pos = end;
+    }
+    if (!g_last_launch.empty()) g_last_launch += ',';
+    g_last_launch += k;
+}
+
+// Starts a new launch trace for one entry-point call.
+struct LaunchTrace {
+    LaunchTrace() { g_last_launch.clear(); }
+};
 
 #define LH_HIP(expr)                                                                       \
     do {                                                                                   \
@@ -154,10 +174,31 @@ static int current_device(Device **out) {
     return kOk;
 }
 
-static int device_generator(Device *d, int k, int m, const uint8_t **out, const uint8_t **points = nullptr) {
+// True when `st` is being captured into a graph: memory must not be allocated then (a
+// stream-ordered allocation would become graph-owned memory that later non-graph launches
+// still point at, and the old buffer would be freed inside the graph).
+static bool capturing(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return cs != hipStreamCaptureStatusNone;
+}
+
+static int capture_growth_error(const char *what) {
+    return fail(kHipError, std::string("longhair_amd: the ") + what +
+                               " must grow while the stream is being captured; reserve it before capture with "
+                               "cauchy_256_batch_prepare_stream(k, m, bytes, max_stripes, stream) or an "
+                               "uncaptured call of the same size on that stream");
+}
+
+static int device_generator(Device *d, int k, int m, const uint8_t **out, const uint8_t **points = nullptr,
+                            hipStream_t st = nullptr) {
     std::lock_guard<std::mutex> g(d->mu);
     auto it = d->generators.find({k, m});
     if (it == d->generators.end()) {
+        if (capturing(st)) return capture_growth_error("generator matrix");
         std::vector<uint8_t> G = generator_matrix(k, m);
         std::vector<uint8_t> xs, ys;
         const bool pts = cauchy_points(k, m, xs, ys);
@@ -179,9 +220,10 @@ static int device_generator(Device *d, int k, int m, const uint8_t **out, const 
 // device synchronisation: the old page stays allocated (kernels in flight on other streams
 // may still read it) and the new page is cleared on the null stream, which this thread
 // waits for before publishing the pointer (non-blocking streams are not stalled).
-static int zero_page(Device *d, size_t bytes, const uint8_t **out) {
+static int zero_page(Device *d, size_t bytes, const uint8_t **out, hipStream_t st = nullptr) {
     std::lock_guard<std::mutex> g(d->mu);
     if (d->zero.size < bytes) {
+        if (capturing(st)) return capture_growth_error("zero page");
         uint8_t *p = nullptr;
         LH_HIP(hipMalloc(&p, bytes));
         LH_HIP(hipMemsetAsync(p, 0, bytes, nullptr));
@@ -197,6 +239,8 @@ static int zero_page(Device *d, size_t bytes, const uint8_t **out) {
 static int workspace(Device *d, hipStream_t st, size_t plan_bytes, size_t work_bytes, Workspace **out) {
     std::lock_guard<std::mutex> g(d->mu);
     Workspace &w = d->ws[st];
+    if ((plan_bytes > w.plan.size || work_bytes > w.work.size) && capturing(st))
+        return capture_growth_error("per-stream decode workspace");
     LH_HIP(w.plan.reserve(plan_bytes, st));
     if (work_bytes) LH_HIP(w.work.reserve(work_bytes, st));
     *out = &w;
@@ -219,6 +263,19 @@ static int generic_word(int sub) {
     if (sub >= 4) return 4;
     if (sub >= 2) return 2;
     return 1;
+}
+
+// Specialised kernels of a configuration.  Batch calls (allow_compile) compile a missing
+// module with hiprtc unless LONGHAIR_AMD_JIT_COMPILE=0; drop-in calls never compile.
+// Without compiling, a module is still used when it is loaded or in the on-disk cache
+// (jit_cache/, tools/precompile.py); otherwise the caller takes the generic kernels.
+// Returns nullptr with *hard set when a compilation was attempted and failed.
+static const JitKernels *jit_lookup(Device *d, const JitConfig &cfg, bool allow_compile, std::string *err,
+                                    bool *hard) {
+    const bool compile = allow_compile && jit_compile_allowed();
+    const JitKernels *jk = d->jit.get(cfg, err, compile);
+    *hard = !jk && compile;
+    return jk;
 }
 
 // ------------------------------------------------------------------------ encode
@@ -261,7 +318,8 @@ static int encode_batch(int k, int m, int bytes, int stripes, const uint8_t *d_d
     // 32-bit range must cover them: jit_codec.hip lh_encode_wave)
     if (jit_config_for(k, m, bytes, false, &cfg) && data_stride * (cfg.spw ? cfg.spw : 1) < (1ll << 31)) {
         std::string err;
-        const JitKernels *jk = allow_compile ? d->jit.get(cfg, &err) : d->jit.peek(cfg);
+        bool hard = false;
+        const JitKernels *jk = jit_lookup(d, cfg, allow_compile, &err, &hard);
         if (jk) {
             const long long blocks = jit_blocks(cfg, stripes);
             if (blocks > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
@@ -270,13 +328,15 @@ static int encode_batch(int k, int m, int bytes, int stripes, const uint8_t *d_d
             void *args[] = {(void *)&d_data, &in_stride, (void *)&d_rec, &out_stride, &n};
             LH_HIP(hipModuleLaunchKernel(jk->encode, (unsigned)blocks, 1, 1, 256,
                                          1, 1, 0, st, args, nullptr));
+            note_launch("lh_jit_encode");
             return kOk;
         }
-        if (allow_compile) return fail(kHipError, err);
+        if (hard) return fail(kHipError, err);
     }
     if (jit_win_config_for(k, m, bytes, &cfg)) {
         std::string err;
-        const JitKernels *jk = allow_compile ? d->jit.get(cfg, &err) : d->jit.peek(cfg);
+        bool hard = false;
+        const JitKernels *jk = jit_lookup(d, cfg, allow_compile, &err, &hard);
         if (jk && jk->encode_win) {
             const long long blocks = (long long)stripes * (cfg.sub / (64 * cfg.W));
             if (blocks > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
@@ -285,12 +345,13 @@ static int encode_batch(int k, int m, int bytes, int stripes, const uint8_t *d_d
             int n = stripes;
             void *args[] = {(void *)&d_data, &in_stride, (void *)&d_rec, &out_stride, &n};
             LH_HIP(hipModuleLaunchKernel(jk->encode_win, (unsigned)blocks, 1, 1, threads, 1, 1, 0, st, args, nullptr));
+            note_launch("lh_jit_encode_win");
             return kOk;
         }
-        if (allow_compile && !jk) return fail(kHipError, err);
+        if (hard) return fail(kHipError, err);
     }
     const uint8_t *G = nullptr;
-    if (int rc = device_generator(d, k, m, &G)) return rc;
+    if (int rc = device_generator(d, k, m, &G, nullptr, st)) return rc;
     ApplyArgs a{};
     a.in = d_data;
     a.in_stride = data_stride;
@@ -331,14 +392,15 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
     const JitKernels *jk = nullptr;
     std::string err;
     if (jit_ok) {
-        jk = allow_compile ? d->jit.get(cfg, &err) : d->jit.peek(cfg);
-        if (!jk && allow_compile) return fail(kHipError, err);
+        bool hard = false;
+        jk = jit_lookup(d, cfg, allow_compile, &err, &hard);
+        if (hard) return fail(kHipError, err);
     }
     const bool generic = (k > 1 && m > 1) && !jk;
     if (jk && jk->decode_fused && std::getenv("LONGHAIR_AMD_NO_FUSED_PLAN") == nullptr) {
         // Plan computed inside the decode kernel: one launch, no plan workspace.
         const uint8_t *zero = nullptr;
-        if (int rc = zero_page(d, (size_t)bytes, &zero)) return rc;
+        if (int rc = zero_page(d, (size_t)bytes, &zero, st)) return rc;
         const long long blocks = jit_blocks(cfg, stripes);
         hipFunction_t fn = jk->decode_fused;
         long long s1 = stride;
@@ -348,6 +410,7 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         void *args[] = {(void *)&d_blocks, &s1, (void *)&d_rows, (void *)&d_status, (void *)&zero,
                         (void *)&gexp, (void *)&glog, &n};
         LH_HIP(hipModuleLaunchKernel(fn, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr));
+        note_launch("lh_jit_decode_fused");
         return kOk;
     }
     // Large m (<= 64), sub % (64 W) == 0, after the planner: the windowed phase-A kernel
@@ -356,15 +419,16 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
     JitConfig wcfg;
     const JitKernels *wk = nullptr;
     if (generic && jit_win_config_for(k, m, bytes, &wcfg, true)) {
-        wk = allow_compile ? d->jit.get(wcfg, &err) : d->jit.peek(wcfg);
-        if (!wk && allow_compile) return fail(kHipError, err);
+        bool hard = false;
+        wk = jit_lookup(d, wcfg, allow_compile, &err, &hard);
+        if (hard) return fail(kHipError, err);
         if (wk && !wk->decode_wide) wk = nullptr;
     }
     const size_t work_bytes = (generic && !wk) ? (size_t)stripes * e_max * bytes : 0;
     Workspace *w = nullptr;
     if (int rc = workspace(d, st, (size_t)stripes * plan_stride, work_bytes, &w)) return rc;
     const uint8_t *G = nullptr, *points = nullptr;
-    if (int rc = device_generator(d, k, m, &G, &points)) return rc;
+    if (int rc = device_generator(d, k, m, &G, &points, st)) return rc;
 
     PlanArgs pa{};
     pa.rows = d_rows;
@@ -404,18 +468,19 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
     }
     if (jk) {
         const uint8_t *zero = nullptr;
-        if (int rc = zero_page(d, (size_t)bytes, &zero)) return rc;
+        if (int rc = zero_page(d, (size_t)bytes, &zero, st)) return rc;
         const long long blocks = jit_blocks(cfg, stripes);
         long long s1 = stride, s2 = plan_stride;
         const uint8_t *plan = w->plan.ptr;
         int n = stripes;
         void *args[] = {(void *)&d_blocks, &s1, (void *)&plan, &s2, (void *)&zero, &n};
         LH_HIP(hipModuleLaunchKernel(jk->decode, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr));
+        note_launch("lh_jit_decode");
         return kOk;
     }
     if (wk) {
         const uint8_t *zero = nullptr;
-        if (int rc = zero_page(d, (size_t)bytes, &zero)) return rc;
+        if (int rc = zero_page(d, (size_t)bytes, &zero, st)) return rc;
         const long long blocks = (long long)stripes * (wcfg.sub / (64 * wcfg.W));
         if (blocks > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
         const unsigned threads = 64u * (unsigned)((m + wcfg.rows_per_wave - 1) / wcfg.rows_per_wave);
@@ -424,6 +489,7 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         int n = stripes;
         void *args[] = {(void *)&d_blocks, &s1, (void *)&plan, &s2, (void *)&zero, &n};
         LH_HIP(hipModuleLaunchKernel(wk->decode_wide, (unsigned)blocks, 1, 1, threads, 1, 1, 0, st, args, nullptr));
+        note_launch(wk->cfg.win_split ? "lh_jit_decode_wide" : "lh_jit_decode_wide(fused phase B)");
         if (wk->cfg.win_split) {  // phase A left V_r in the recovery slots: phase B
             InverseArgs ia{};
             ia.blocks = d_blocks;
@@ -642,18 +708,21 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
 }
 
 // ------------------------------------------------------------ drop-in dispatch
-// Where a drop-in call (one stripe, the reference's call shape) runs.  kGpu: always on the
-// device (default).  kAuto: calls whose blocks all live in host memory and whose XOR work
-// is at most g_host_max_work bytes run on the host SIMD engine (host_codec.cpp), the rest
-// on the device.  kHost: every all-host-memory call on the host engine.  Device (or mixed)
-// pointers always go to the device.  The library needs a GPU under every policy.
+// Where a drop-in call (one stripe, the reference's call shape) runs.  kAuto (default):
+// calls whose blocks all live in host memory and whose XOR work is at most
+// g_host_max_work bytes run on the host SIMD engine (host_codec.cpp), the rest on the
+// device -- a one-stripe call from host memory cannot amortise a PCIe round trip (k29/m4:
+// ~35 us staged through the GPU against ~7 us on the host engine and ~9 us for the
+// reference).  kGpu: always on the device.  kHost: every all-host-memory call on the host
+// engine.  Device (or mixed) pointers always go to the device.  The library needs a GPU
+// under every policy.
 enum { kDispatchGpu = 0, kDispatchAuto = 1, kDispatchHost = 2 };
 
 static int env_dispatch() {
     const char *e = std::getenv("LONGHAIR_AMD_DISPATCH");
-    if (!e) return kDispatchGpu;
+    if (!e) return kDispatchAuto;
     const std::string v(e);
-    return v == "auto" ? kDispatchAuto : v == "host" ? kDispatchHost : kDispatchGpu;
+    return v == "gpu" ? kDispatchGpu : v == "host" ? kDispatchHost : kDispatchAuto;
 }
 static std::atomic<int> g_dispatch{env_dispatch()};
 static std::atomic<long long> g_host_max_work{[] {
@@ -815,21 +884,25 @@ LH_API int _cauchy_256_init(int expected_version) {
 }
 
 LH_API int cauchy_256_encode(int k, int m, const unsigned char *data_ptrs[], void *recovery_blocks, int block_bytes) {
+    lh::LaunchTrace trace;
     return lh::dropin_encode(k, m, data_ptrs, recovery_blocks, block_bytes);
 }
 
 LH_API int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes) {
+    lh::LaunchTrace trace;
     return lh::dropin_decode(k, m, blocks, block_bytes);
 }
 
 LH_API int cauchy_256_encode_batch(int k, int m, int block_bytes, int stripes, const void *d_data, long long data_stride,
                             void *d_recovery, long long recovery_stride, void *stream) {
+    lh::LaunchTrace trace;
     return lh::encode_batch(k, m, block_bytes, stripes, (const uint8_t *)d_data, data_stride, (uint8_t *)d_recovery,
                             recovery_stride, (hipStream_t)stream, true);
 }
 
 LH_API int cauchy_256_decode_batch(int k, int m, int block_bytes, int stripes, void *d_blocks, long long stripe_stride,
                             unsigned char *d_rows, signed char *d_status, void *stream) {
+    lh::LaunchTrace trace;
     return lh::decode_batch(k, m, block_bytes, stripes, (uint8_t *)d_blocks, stripe_stride, d_rows,
                             (int8_t *)d_status, (hipStream_t)stream, true);
 }
@@ -837,6 +910,7 @@ LH_API int cauchy_256_decode_batch(int k, int m, int block_bytes, int stripes, v
 LH_API int cauchy_256_encode_host_batch(int k, int m, int block_bytes, int stripes, const void *h_data,
                                         long long data_stride, void *h_recovery, long long recovery_stride,
                                         int chunk_stripes) {
+    lh::LaunchTrace trace;
     return lh::host_encode_batch(k, m, block_bytes, stripes, (const uint8_t *)h_data, data_stride,
                                  (uint8_t *)h_recovery, recovery_stride, chunk_stripes);
 }
@@ -844,11 +918,12 @@ LH_API int cauchy_256_encode_host_batch(int k, int m, int block_bytes, int strip
 LH_API int cauchy_256_decode_host_batch(int k, int m, int block_bytes, int stripes, void *h_blocks,
                                         long long stripe_stride, unsigned char *h_rows, signed char *h_status,
                                         int chunk_stripes) {
+    lh::LaunchTrace trace;
     return lh::host_decode_batch(k, m, block_bytes, stripes, (uint8_t *)h_blocks, stripe_stride, h_rows,
                                  (int8_t *)h_status, chunk_stripes);
 }
 
-LH_API int cauchy_256_batch_prepare(int k, int m, int block_bytes, int max_stripes) {
+LH_API int cauchy_256_batch_prepare_stream(int k, int m, int block_bytes, int max_stripes, void *stream) {
     lh::Device *d = nullptr;
     if (int rc = lh::current_device(&d)) return rc;
     std::string err;
@@ -871,16 +946,22 @@ LH_API int cauchy_256_batch_prepare(int k, int m, int block_bytes, int max_strip
         lh::JitConfig cfg;
         const bool generic = !lh::jit_config_for(k, m, block_bytes, true, &cfg);
         lh::Workspace *w = nullptr;
-        hipStream_t st = nullptr;
+        hipStream_t st = (hipStream_t)stream;
         if (int rc = lh::workspace(d, st, (size_t)max_stripes * lh::PlanView::bytes(k, m, e_max),
                                    generic ? (size_t)max_stripes * e_max * block_bytes : 0, &w))
             return rc;
         const uint8_t *G = nullptr, *z = nullptr;
-        if (int rc = lh::device_generator(d, k, m, &G)) return rc;
-        if (int rc = lh::zero_page(d, (size_t)block_bytes, &z)) return rc;
+        if (int rc = lh::zero_page(d, (size_t)block_bytes, &z, st)) return rc;
+        if (int rc = lh::device_generator(d, k, m, &G, nullptr, st)) return rc;
     }
     return 0;
 }
+
+LH_API int cauchy_256_batch_prepare(int k, int m, int block_bytes, int max_stripes) {
+    return cauchy_256_batch_prepare_stream(k, m, block_bytes, max_stripes, nullptr);
+}
+
+LH_API const char *cauchy_256_last_launch(void) { return lh::g_last_launch.c_str(); }
 
 // Compile the specialised code objects of a shape into the on-disk cache without a GPU
 // (build-time warm-up for shapes whose compilation takes long).  0 ok, -3 on failure.

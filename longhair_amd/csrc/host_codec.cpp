@@ -264,10 +264,15 @@ int encode(int k, int m, const uint8_t *const *data, uint8_t *rec, int bytes) {
     if (k + m > 256 || bytes % 8 != 0) return -1;
     const int sub = bytes / 8;
     const ShapeCache::Entry &S = shape(k, m);
-    const uint8_t *src[256 * 8];
+    // Per-thread scratch, not stack arrays: callers' threads may have small stacks.
+    thread_local std::vector<const uint8_t *> srcv;
+    thread_local std::vector<OutRow> rowv;
+    srcv.resize((size_t)8 * k);
+    rowv.resize((size_t)8 * (m - 1));
+    const uint8_t **src = srcv.data();
     for (int x = 0; x < k; ++x)
         for (int b = 0; b < 8; ++b) src[8 * x + b] = data[x] + (size_t)b * sub;
-    OutRow rows[255 * 8];
+    OutRow *rows = rowv.data();
     for (int r = 1; r < m; ++r) term_rows(S.T, r, rec + (size_t)r * bytes, sub, nullptr, 0, rows + 8 * (r - 1));
     apply(rows, 8 * (m - 1), src, sub);
     return 0;
@@ -331,7 +336,9 @@ int decode(int k, int m, Block *blocks, int bytes) {
     thread_local std::vector<uint8_t> zero, V;
     if (zero.size() < (size_t)bytes) zero.assign((size_t)bytes, 0);
     if (V.size() < (size_t)e * bytes) V.resize((size_t)e * bytes);
-    const uint8_t *src[256 * 8];
+    thread_local std::vector<const uint8_t *> srcv;
+    srcv.resize((size_t)8 * k);
+    const uint8_t **src = srcv.data();
     for (int x = 0; x < k; ++x) {
         const uint8_t *d = slot_of_row[x] >= 0 ? blocks[slot_of_row[x]].data : zero.data();
         for (int b = 0; b < 8; ++b) src[8 * x + b] = d + (size_t)b * sub;

@@ -634,7 +634,12 @@ static std::string cache_path(const std::string &src) {
     return d.empty() ? "" : d + name;
 }
 
-bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::string *err, bool fresh) {
+bool jit_compile_allowed() {
+    const char *e = std::getenv("LONGHAIR_AMD_JIT_COMPILE");
+    return !(e && std::string(e) == "0");
+}
+
+bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::string *err, bool fresh, bool compile) {
     const std::string src = jit_source_for(cfg);
     const std::string path = cache_path(src);
     if (fresh && !path.empty()) unlink(path.c_str());  // a cached object the loader rejected
@@ -659,6 +664,10 @@ bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::str
                 return true;
             }
         }
+    }
+    if (!compile) {
+        *err = "not cached";
+        return false;
     }
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "lh_jit_codec.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
@@ -692,21 +701,28 @@ bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::str
     return true;
 }
 
-const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err) {
+const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err, bool compile) {
     std::lock_guard<std::mutex> g(mu_);
     const Key key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines, cfg.win_split * 1000000 + cfg.win * 100000 + cfg.win_lds * 10000 + cfg.rows_per_wave * 100 + cfg.win_pf);
     auto it = cache_.find(key);
     if (it != cache_.end()) return &it->second;
+    if (!compile && not_cached_.count(key)) {  // (generating the source to hash it costs ms)
+        *err = "not cached";
+        return nullptr;
+    }
 
     std::vector<char> code;
-    if (!compile_code_object(cfg, &code, err)) return nullptr;
+    if (!compile_code_object(cfg, &code, err, false, compile)) {
+        if (!compile) not_cached_[key] = true;
+        return nullptr;
+    }
 
     JitKernels kern;
     kern.cfg = cfg;
     if (hipModuleLoadData(&kern.module, code.data()) != hipSuccess) {
         // A damaged or foreign cached object: drop it and compile once more.
         (void)hipGetLastError();
-        if (!compile_code_object(cfg, &code, err, true)) return nullptr;
+        if (!compile_code_object(cfg, &code, err, true, compile)) return nullptr;
         if (hipModuleLoadData(&kern.module, code.data()) != hipSuccess) {
             *err = "hipModuleLoadData failed for the specialised kernels";
             return nullptr;

@@ -52,8 +52,9 @@ long long generator_ones(int k, int m);
 class JitCache {
 public:
     // Returns compiled kernels for the configuration (compiling on first use).  On
-    // failure returns nullptr and fills *err.
-    const JitKernels *get(const JitConfig &cfg, std::string *err);
+    // failure returns nullptr and fills *err.  compile = false: only a module already in
+    // memory or in the on-disk cache (nullptr, *err = "not cached", when there is none).
+    const JitKernels *get(const JitConfig &cfg, std::string *err, bool compile = true);
     // Only returns an already compiled entry (no compilation).
     const JitKernels *peek(const JitConfig &cfg);
 
@@ -61,6 +62,7 @@ private:
     using Key = std::tuple<int, int, int, int, std::string, int>;
     std::mutex mu_;
     std::map<Key, JitKernels> cache_;
+    std::map<Key, bool> not_cached_;  // lookups without compilation that found no module
 };
 
 std::string jit_source_for(const JitConfig &cfg);
@@ -68,6 +70,12 @@ std::string jit_source_for(const JitConfig &cfg);
 // Compile (or fetch from the on-disk cache) the code object of a configuration.  Needs
 // no GPU, so build steps can pre-populate the cache.
 // fresh: ignore (and delete) a cached object.
-bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::string *err, bool fresh = false);
+// compile = false: only read the on-disk cache (false, *err = "not cached", if absent).
+bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::string *err, bool fresh = false,
+                         bool compile = true);
+
+// True unless LONGHAIR_AMD_JIT_COMPILE=0: batch calls may run hiprtc for a shape whose
+// specialised module is not cached (drop-in calls never do).
+bool jit_compile_allowed();
 
 }  // namespace lh

@@ -257,7 +257,9 @@ __global__ void __launch_bounds__(256) lh_plan_kernel(lh::PlanArgs a) {
         const int r = rows[i];
         if (r < k + m && slot_of[r] != i) bad = true;
     }
-    const int status = __ballot(bad) ? -1 : 0;
+    // m == 1 follows cauchy_decode_m1 (:487-535), which accepts any rows: every row >= k is
+    // a recovery block (the last one in array order is the output), repeats are harmless.
+    const int status = (__ballot(bad) && m > 1) ? -1 : 0;
     const unsigned long long below = (1ull << lane) - 1;
     int n_rcv = 0, n_miss = 0;
     for (int i0 = 0; i0 < k; i0 += 64) {
@@ -693,8 +695,10 @@ __device__ __forceinline__ void lh_inv_rows(uint32_t (&acc)[OPW][8], const uint8
 // indices are the nibbles of c * 2^y.  Those are compile-time constants of 256 fixed-size
 // bodies (8 v_bitop3 + s_branch = 68 bytes, inv_jump.inc, tools/gen_inv_jump.py); the
 // wave jumps to body c with s_setpc_b64 (c is wave-uniform): 8 VALU per (output, row)
-// against the Horner form's 8 bit branches and ~32 XORs.  Two outputs per wave: the two
-// jump tables (35 KiB) stay within the instruction cache.
+// against the Horner form's 8 bit branches and ~32 XORs.  Every output of a wave inlines
+// its own copy of the 17 KiB table: JO = 4 (the default) is about 70 KiB of code, more than
+// the instruction cache (JO = 2, 35 KiB, fits but builds the tables for half as many
+// outputs and measured slower).
 #include "inv_jump.inc"
 
 __device__ __forceinline__ void lh_mul_jump(unsigned c, uint32_t (&a)[8], const uint32_t (&tl)[16],
@@ -885,6 +889,7 @@ hipError_t launch_apply_generic(const ApplyArgs &a, int W, hipStream_t st) {
         case 4: hipLaunchKernelGGL(lh_apply_generic_kernel<4>, grid, dim3(256), 0, st, a); break;
         default: return hipErrorInvalidValue;
     }
+    note_launch("lh_apply_generic_kernel");
     return hipGetLastError();
 }
 
@@ -894,35 +899,45 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     const long long blocks = (long long)a.stripes * (a.bytes / 2048);
     if (blocks <= 0) return hipSuccess;
     if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-    // Outputs per wave: 4 (default; LONGHAIR_AMD_INV_OPW=8: half the waves, twice the
-    // accumulators: k128/m32 decode 4.24 against 4.12 ms).  (Rows taken in pairs, XOR3 when both
-    // coefficient bits are set, 25 % fewer XORs behind nested branches: 5.90 against 4.12 ms.)
-    const char *o = std::getenv("LONGHAIR_AMD_INV_OPW");
-    const int opw = (o && std::atoi(o) == 8) ? 8 : 4;
-    // The computed-jump kernel with 4 outputs per wave (default): for e_max <= 32 the V rows
-    // are staged 16 at a time (32 KiB tile; k128/m32 decode 4.10 -> 3.84 ms against all 32
-    // at once), above that all at once (128 KiB; 16-row staging measured 2 % slower for
-    // k200/m56).  LONGHAIR_AMD_INV_JUMP=0: the Horner kernel; =2: two outputs per wave
-    // (e_max <= 32); =40: e_max <= 32 staged at once (profiles/r2_tune_split_decode.txt).
-    bool jt_done = true;
+    // Phase-B kernel, knob LONGHAIR_AMD_INV_JUMP (profiles/r2_tune_split_decode.txt):
+    //    4 (default)  computed jump, 4 outputs per wave: e_max <= 32 stages the V rows 16 at
+    //                 a time (lh_inverse_jt_kernel<4,32,16>; k128/m32 decode 4.10 -> 3.84 ms
+    //                 against all 32 at once), e_max > 32 all at once (<4,64,0>; 16-row
+    //                 staging measured 2 % slower for k200/m56)
+    //   40            e_max <= 32 staged all at once (<4,32,0>); e_max > 32 as 4
+    //    2            two outputs per wave (<2,32,0>, 4.51 ms), e_max <= 32 only; larger
+    //                 e_max falls back to the Horner kernel
+    //    0            the Horner kernel lh_inverse_kernel, LONGHAIR_AMD_INV_OPW = 4 (default)
+    //                 or 8 outputs per wave (k128/m32 decode 4.24 against 4.12 ms)
     const char *jpe = std::getenv("LONGHAIR_AMD_INV_JUMP");
     const int jp = jpe ? std::atoi(jpe) : 4;
-    if (jp != 0) {
-        const unsigned jt = 64u * (unsigned)((a.e_max + (jp == 2 ? 1 : 3)) / (jp == 2 ? 2 : 4));
-        const dim3 grid((unsigned)blocks);
-        if (jp == 2 && a.e_max <= 32) hipLaunchKernelGGL((lh_inverse_jt_kernel<2, 32, 0>), grid, dim3(jt), 0, st, a);
-        else if (jp == 40 && a.e_max <= 32)  // (A/B) all rows staged at once
-            hipLaunchKernelGGL((lh_inverse_jt_kernel<4, 32, 0>), grid, dim3(jt), 0, st, a);
-        else if (a.e_max <= 32) hipLaunchKernelGGL((lh_inverse_jt_kernel<4, 32, 16>), grid, dim3(jt), 0, st, a);
-        else if (jp != 2) hipLaunchKernelGGL((lh_inverse_jt_kernel<4, 64, 0>), grid, dim3(jt), 0, st, a);
-        else jt_done = false;
-        if (jt_done) return hipGetLastError();
+    const dim3 grid((unsigned)blocks);
+    if (jp == 2 && a.e_max <= 32) {
+        hipLaunchKernelGGL((lh_inverse_jt_kernel<2, 32, 0>), grid, dim3(64u * (unsigned)((a.e_max + 1) / 2)), 0, st, a);
+        note_launch("lh_inverse_jt_kernel<2,32,0>");
+        return hipGetLastError();
     }
+    if (jp != 0 && jp != 2) {
+        const dim3 block(64u * (unsigned)((a.e_max + 3) / 4));
+        if (a.e_max > 32) {
+            hipLaunchKernelGGL((lh_inverse_jt_kernel<4, 64, 0>), grid, block, 0, st, a);
+            note_launch("lh_inverse_jt_kernel<4,64,0>");
+        } else if (jp == 40) {
+            hipLaunchKernelGGL((lh_inverse_jt_kernel<4, 32, 0>), grid, block, 0, st, a);
+            note_launch("lh_inverse_jt_kernel<4,32,0>");
+        } else {
+            hipLaunchKernelGGL((lh_inverse_jt_kernel<4, 32, 16>), grid, block, 0, st, a);
+            note_launch("lh_inverse_jt_kernel<4,32,16>");
+        }
+        return hipGetLastError();
+    }
+    const char *o = std::getenv("LONGHAIR_AMD_INV_OPW");
+    const int opw = (o && std::atoi(o) == 8) ? 8 : 4;
     const unsigned threads = 64u * (unsigned)((a.e_max + opw - 1) / opw);
     if (threads > 1024) return hipErrorInvalidValue;
-    const dim3 grid((unsigned)blocks), block(threads);
-    if (opw == 4) hipLaunchKernelGGL(lh_inverse_kernel<4>, grid, block, 0, st, a);
-    else hipLaunchKernelGGL(lh_inverse_kernel<8>, grid, block, 0, st, a);
+    if (opw == 4) hipLaunchKernelGGL(lh_inverse_kernel<4>, grid, dim3(threads), 0, st, a);
+    else hipLaunchKernelGGL(lh_inverse_kernel<8>, grid, dim3(threads), 0, st, a);
+    note_launch(opw == 4 ? "lh_inverse_kernel<4>" : "lh_inverse_kernel<8>");
     return hipGetLastError();
 }
 
@@ -932,18 +947,21 @@ hipError_t launch_writeback(const WritebackArgs &a, hipStream_t st) {
     if (((a.bytes | a.host_stride | (long long)(uintptr_t)a.host) & 7) != 0 || a.k < 1 || a.k > 255)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(lh_writeback_kernel, dim3((unsigned)a.stripes), dim3(256), 0, st, a);
+    note_launch("lh_writeback_kernel");
     return hipGetLastError();
 }
 
 hipError_t launch_xor_reduce(const XorArgs &a, hipStream_t st) {
     const long long lanes = (long long)a.stripes * a.nch;
     hipLaunchKernelGGL(lh_xor_reduce_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
+    note_launch("lh_xor_reduce_kernel");
     return hipGetLastError();
 }
 
 hipError_t launch_scatter(const ScatterArgs &a, hipStream_t st) {
     const long long lanes = (long long)a.stripes * a.e_max * ((a.bytes + 15) / 16);
     hipLaunchKernelGGL(lh_scatter_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
+    note_launch("lh_scatter_kernel");
     return hipGetLastError();
 }
 
@@ -951,6 +969,7 @@ hipError_t launch_frame(const FrameArgs &a, hipStream_t st) {
     const long long threads = (long long)a.stripes * a.npk * ((a.bytes + 3) / 4);
     if (threads <= 0) return hipSuccess;
     hipLaunchKernelGGL(lh_frame_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, a);
+    note_launch("lh_frame_kernel");
     return hipGetLastError();
 }
 
@@ -959,6 +978,7 @@ hipError_t launch_plan(const PlanArgs &a, hipStream_t st) {
         const unsigned blocks = (unsigned)((a.stripes + 255) / 256);
         if (a.e_max <= 4) hipLaunchKernelGGL(lh_plan_small_kernel<4>, dim3(blocks), dim3(256), 0, st, a);
         else hipLaunchKernelGGL(lh_plan_small_kernel<8>, dim3(blocks), dim3(256), 0, st, a);
+        note_launch(a.e_max <= 4 ? "lh_plan_small_kernel<4>" : "lh_plan_small_kernel<8>");
         return hipGetLastError();
     }
     // Few stripes (latency-bound: one workgroup per stripe cannot fill the chip): four
@@ -970,6 +990,7 @@ hipError_t launch_plan(const PlanArgs &a, hipStream_t st) {
         if (v == 64 || v == 128 || v == 256) threads = (unsigned)v;
     }
     hipLaunchKernelGGL(lh_plan_kernel, dim3((unsigned)a.stripes), dim3(threads), lds, st, a);
+    note_launch(a.points ? "lh_plan_kernel(closed form)" : "lh_plan_kernel");
     return hipGetLastError();
 }
 

@@ -125,6 +125,10 @@ struct WritebackArgs {
     int k, bytes, stripes;
 };
 
+// Launch trace (codec.cpp): every launch site records the kernel it enqueued, so the
+// calling thread can ask which kernels its last batch call ran (cauchy_256_last_launch).
+void note_launch(const char *kernel);
+
 hipError_t launch_writeback(const WritebackArgs &a, hipStream_t st);
 hipError_t launch_apply_generic(const ApplyArgs &a, int W, hipStream_t st);
 hipError_t launch_frame(const FrameArgs &a, hipStream_t st);

@@ -13,7 +13,7 @@
  * recovery block is appended in their place; decode must return 0 and every Block must
  * then hold the original of its row.  Exit status 0 = every round trip restored its data.
  *
- * Usage: c_caller gpu|auto|host OUT_FILE < cases
+ * Usage: c_caller default|gpu|auto|host OUT_FILE < cases
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -45,17 +45,19 @@ int main(int argc, char **argv) {
     uint64_t prng = 0x243F6A8885A308D3ull;
     FILE *out;
     if (argc < 3) {
-        fprintf(stderr, "usage: %s gpu|auto|host OUT_FILE < cases\n", argv[0]);
+        fprintf(stderr, "usage: %s default|gpu|auto|host OUT_FILE < cases\n", argv[0]);
         return 2;
     }
     if (cauchy_256_init() != 0) {
         fprintf(stderr, "cauchy_256_init failed\n");
         return 2;
     }
-    cauchy_256_set_dispatch(strcmp(argv[1], "host") == 0   ? CAUCHY_256_DISPATCH_HOST
-                            : strcmp(argv[1], "auto") == 0 ? CAUCHY_256_DISPATCH_AUTO
-                                                           : CAUCHY_256_DISPATCH_GPU,
-                            -1);
+    /* "default": an unchanged reference caller, whatever policy the library starts with */
+    if (strcmp(argv[1], "default") != 0)
+        cauchy_256_set_dispatch(strcmp(argv[1], "host") == 0   ? CAUCHY_256_DISPATCH_HOST
+                                : strcmp(argv[1], "auto") == 0 ? CAUCHY_256_DISPATCH_AUTO
+                                                               : CAUCHY_256_DISPATCH_GPU,
+                                -1);
     out = fopen(argv[2], "wb");
     if (!out) return 2;
     while (scanf("%d %d %d %u", &k, &m, &bytes, &seed) == 4) {

@@ -85,9 +85,37 @@ def test_no_silent_cpu_path():
 
 def test_dispatch_policy_api():
     import longhair_amd
-    assert longhair_amd.dispatch_policy() == "gpu"  # default without LONGHAIR_AMD_DISPATCH
+    if "LONGHAIR_AMD_DISPATCH" not in os.environ:
+        assert longhair_amd.dispatch_policy() == "auto"  # default: small host calls stay on the host
+    prev = longhair_amd.set_dispatch("gpu")
+    assert longhair_amd.dispatch_policy() == "gpu"
     assert longhair_amd.set_dispatch("auto") == "gpu"
-    assert longhair_amd.dispatch_policy() == "auto"
-    assert longhair_amd.set_dispatch("gpu") == "auto"
+    assert longhair_amd.set_dispatch(prev) == "auto"
     assert longhair_amd.lib().cauchy_256_set_dispatch(7, -1) == -1
     assert longhair_amd.host_isa() in ("avx512bw", "avx2", "scalar")
+
+
+def test_launch_trace_empty_without_gpu():
+    """cauchy_256_last_launch names the kernels of the last call; a call that fails before
+    any launch (no device here) leaves it empty."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import longhair_amd
+    rc = longhair_amd.lib().cauchy_256_encode_batch(4, 2, 16, 1, None, 64, None, 32, None)
+    assert rc == -2
+    assert longhair_amd.last_launch() == []
+
+
+def test_inv_jump_table_is_generated():
+    """inv_jump.inc (the computed-jump bodies of lh_inverse_jt_kernel) is exactly what
+    tools/gen_inv_jump.py renders: no hand edits, no stale generator."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_inv_jump", os.path.join(REPO, "tools", "gen_inv_jump.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    committed = open(os.path.join(REPO, "longhair_amd", "csrc", "inv_jump.inc")).read()
+    assert committed == gen.render()
+    # 256 bodies of 8 v_bitop3_b32 + a branch: the fixed 68-byte stride the jump assumes
+    assert committed.count("v_bitop3_b32") == 256 * 8
+    assert committed.count("s_branch 3f") == 256

@@ -1,0 +1,263 @@
+"""GPU parity at every kernel-selection boundary, each side asserted by the launch trace.
+
+The product picks its kernels by shape (longhair_amd/csrc/jit.cpp jit_config_for /
+jit_win_config_for, codec.cpp encode_batch / decode_batch, kernels.hip launch_plan /
+launch_inverse).  For each boundary a pair of shapes straddles it; both are encoded and
+decoded against the C oracle (bit-exact data and rewritten rows), with random erasure
+counts (the first stripe always at e = e_max), random recovery rows and shuffled slots,
+and `cauchy_256_last_launch` must name the kernels the boundary predicts -- so every
+variant test runs the kernel it names.
+
+The last test is a sweep shaped like the reference's own `main()` (every k in [1, 255],
+tests/cauchy_256_tests.cpp:227-381) and `order_test` (random positions, :122-205).
+`-m gpu`: needs an MI355X.  The specialised modules of every shape here are compiled at
+build time (tools/precompile.py), so no test waits on hiprtc.
+"""
+import numpy as np
+import pytest
+
+import lhutil
+
+pytestmark = pytest.mark.gpu
+
+FUSED = ["lh_jit_decode_fused"]
+SMALL4 = ["lh_plan_small_kernel<4>", "lh_jit_decode"]
+SMALL8 = ["lh_plan_small_kernel<8>", "lh_jit_decode"]
+GENERIC_CF = ["lh_plan_kernel(closed form)", "lh_apply_generic_kernel", "lh_scatter_kernel"]
+GENERIC_S8 = ["lh_plan_small_kernel<8>", "lh_apply_generic_kernel", "lh_scatter_kernel"]
+WIDE16 = ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_jt_kernel<4,32,16>"]
+WIDE64 = ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_jt_kernel<4,64,0>"]
+
+# (id, k, m, bytes, stripes, env, encode kernels, decode kernels)
+BOUNDARIES = [
+    # fused in-kernel plan <-> separate planner: k <= 64
+    ("k64-fused", 64, 4, 1296, 48, {}, ["lh_jit_encode"], FUSED),
+    ("k65-planned", 65, 4, 1296, 48, {}, ["lh_jit_encode"], SMALL4),
+    # ... and one stripe per <= 64 lanes (nch = 64 with 8-byte lanes; 65 with W pinned to 8)
+    ("nch64-fused", 8, 4, 4096, 24, {}, ["lh_jit_encode"], FUSED),
+    ("nch65-planned", 8, 4, 4160, 24, {"LONGHAIR_AMD_JIT_W": "8"}, ["lh_jit_encode"], SMALL4),
+    # ... and e_max <= 4 (both sides of e_max = min(k, m) = 4 / 5, from k and from m)
+    ("emax4-k", 4, 8, 64, 64, {}, ["lh_jit_encode"], FUSED),
+    ("emax5-k", 5, 8, 64, 64, {}, ["lh_jit_encode"], SMALL8),
+    ("emax4-m", 10, 4, 64, 64, {}, ["lh_jit_encode"], FUSED),
+    ("emax5-m", 10, 5, 64, 64, {}, ["lh_jit_encode"], SMALL8),
+    # specialised decode needs e_max * m <= 64 (e_max 8 / 9): small planner <-> Cauchy planner
+    ("emax8", 9, 8, 64, 64, {}, ["lh_jit_encode"], SMALL8),
+    ("emax9", 9, 9, 64, 64, {}, ["lh_jit_encode"], GENERIC_CF),
+    ("emax8-k16", 16, 8, 64, 64, {}, ["lh_jit_encode"], SMALL8),
+    ("emax9-k16", 16, 9, 64, 64, {}, ["lh_jit_encode"], GENERIC_CF),
+    # generator from the CAUCHY_MATRIX_2..6 tables (m <= 6) <-> from the X/Y points (m >= 7)
+    ("m6-jit", 20, 6, 64, 64, {}, ["lh_jit_encode"], SMALL8),
+    ("m7-jit", 20, 7, 64, 64, {}, ["lh_jit_encode"], SMALL8),
+    ("m6-generic", 20, 6, 64, 64, {"LONGHAIR_AMD_PATH": "generic"}, ["lh_apply_generic_kernel"], GENERIC_S8),
+    ("m7-generic", 20, 7, 64, 64, {"LONGHAIR_AMD_PATH": "generic"}, ["lh_apply_generic_kernel"], GENERIC_S8),
+    # register-resident encode network: m <= 12 (96 accumulator dwords) <-> windowed / generic
+    ("enc-m12", 40, 12, 2048, 8, {}, ["lh_jit_encode"], WIDE16),
+    ("enc-m13", 40, 13, 2048, 8, {}, ["lh_jit_encode_win"], WIDE16),
+    ("enc-m12-small", 10, 12, 64, 32, {}, ["lh_jit_encode"], GENERIC_CF),
+    ("enc-m13-small", 10, 13, 64, 32, {}, ["lh_apply_generic_kernel"], GENERIC_CF),
+    # windowed decode: m <= 64 (the used-row ballot) and sub % 256 == 0
+    ("wide-m64", 20, 64, 2048, 8, {}, ["lh_jit_encode_win"], WIDE16),
+    ("generic-m65", 20, 65, 2048, 8, {}, ["lh_jit_encode_win"], GENERIC_CF),
+    ("wide-sub512", 40, 20, 4096, 8, {}, ["lh_jit_encode_win"], WIDE16),
+    ("generic-sub513", 40, 20, 4104, 8, {}, ["lh_apply_generic_kernel"], GENERIC_CF),
+    # phase B: V rows staged 16 at a time for e_max <= 32, all at once above
+    ("jump-emax32", 40, 32, 2048, 8, {}, ["lh_jit_encode_win"], WIDE16),
+    ("jump-emax33", 40, 33, 2048, 8, {}, ["lh_jit_encode_win"], WIDE64),
+]
+
+# Phase-B kernel variants (kernels.hip launch_inverse, LONGHAIR_AMD_INV_JUMP / _INV_OPW).
+PHASE_B = [
+    ({"LONGHAIR_AMD_INV_JUMP": "0"}, 32, "lh_inverse_kernel<4>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "0", "LONGHAIR_AMD_INV_OPW": "8"}, 32, "lh_inverse_kernel<8>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "0"}, 33, "lh_inverse_kernel<4>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "0", "LONGHAIR_AMD_INV_OPW": "8"}, 33, "lh_inverse_kernel<8>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "2"}, 32, "lh_inverse_jt_kernel<2,32,0>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "2"}, 33, "lh_inverse_kernel<4>"),      # e_max > 32: Horner
+    ({"LONGHAIR_AMD_INV_JUMP": "40"}, 32, "lh_inverse_jt_kernel<4,32,0>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "40"}, 33, "lh_inverse_jt_kernel<4,64,0>"),
+]
+
+
+@pytest.fixture(scope="module")
+def lh():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need an MI355X"
+    import longhair_amd
+    assert longhair_amd.cauchy_256_init() == 0
+    return longhair_amd
+
+
+def _gpu(arr):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(arr)).cuda()
+
+
+def _scenarios(k, m, stripes, seed, e_first=None):
+    """Per stripe: random e in [0, e_max] (stripe 0: e_first, default e_max), random erased
+    originals, random recovery rows, shuffled slot order (lhutil.erasure_case)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    e_max = min(k, m)
+    out = []
+    for s in range(stripes):
+        e = (e_max if e_first is None else e_first) if s == 0 else int(rng.integers(0, e_max + 1))
+        out.append(lhutil.erasure_case(int(rng.integers(0, 2**31)), k, m, e))
+    return out
+
+
+def roundtrip(lh, oracle, k, m, nbytes, stripes, seed, scen=None):
+    """encode_batch + decode_batch of `stripes` stripes against the oracle.  Returns the
+    launch traces (encode, decode)."""
+    import torch
+    data = lhutil.fill(seed, stripes * k * nbytes).reshape(stripes, k, nbytes)
+    rec = lh.encode_batch(_gpu(data), m)
+    torch.cuda.synchronize()
+    enc_trace = lh.last_launch()
+    got_rec = rec.cpu().numpy()
+    scen = scen or _scenarios(k, m, stripes, seed)
+    blocks = np.zeros((stripes, k, nbytes), dtype=np.uint8)
+    rows = np.zeros((stripes, k), dtype=np.uint8)
+    for s in range(stripes):
+        rc, exp = oracle.encode(k, m, data[s], nbytes)
+        assert rc == 0
+        assert got_rec[s].tobytes() == exp.tobytes(), ("encode", k, m, nbytes, s)
+        exp = exp.reshape(m, nbytes)
+        slots, rws = scen[s]
+        for i, (kind, x) in enumerate(slots):
+            blocks[s, i] = data[s, x] if kind == "d" else exp[x]
+        rows[s] = rws
+    d_blocks, d_rows = _gpu(blocks), _gpu(rows)
+    status = lh.decode_batch(d_blocks, d_rows, m)
+    torch.cuda.synchronize()
+    dec_trace = lh.last_launch()
+    got, got_rows, st = d_blocks.cpu().numpy(), d_rows.cpu().numpy(), status.cpu().numpy()
+    assert (st == 0).all()
+    for s in range(stripes):
+        bufs = [blocks[s, i].copy() for i in range(k)]
+        rc, exp_rows = oracle.decode(k, m, bufs, list(rows[s]), nbytes)
+        assert rc == 0
+        assert list(got_rows[s]) == exp_rows, ("rows", k, m, nbytes, s)
+        for i in range(k):
+            assert got[s, i].tobytes() == bufs[i].tobytes(), ("decode", k, m, nbytes, s, i)
+    return enc_trace, dec_trace
+
+
+@pytest.mark.parametrize("case", BOUNDARIES, ids=[c[0] for c in BOUNDARIES])
+def test_selection_boundary(lh, oracle, monkeypatch, case):
+    name, k, m, nbytes, stripes, env, enc_k, dec_k = case
+    for key, v in env.items():
+        monkeypatch.setenv(key, v)
+    enc, dec = roundtrip(lh, oracle, k, m, nbytes, stripes, seed=k * 1000 + m * 10 + nbytes)
+    assert enc == enc_k, (name, enc)
+    assert dec == dec_k, (name, dec)
+
+
+@pytest.mark.parametrize("env,m,kernel", PHASE_B,
+                         ids=[f"{'-'.join(v for v in e.values())}-m{m}" for e, m, _ in PHASE_B])
+def test_phase_b_variant(lh, oracle, monkeypatch, env, m, kernel):
+    """Every phase-B kernel of the split large-m decode against the oracle (k = 40, 2048-byte
+    blocks, e_max = m), on both sides of e_max = 32."""
+    for key, v in env.items():
+        monkeypatch.setenv(key, v)
+    k, nbytes = 40, 2048
+    enc, dec = roundtrip(lh, oracle, k, m, nbytes, 8, seed=m * 31)
+    assert dec == ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", kernel], dec
+
+
+def _sweep_ms(k):
+    return sorted({m for m in list(range(1, 9)) + [16, 32, 64, 256 - k] if 1 <= m and k + m <= 256})
+
+
+def test_reference_main_sweep(lh, oracle, monkeypatch):
+    """Every k in [1, 255] x m in {1..8, 16, 32, 64, 256 - k}: 3 stripes each, the first at
+    e = min(k, m) erasures, the others at random e in [0, min(k, m)], random positions and
+    recovery rows, shuffled slots, block sizes 8..64 bytes; encode_batch + decode_batch
+    against the oracle.
+
+    Shapes whose specialised module is in the build's code-object cache take it (every
+    k <= 16 with m <= 8 is precompiled, tools/precompile.py SWEEP); the rest run the generic
+    kernels -- LONGHAIR_AMD_JIT_COMPILE=0 keeps hiprtc out of the test (a k = 100 module
+    takes minutes to compile).  The launch traces must show both families."""
+    monkeypatch.setenv("LONGHAIR_AMD_JIT_COMPILE", "0")
+    seen = set()
+    n = 0
+    for k in range(1, 256):
+        for m in _sweep_ms(k):
+            nbytes = 8 * (1 + (7 * k + m) % 8)
+            scen = _scenarios(k, m, 3, seed=k * 257 + m)
+            enc, dec = roundtrip(lh, oracle, k, m, nbytes, 3, seed=k * 997 + m, scen=scen)
+            seen.update(enc + dec)
+            n += 1
+    assert n > 2500
+    assert {"lh_jit_encode", "lh_jit_decode_fused", "lh_jit_decode", "lh_apply_generic_kernel",
+            "lh_xor_reduce_kernel"} <= seen, sorted(seen)
+
+
+@pytest.mark.parametrize("k,nbytes", [(29, 1296), (5, 24), (2, 8)])
+def test_m1_accepts_any_rows_like_the_reference(lh, oracle, k, nbytes):
+    """m == 1 decode (cauchy_decode_m1, cauchy_256.cpp:487-535) accepts any rows: rows >= k
+    are recovery blocks (the last in array order is the output), repeated originals are
+    harmless, and with no recovery block blocks[0] is overwritten.  The batch path must
+    give the oracle's bytes, rows and status 0 for all of them."""
+    import torch
+    rng = np.random.Generator(np.random.PCG64(k))
+    cases = [
+        [k + 5] + list(range(1, k)),                       # recovery row out of range for m = 1
+        [0] * k,                                           # every slot claims original 0
+        list(range(k - 1)) + [k],                          # one recovery block, last slot
+        [k, k + 1] + list(range(2, k)) if k > 2 else [k, k + 1],  # two recovery blocks
+        list(range(k)),                                    # no erasure: the quirk
+        list(rng.integers(0, 256, k)),                     # anything
+    ]
+    for rows in cases:
+        rows = [int(r) for r in rows][:k]
+        blocks = lhutil.fill(k + len(rows), k * nbytes).reshape(1, k, nbytes)
+        d_blocks, d_rows = _gpu(blocks), _gpu(np.array([rows], dtype=np.uint8))
+        status = lh.decode_batch(d_blocks, d_rows, 1)
+        torch.cuda.synchronize()
+        bufs = [blocks[0, i].copy() for i in range(k)]
+        rc, exp_rows = oracle.decode(k, 1, bufs, rows, nbytes)
+        assert rc == 0
+        assert int(status.cpu()[0]) == 0, rows
+        assert list(d_rows.cpu().numpy()[0]) == exp_rows, rows
+        got = d_blocks.cpu().numpy()[0]
+        assert all(got[i].tobytes() == bufs[i].tobytes() for i in range(k)), rows
+
+
+def test_capture_never_allocates(lh):
+    """A decode captured into a graph on a stream whose workspace was never reserved must
+    fail with -3 (nothing enqueued) instead of allocating graph-owned memory; after
+    cauchy_256_batch_prepare_stream on that stream the same capture works and replays."""
+    import torch
+    k, m, nbytes, stripes = 200, 56, 65536 // 64, 16   # generic path (sub % 256 != 0): plan + work
+    data = torch.randint(0, 256, (stripes, k, nbytes), dtype=torch.uint8, device="cuda")
+    rec = lh.encode_batch(data, m)
+    blocks = data.clone()
+    blocks[:, :m] = rec
+    rows0 = torch.tensor([[k + r for r in range(m)] + list(range(m, k))] * stripes, dtype=torch.uint8,
+                         device="cuda")
+    rows = rows0.clone()
+    status = torch.empty((stripes,), dtype=torch.int8, device="cuda")
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    graph = torch.cuda.CUDAGraph()
+    failed = None
+    try:
+        with torch.cuda.graph(graph, stream=s):
+            try:
+                lh.decode_batch(blocks, rows, m, status=status, stream=s)
+            except lh.LonghairError as e:
+                failed = e
+    except RuntimeError:
+        pass  # an empty capture may be rejected by torch; what matters is the codec's error
+    assert failed is not None and failed.code == -3 and "capture" in str(failed)
+    torch.cuda.synchronize()
+    lh.prepare(k, m, nbytes, stripes, stream=s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        rows.copy_(rows0)
+        lh.decode_batch(blocks, rows, m, status=status, stream=s)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert int((status != 0).sum()) == 0
+    assert torch.equal(blocks, data) and torch.equal(rows[0].cpu(), torch.arange(k, dtype=torch.uint8))

@@ -1,8 +1,8 @@
 """A native C program calls the drop-in boundary exactly as a user of the reference would:
 compiled against include/cauchy_256.h and linked with -llonghair_amd (tests/native/c_caller.c,
 order_test-style round trips, tests/cauchy_256_tests.cpp:122-205).  Its encode bytes and
-codes must equal the reference's golden fixtures.  Runs under the GPU and host dispatch
-policies.  `-m gpu`: the library needs an MI355X."""
+codes must equal the reference's golden fixtures.  Runs under the library's default dispatch
+policy (AUTO) and under the GPU and host policies.  `-m gpu`: the library needs an MI355X."""
 import json
 import os
 import subprocess
@@ -25,7 +25,7 @@ def exe():
     return EXE
 
 
-@pytest.mark.parametrize("policy", ["gpu", "host"])
+@pytest.mark.parametrize("policy", ["default", "gpu", "host"])
 def test_c_caller_matches_goldens(exe, policy, tmp_path):
     grid = json.load(open(os.path.join(lhutil.GOLDEN, "encode_grid.json")))["cases"]
     # every k in [1, 255] at some m, the invalid-parameter cases and the BASELINE shapes

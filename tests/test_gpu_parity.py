@@ -34,11 +34,16 @@ def _load(name):
     return json.load(open(os.path.join(lhutil.GOLDEN, name)))
 
 
-@pytest.fixture(params=["gpu", "host-avx512bw", "host-avx2", "host-scalar"])
+@pytest.fixture(params=["default", "gpu", "host-avx512bw", "host-avx2", "host-scalar"])
 def policy(request, lh, monkeypatch):
-    """Drop-in dispatch policy (include/cauchy_256_dispatch.h): every drop-in test runs on
-    the GPU and on each instruction-set level of the host SIMD engine."""
-    if request.param == "gpu":
+    """Drop-in dispatch policy (include/cauchy_256_dispatch.h): every drop-in test runs under
+    the library's default policy (AUTO, as an unchanged reference caller), on the GPU and on
+    each instruction-set level of the host SIMD engine."""
+    if request.param == "default":
+        if "LONGHAIR_AMD_DISPATCH" not in os.environ:
+            assert lh.dispatch_policy() == "auto"
+        prev = lh.dispatch_policy()
+    elif request.param == "gpu":
         prev = lh.set_dispatch("gpu")
     else:
         isa = request.param.split("-")[1]
@@ -139,15 +144,16 @@ def test_dropin_invalid_rows_untouched(lh, policy):
 
 
 def test_dropin_auto_policy_routes_by_size(lh, oracle):
-    """AUTO: a small all-host call runs on the host engine, a large one on the GPU; both
-    return the oracle's bytes."""
+    """AUTO: a small all-host call runs on the host engine (no kernel launched), a large one
+    on the GPU (its kernels in the launch trace); both return the oracle's bytes."""
     codec = DropIn(lh)
     prev = lh.set_dispatch("auto", 1 << 20)
     try:
-        for k, m, nbytes in ((29, 4, 1296), (128, 32, 8192)):
+        for k, m, nbytes, on_gpu in ((29, 4, 1296, False), (128, 32, 8192, True)):
             data = lhutil.fill(k + m, k * nbytes)
             rc, rec = codec.encode(k, m, data, nbytes)
             assert rc == 0 and rec.tobytes() == oracle.encode(k, m, data, nbytes)[1].tobytes()
+            assert bool(lh.last_launch()) == on_gpu, (k, m, lh.last_launch())
     finally:
         lh.set_dispatch(prev, 4 << 20)
 
@@ -240,14 +246,15 @@ def test_decode_batch_vs_oracle(lh, oracle, path, k, m, nbytes, stripes, e):
     _decode_batch_vs_oracle(lh, oracle, k, m, nbytes, stripes, e)
 
 
-@pytest.mark.parametrize("knob,value", [("LONGHAIR_AMD_WIN_SPLIT", "0"), ("LONGHAIR_AMD_INV_OPW", "8")])
 @pytest.mark.parametrize("k,m,nbytes,stripes", [(40, 20, 4096, 8), (100, 16, 2048, 6)])
-def test_wide_decode_variants(lh, oracle, monkeypatch, knob, value, k, m, nbytes, stripes):
-    """Large-m decode with the non-default kernels: the fused phase A + B kernel
-    (LONGHAIR_AMD_WIN_SPLIT=0) and lh_inverse_kernel with 8 outputs per wave."""
-    monkeypatch.setenv(knob, value)
+def test_wide_decode_fused_variant(lh, oracle, monkeypatch, k, m, nbytes, stripes):
+    """Large-m decode with the fused phase A + B kernel (LONGHAIR_AMD_WIN_SPLIT=0): the
+    launch trace shows that kernel ran and no separate phase B.  (The phase-B kernel
+    variants are tested in test_gpu_boundaries.py.)"""
+    monkeypatch.setenv("LONGHAIR_AMD_WIN_SPLIT", "0")
     assert lh.batch_path(k, m, nbytes, True) == "jit-wide"
     _decode_batch_vs_oracle(lh, oracle, k, m, nbytes, stripes, None)
+    assert lh.last_launch() == ["lh_plan_kernel(closed form)", "lh_jit_decode_wide(fused phase B)"]
 
 
 def _decode_batch_vs_oracle(lh, oracle, k, m, nbytes, stripes, e):

@@ -117,3 +117,29 @@ def test_bench_rejects_world_mismatch():
     """Under a torchrun environment the world size must equal --gpus."""
     r, _ = _bench("--gpus", "2", "--dry-run", "--steps", "1", env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_cpu_baseline_uses_the_workload_patterns():
+    """bench.py's cpu_baseline decodes the GPU workload's own erasure patterns (per-stripe e
+    and recovery rows from the Block.row bytes), so its sample states the same mean e."""
+    import numpy as np
+    import bench
+    if not os.path.exists(os.path.join(lhutil.REPO, "oracle", "liblh_cpubench.so")):
+        pytest.skip("oracle/liblh_cpubench.so not built")
+    k, m, nbytes = 12, 5, 64
+    rng = np.random.Generator(np.random.PCG64(3))
+    rows = []
+    for s in range(10):
+        e = int(rng.integers(1, m + 1))
+        keep = rng.permutation(k)[: k - e]
+        rr = rng.permutation(m)[:e]
+        rows.append(np.concatenate([keep, k + rr]))
+    rows = np.array(rows, dtype=np.uint8)
+    erased, e_of, rec, e_max = bench.erasure_patterns(rows, k)
+    assert list(e_of) == [int((r >= k).sum()) for r in rows]
+    for s in range(10):
+        assert set(erased[s, : e_of[s]]) == set(range(k)) - set(rows[s][rows[s] < k].tolist())
+        assert sorted(rec[s, : e_of[s]] + k) == sorted(rows[s][rows[s] >= k].tolist())
+    out = bench.cpu_baseline(k, m, nbytes, 0.3, stripes=10, patterns=rows)
+    assert out["ok"], out
+    assert f"mean e {e_of.mean():.1f}" in out["sample"]

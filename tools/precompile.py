@@ -21,6 +21,21 @@ TESTS = [(29, 2, 1296), (29, 3, 1296), (29, 8, 1296), (4, 2, 16), (10, 6, 8), (1
 VARIANT_SHAPES = [(40, 20, 4096), (100, 16, 2048)]
 
 
+def boundary_jobs():
+    """(shape, env) of every kernel-selection boundary case in tests/test_gpu_boundaries.py
+    (its own list, so the two cannot drift apart)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+    import test_gpu_boundaries as tb
+    jobs = [((k, m, b), dict(env)) for _, k, m, b, _, env, _, _ in tb.BOUNDARIES if "LONGHAIR_AMD_PATH" not in env]
+    return jobs, tb
+
+
+def sweep_shapes(tb):
+    """The specialised shapes of the reference-main sweep (test_reference_main_sweep):
+    every k <= 16 with 2 <= m <= 8 at the sweep's block size (small networks, seconds each)."""
+    return [(k, m, 8 * (1 + (7 * k + m) % 8)) for k in range(2, 17) for m in tb._sweep_ms(k) if 2 <= m <= 8]
+
+
 def main():
     if sys.argv[1:] == ["--prune"]:
         # --all, then delete the cached code objects it neither compiled nor used (outdated
@@ -45,8 +60,16 @@ def main():
             # the large-m shapes' encode and decode modules compile in separate processes
             jobs_list = [(s, part) for s in slow[:2] for part in ("dec", "enc")]
             jobs_list += [(s, None) for s in slow[2:] + [s for s in DEFAULT + TESTS if s not in slow]]
-            # non-default kernels the GPU tests also run (test_wide_decode_variants)
+            # non-default kernels the GPU tests also run (test_wide_decode_fused_variant)
             jobs_list += [(s, ("dec", {"LONGHAIR_AMD_WIN_SPLIT": "0"})) for s in VARIANT_SHAPES]
+            # kernel-selection boundaries and the reference-main sweep (test_gpu_boundaries.py)
+            bj, tb = boundary_jobs()
+            have = {s for s, _ in jobs_list}
+            for sh, env in bj:
+                if env or sh not in have:
+                    jobs_list.append((sh, (None, env)))
+                    have.add(sh)
+            jobs_list += [(sh, None) for sh in dict.fromkeys(sweep_shapes(tb)) if sh not in have]
 
             def run(job):
                 shape, part = job
