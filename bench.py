@@ -590,7 +590,8 @@ def main():
         sq = load_profile(f"sq_{args.config}.json")
         if sq and args.config != "k29m4" and stripes == CONFIGS[args.config][3]:
             names = dec_k if dom == "decode" else enc_k
-            counts = [sq.get("kernels", {}).get(n, {}).get("SQ_INSTS_VALU") for n in names]
+            base = [n.split("<")[0].split("(")[0] for n in names]   # rocprof names: no template args
+            counts = [sq.get("kernels", {}).get(n, {}).get("SQ_INSTS_VALU") for n in base]
             if all(counts):
                 insts = float(sum(counts))   # every kernel of the phase, over the phase's event time
                 ach = insts / (roof[dom]["ms"] * 1e-3) / 1e9

@@ -67,7 +67,7 @@ int cauchy_256_batch_prepare(int k, int m, int block_bytes, int max_stripes);
  * stream first. */
 int cauchy_256_batch_prepare_stream(int k, int m, int block_bytes, int max_stripes, void *stream);
 
-/* Diagnostics: comma-separated names of the kernels the calling thread's last entry-point
+/* Diagnostics: semicolon-separated names of the kernels the calling thread's last entry-point
  * call (drop-in or batch) enqueued, each once, in launch order (empty when it ran none,
  * e.g. on the host engine). */
 const char *cauchy_256_last_launch(void);

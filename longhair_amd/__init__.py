@@ -223,7 +223,7 @@ def last_launch():
     """Kernels this thread's last entry-point call enqueued (cauchy_256_last_launch), in
     launch order; [] when it ran on the host engine or launched nothing."""
     s = lib().cauchy_256_last_launch().decode()
-    return s.split(",") if s else []
+    return s.split(";") if s else []
 
 
 def batch_path(k, m, block_bytes, decode=False):

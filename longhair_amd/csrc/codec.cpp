@@ -41,11 +41,11 @@ void note_launch(const char *kernel) {
     size_t pos = 0;
     while ((pos = g_last_launch.find(k, pos)) != std::string::npos) {
         const size_t end = pos + k.size();
-        if ((pos == 0 || g_last_launch[pos - 1] == ',') && (end == g_last_launch.size() || g_last_launch[end] == ','))
+        if ((pos == 0 || g_last_launch[pos - 1] == ';') && (end == g_last_launch.size() || g_last_launch[end] == ';'))
             return;
         pos = end;
     }
-    if (!g_last_launch.empty()) g_last_launch += ',';
+    if (!g_last_launch.empty()) g_last_launch += ';';
     g_last_launch += k;
 }
 
@@ -120,6 +120,10 @@ struct HostPinned {
 // Per-stream scratch (decode plans and the generic path's output workspace).
 struct Workspace {
     DevBuf plan, work;
+    // Side stream + events of the chunked large-m decode (phase B of chunk c on `side`
+    // while phase A of chunk c + 1 runs on the caller's stream); created on first use.
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_a = nullptr, ev_join = nullptr;
 };
 
 // Per-device state.
@@ -481,27 +485,73 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
     if (wk) {
         const uint8_t *zero = nullptr;
         if (int rc = zero_page(d, (size_t)bytes, &zero, st)) return rc;
-        const long long blocks = (long long)stripes * (wcfg.sub / (64 * wcfg.W));
-        if (blocks > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
+        const long long cps = wcfg.sub / (64 * wcfg.W);
+        if ((long long)stripes * cps > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
         const unsigned threads = 64u * (unsigned)((m + wcfg.rows_per_wave - 1) / wcfg.rows_per_wave);
-        long long s1 = stride, s2 = plan_stride;
-        const uint8_t *plan = w->plan.ptr;
-        int n = stripes;
-        void *args[] = {(void *)&d_blocks, &s1, (void *)&plan, &s2, (void *)&zero, &n};
-        LH_HIP(hipModuleLaunchKernel(wk->decode_wide, (unsigned)blocks, 1, 1, threads, 1, 1, 0, st, args, nullptr));
-        note_launch(wk->cfg.win_split ? "lh_jit_decode_wide" : "lh_jit_decode_wide(fused phase B)");
-        if (wk->cfg.win_split) {  // phase A left V_r in the recovery slots: phase B
-            InverseArgs ia{};
-            ia.blocks = d_blocks;
-            ia.stride = stride;
-            ia.plan = plan;
-            ia.plan_stride = plan_stride;
-            ia.k = k;
-            ia.m = m;
-            ia.e_max = e_max;
-            ia.bytes = bytes;
-            ia.stripes = stripes;
-            LH_HIP(launch_inverse(ia, st));
+        // Split decode in stripe chunks, phase A then phase B per chunk: phase A leaves V_r
+        // in the recovery slots and phase B overwrites those same slots with the outputs, so
+        // when a chunk's V (m blocks per stripe) fits the 256 MiB Infinity Cache, V is read
+        // back from the cache and its lines are rewritten before they reach HBM.
+        // LONGHAIR_AMD_WIDE_CHUNK = stripes per chunk (0 = whole batch at once).
+        long long chunk = stripes;
+        if (wk->cfg.win_split) {
+            const long long vbytes = (long long)m * bytes;  // V per stripe
+            chunk = std::max(1LL, (64LL << 20) / vbytes);
+            if (const char *c = std::getenv("LONGHAIR_AMD_WIDE_CHUNK")) chunk = std::atoll(c) > 0 ? std::atoll(c) : stripes;
+        }
+        // LONGHAIR_AMD_WIDE_OVERLAP=1: phase B of chunk c runs on a side stream, overlapping
+        // phase A of chunk c + 1 (memory-bound) on the caller's stream (fork / join by events,
+        // so the call stays stream-ordered and capturable).
+        bool overlap = false;
+        if (wk->cfg.win_split && chunk < stripes) {
+            const char *o = std::getenv("LONGHAIR_AMD_WIDE_OVERLAP");
+            overlap = o && std::atoi(o) != 0;
+        }
+        if (overlap && !w->side) {
+            if (capturing(st)) {
+                overlap = false;  // (created outside capture only)
+            } else {
+                LH_HIP(hipStreamCreateWithFlags(&w->side, hipStreamNonBlocking));
+                LH_HIP(hipEventCreateWithFlags(&w->ev_fork, hipEventDisableTiming));
+                LH_HIP(hipEventCreateWithFlags(&w->ev_a, hipEventDisableTiming));
+                LH_HIP(hipEventCreateWithFlags(&w->ev_join, hipEventDisableTiming));
+            }
+        }
+        if (overlap) {  // the side stream starts after everything enqueued on st so far
+            LH_HIP(hipEventRecord(w->ev_fork, st));
+            LH_HIP(hipStreamWaitEvent(w->side, w->ev_fork, 0));
+        }
+        for (long long s0 = 0; s0 < stripes; s0 += chunk) {
+            const int n = (int)std::min<long long>(chunk, stripes - s0);
+            uint8_t *cb = d_blocks + s0 * stride;
+            const uint8_t *plan = w->plan.ptr + s0 * plan_stride;
+            long long s1 = stride, s2 = plan_stride;
+            int nn = n;
+            void *args[] = {(void *)&cb, &s1, (void *)&plan, &s2, (void *)&zero, &nn};
+            LH_HIP(hipModuleLaunchKernel(wk->decode_wide, (unsigned)(n * cps), 1, 1, threads, 1, 1, 0, st, args,
+                                         nullptr));
+            note_launch(wk->cfg.win_split ? "lh_jit_decode_wide" : "lh_jit_decode_wide(fused phase B)");
+            if (wk->cfg.win_split) {  // phase A left V_r in the recovery slots: phase B
+                InverseArgs ia{};
+                ia.blocks = cb;
+                ia.stride = stride;
+                ia.plan = plan;
+                ia.plan_stride = plan_stride;
+                ia.k = k;
+                ia.m = m;
+                ia.e_max = e_max;
+                ia.bytes = bytes;
+                ia.stripes = n;
+                if (overlap) {
+                    LH_HIP(hipEventRecord(w->ev_a, st));
+                    LH_HIP(hipStreamWaitEvent(w->side, w->ev_a, 0));
+                }
+                LH_HIP(launch_inverse(ia, overlap ? w->side : st));
+            }
+        }
+        if (overlap) {  // join: later work on st waits for the last phase B
+            LH_HIP(hipEventRecord(w->ev_join, w->side));
+            LH_HIP(hipStreamWaitEvent(st, w->ev_join, 0));
         }
         return kOk;
     }

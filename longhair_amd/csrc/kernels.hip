@@ -798,6 +798,108 @@ __global__ void __launch_bounds__(1024) lh_inverse_jt_kernel(lh::InverseArgs a) 
     }
 }
 
+// ---- the computed jump with ONE copy of the table per kernel (round 3).  The wave's JO
+// outputs keep their accumulators in pinned registers v[40 + 8i .. 40 + 8i + 7] (LH_INV_IDX_BASE); the table
+// is written for output 0 and output i reaches it with GPR indexing on (SRC0 and DST
+// relative to index 8i): per row one asm statement builds the JO jump targets from the
+// coefficient bytes, enters the table JO times and returns through s[94:95]
+// (tools/gen_inv_jump.py render_indexed).  17 KiB of table code instead of JO copies.
+template <int JO>
+__device__ __forceinline__ void lh_mul_jump_idx(unsigned c0, unsigned c1, uint32_t (&a)[JO][8],
+                                                const uint32_t (&tl)[16], const uint32_t (&th)[16]) {
+    if constexpr (JO == 4) {
+        asm volatile(LH_INV_JUMPI4_ASM : LH_INV_JUMPI4_OUTS(a) : [c0] "s"(c0), [c1] "s"(c1), LH_INV_JUMPI_INS(tl, th)
+                     : "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "scc");
+    } else {
+        asm volatile(LH_INV_JUMPI8_ASM : LH_INV_JUMPI8_OUTS(a) : [c0] "s"(c0), [c1] "s"(c1), LH_INV_JUMPI_INS(tl, th)
+                     : "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "scc");
+    }
+}
+
+template <int JO, int MAXE, int BLK>
+__global__ void __launch_bounds__(1024) lh_inverse_ji_kernel(lh::InverseArgs a) {
+    static_assert(JO == 4 || JO == 8, "indexed table: 4 or 8 outputs per wave");
+    constexpr int TILE = BLK > 0 ? BLK : MAXE;
+    __shared__ uint32_t lv[TILE * 8 * 64];  // V rows, [row in tile][sub-block][lane]
+    const int nw = (int)(blockDim.x >> 6);
+    const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = (int)(threadIdx.x & 63);
+    const int cps = a.bytes >> 11;
+    const long long stripe = blockIdx.x / cps;
+    if (stripe >= a.stripes) return;  // workgroup-uniform
+    const uint8_t *pl = a.plan + stripe * a.plan_stride;
+    const int e = pl[0];
+    if (e == 0) return;  // workgroup-uniform
+    const int m = a.m, sub = a.bytes >> 3;
+    const lh::PlanView pv(pl, a.k, m, a.e_max);
+    const uint32_t rslot = lane < m ? (uint32_t)pv.rec_slot(lane) : 0xFFu;
+    const unsigned long long used = __ballot(rslot != 0xFFu);
+    uint8_t *base = a.blocks + stripe * a.stride + (int)(blockIdx.x % cps) * 256 + lane * 4;
+    const int nout = g < e ? (e - g + nw - 1) / nw : 0;  // outputs g, g + nw, ... (<= JO)
+    uint32_t cpk0 = 0, cpk1 = 0;  // lane r: this wave's coefficients for recovery row r
+    if (rslot != 0xFFu) {
+        const uint8_t *cf = pv.coef_ptr();
+#pragma unroll
+        for (int i = 0; i < JO; ++i)
+            if (i < nout) {
+                const uint32_t c = (uint32_t)cf[(g + i * nw) * m + lane] << (8 * (i & 3));
+                if (i < 4) cpk0 |= c;
+                else cpk1 |= c;
+            }
+    }
+    uint32_t acc[JO][8];
+#pragma unroll
+    for (int i = 0; i < JO; ++i)
+#pragma unroll
+        for (int y = 0; y < 8; ++y) acc[i][y] = 0;
+    unsigned long long todo = used;  // rows not yet staged
+    while (todo) {  // workgroup-uniform
+        {  // stage the next TILE used rows: wave g copies tile rows g, g + nw, ...
+            unsigned long long rest = todo;
+            for (int j = 0; rest && j < TILE; ++j, rest &= rest - 1) {
+                if (j % nw != g) continue;
+                const int r = __builtin_ctzll(rest);
+                const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)rslot, r);
+                const uint8_t *p = base + (long long)slot * a.bytes;
+                uint32_t v[8];
+#pragma unroll
+                for (int y = 0; y < 8; ++y) v[y] = *(const uint32_t *)(p + (long long)y * sub);
+#pragma unroll
+                for (int y = 0; y < 8; ++y) lv[(j * 8 + y) * 64 + lane] = v[y];
+            }
+        }
+        __syncthreads();  // this tile is in LDS
+        for (int j = 0; todo && j < TILE; ++j, todo &= todo - 1) {
+            if (nout == 0) continue;
+            const int r = __builtin_ctzll(todo);
+            uint32_t v[8];
+#pragma unroll
+            for (int y = 0; y < 8; ++y) v[y] = lv[(j * 8 + y) * 64 + lane];
+            uint32_t tl[16], th[16];
+            tl[0] = th[0] = 0;
+#pragma unroll
+            for (int q = 1; q < 16; ++q) {
+                const int low = __builtin_ctz(q), pre = q & (q - 1);
+                tl[q] = pre ? (tl[pre] ^ v[low]) : v[low];
+                th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];
+            }
+            // unused outputs (i >= nout) have coefficient 0: body 0 leaves them unchanged
+            const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)cpk0, r);
+            const uint32_t c1 = JO > 4 ? (uint32_t)__builtin_amdgcn_readlane((int)cpk1, r) : 0u;
+            lh_mul_jump_idx<JO>(c0, c1, acc, tl, th);
+        }
+        if (todo) __syncthreads();  // the tile is consumed before the next staging
+    }
+#pragma unroll
+    for (int i = 0; i < JO; ++i) {
+        if (i < nout) {
+            uint8_t *dst = base + (long long)pv.out_slot(g + i * nw) * a.bytes;
+#pragma unroll
+            for (int y = 0; y < 8; ++y) __builtin_nontemporal_store(acc[i][y], (uint32_t *)(dst + (long long)y * sub));
+        }
+    }
+}
+
 // OPW: outputs per wave (8, or 4: twice the waves, half the accumulators).
 template <int OPW>
 __global__ void __launch_bounds__(1024) lh_inverse_kernel(lh::InverseArgs a) {
@@ -915,6 +1017,28 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     if (jp == 2 && a.e_max <= 32) {
         hipLaunchKernelGGL((lh_inverse_jt_kernel<2, 32, 0>), grid, dim3(64u * (unsigned)((a.e_max + 1) / 2)), 0, st, a);
         note_launch("lh_inverse_jt_kernel<2,32,0>");
+        return hipGetLastError();
+    }
+    if (jp == 5 || jp == 9) {  // the single-table indexed jump, 4 or 8 outputs per wave
+        const int jo = jp == 5 ? 4 : 8;
+        const dim3 block(64u * (unsigned)((a.e_max + jo - 1) / jo));
+        if (jo == 4) {
+            if (a.e_max > 32) {
+                hipLaunchKernelGGL((lh_inverse_ji_kernel<4, 64, 0>), grid, block, 0, st, a);
+                note_launch("lh_inverse_ji_kernel<4,64,0>");
+            } else {
+                hipLaunchKernelGGL((lh_inverse_ji_kernel<4, 32, 16>), grid, block, 0, st, a);
+                note_launch("lh_inverse_ji_kernel<4,32,16>");
+            }
+        } else {
+            if (a.e_max > 32) {
+                hipLaunchKernelGGL((lh_inverse_ji_kernel<8, 64, 0>), grid, block, 0, st, a);
+                note_launch("lh_inverse_ji_kernel<8,64,0>");
+            } else {
+                hipLaunchKernelGGL((lh_inverse_ji_kernel<8, 32, 16>), grid, block, 0, st, a);
+                note_launch("lh_inverse_ji_kernel<8,32,16>");
+            }
+        }
         return hipGetLastError();
     }
     if (jp != 0 && jp != 2) {

@@ -76,6 +76,11 @@ PHASE_B = [
     ({"LONGHAIR_AMD_INV_JUMP": "2"}, 33, "lh_inverse_kernel<4>"),      # e_max > 32: Horner
     ({"LONGHAIR_AMD_INV_JUMP": "40"}, 32, "lh_inverse_jt_kernel<4,32,0>"),
     ({"LONGHAIR_AMD_INV_JUMP": "40"}, 33, "lh_inverse_jt_kernel<4,64,0>"),
+    # one table copy reached by GPR indexing, 4 or 8 outputs per wave
+    ({"LONGHAIR_AMD_INV_JUMP": "5"}, 32, "lh_inverse_ji_kernel<4,32,16>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "5"}, 33, "lh_inverse_ji_kernel<4,64,0>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "9"}, 32, "lh_inverse_ji_kernel<8,32,16>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "9"}, 33, "lh_inverse_ji_kernel<8,64,0>"),
 ]
 
 
@@ -261,3 +266,15 @@ def test_capture_never_allocates(lh):
     torch.cuda.synchronize()
     assert int((status != 0).sum()) == 0
     assert torch.equal(blocks, data) and torch.equal(rows[0].cpu(), torch.arange(k, dtype=torch.uint8))
+
+
+@pytest.mark.parametrize("overlap", ["0", "1"])
+def test_wide_decode_in_stripe_chunks(lh, oracle, monkeypatch, overlap):
+    """The split large-m decode in stripe chunks (phase A then phase B per chunk; with
+    LONGHAIR_AMD_WIDE_OVERLAP=1 phase B of one chunk on a side stream beside phase A of the
+    next): chunks of 3 stripes over 10, so chunk edges fall inside the batch."""
+    monkeypatch.setenv("LONGHAIR_AMD_WIDE_CHUNK", "3")
+    monkeypatch.setenv("LONGHAIR_AMD_WIDE_OVERLAP", overlap)
+    for k, m, nbytes in ((40, 20, 4096), (40, 33, 2048)):
+        enc, dec = roundtrip(lh, oracle, k, m, nbytes, 10, seed=k + m + int(overlap))
+        assert dec[:2] == ["lh_plan_kernel(closed form)", "lh_jit_decode_wide"], dec
