@@ -488,20 +488,18 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         const long long cps = wcfg.sub / (64 * wcfg.W);
         if ((long long)stripes * cps > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
         const unsigned threads = 64u * (unsigned)((m + wcfg.rows_per_wave - 1) / wcfg.rows_per_wave);
-        // Split decode in stripe chunks, phase A then phase B per chunk: phase A leaves V_r
-        // in the recovery slots and phase B overwrites those same slots with the outputs, so
-        // when a chunk's V (m blocks per stripe) fits the 256 MiB Infinity Cache, V is read
-        // back from the cache and its lines are rewritten before they reach HBM.
-        // LONGHAIR_AMD_WIDE_CHUNK = stripes per chunk (0 = whole batch at once).
+        // LONGHAIR_AMD_WIDE_CHUNK = N (knob, default: the whole batch): phase A then phase B
+        // per chunk of N stripes, so that a chunk's V could be read back from the 256 MiB
+        // Infinity Cache.  Measured slower at every chunk size (profiles/r3c_wide_chunk.txt:
+        // k128/m32 decode 3.94-3.98 ms whole, 4.17 at 1024 stripes, 6.7 at 128; k200/m56 0.60
+        // whole, 0.69 at 32): the per-launch tails cost more than the V traffic saved.
         long long chunk = stripes;
-        if (wk->cfg.win_split) {
-            const long long vbytes = (long long)m * bytes;  // V per stripe
-            chunk = std::max(1LL, (64LL << 20) / vbytes);
+        if (wk->cfg.win_split)
             if (const char *c = std::getenv("LONGHAIR_AMD_WIDE_CHUNK")) chunk = std::atoll(c) > 0 ? std::atoll(c) : stripes;
-        }
-        // LONGHAIR_AMD_WIDE_OVERLAP=1: phase B of chunk c runs on a side stream, overlapping
-        // phase A of chunk c + 1 (memory-bound) on the caller's stream (fork / join by events,
-        // so the call stays stream-ordered and capturable).
+        // LONGHAIR_AMD_WIDE_OVERLAP=1 (with chunks): phase B of chunk c runs on a side stream,
+        // overlapping phase A of chunk c + 1 on the caller's stream (fork / join by events, so
+        // the call stays stream-ordered and capturable).  Also measured slower than the whole
+        // batch (k128/m32 4.08-4.27 ms).
         bool overlap = false;
         if (wk->cfg.win_split && chunk < stripes) {
             const char *o = std::getenv("LONGHAIR_AMD_WIDE_OVERLAP");

@@ -713,97 +713,13 @@ __device__ __forceinline__ void lh_mul_jump(unsigned c, uint32_t (&a)[8], const 
                  : "s96", "s97", "s98", "scc");
 }
 
-// BLK > 0: the V rows are staged BLK at a time (a BLK x 2 KiB tile, more workgroups per
-// CU; a barrier after each block's compute before the next staging, and the outputs are
-// stored once every row has been staged).  BLK == 0: all rows at once (MAXE x 2 KiB).
-template <int JO, int MAXE, int BLK>
-__global__ void __launch_bounds__(1024) lh_inverse_jt_kernel(lh::InverseArgs a) {
-    static_assert(JO >= 1 && JO <= 4, "one coefficient byte per output in a 32-bit word");
-    constexpr int TILE = BLK > 0 ? BLK : MAXE;
-    __shared__ uint32_t lv[TILE * 8 * 64];  // V rows, [row in tile][sub-block][lane]
-    const int nw = (int)(blockDim.x >> 6);
-    const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int lane = (int)(threadIdx.x & 63);
-    const int cps = a.bytes >> 11;
-    const long long stripe = blockIdx.x / cps;
-    if (stripe >= a.stripes) return;  // workgroup-uniform
-    const uint8_t *pl = a.plan + stripe * a.plan_stride;
-    const int e = pl[0];
-    if (e == 0) return;  // workgroup-uniform
-    const int m = a.m, sub = a.bytes >> 3;
-    const lh::PlanView pv(pl, a.k, m, a.e_max);
-    const uint32_t rslot = lane < m ? (uint32_t)pv.rec_slot(lane) : 0xFFu;
-    const unsigned long long used = __ballot(rslot != 0xFFu);
-    uint8_t *base = a.blocks + stripe * a.stride + (int)(blockIdx.x % cps) * 256 + lane * 4;
-    const int nout = g < e ? (e - g + nw - 1) / nw : 0;  // outputs g, g + nw, ... (<= JO)
-    uint32_t cpk = 0;  // lane r: this wave's coefficients for recovery row r
-    if (rslot != 0xFFu) {
-        const uint8_t *cf = pv.coef_ptr();
-#pragma unroll
-        for (int i = 0; i < JO; ++i)
-            if (i < nout) cpk |= (uint32_t)cf[(g + i * nw) * m + lane] << (8 * i);
-    }
-    uint32_t acc[JO][8];
-#pragma unroll
-    for (int i = 0; i < JO; ++i)
-#pragma unroll
-        for (int y = 0; y < 8; ++y) acc[i][y] = 0;
-    unsigned long long todo = used;  // rows not yet staged
-    while (todo) {  // workgroup-uniform
-        {  // stage the next TILE used rows: wave g copies tile rows g, g + nw, ...
-            unsigned long long rest = todo;
-            for (int j = 0; rest && j < TILE; ++j, rest &= rest - 1) {
-                if (j % nw != g) continue;
-                const int r = __builtin_ctzll(rest);
-                const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)rslot, r);
-                const uint8_t *p = base + (long long)slot * a.bytes;
-                uint32_t v[8];
-#pragma unroll
-                for (int y = 0; y < 8; ++y) v[y] = *(const uint32_t *)(p + (long long)y * sub);
-#pragma unroll
-                for (int y = 0; y < 8; ++y) lv[(j * 8 + y) * 64 + lane] = v[y];
-            }
-        }
-        __syncthreads();  // this tile is in LDS
-        for (int j = 0; todo && j < TILE; ++j, todo &= todo - 1) {
-            if (nout == 0) continue;
-            const int r = __builtin_ctzll(todo);
-            uint32_t v[8];
-#pragma unroll
-            for (int y = 0; y < 8; ++y) v[y] = lv[(j * 8 + y) * 64 + lane];
-            uint32_t tl[16], th[16];
-            tl[0] = th[0] = 0;
-#pragma unroll
-            for (int q = 1; q < 16; ++q) {
-                const int low = __builtin_ctz(q), pre = q & (q - 1);
-                tl[q] = pre ? (tl[pre] ^ v[low]) : v[low];
-                th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];
-            }
-            const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane((int)cpk, r);
-#pragma unroll
-            for (int i = 0; i < JO; ++i)
-                if (i < nout) lh_mul_jump((cw >> (8 * i)) & 0xFFu, acc[i], tl, th);
-        }
-        if (todo) __syncthreads();  // the tile is consumed before the next staging
-    }
-    // Every row was staged (read) before the last tile's barrier: the recovery slots may be
-    // overwritten.
-#pragma unroll
-    for (int i = 0; i < JO; ++i) {
-        if (i < nout) {
-            uint8_t *dst = base + (long long)pv.out_slot(g + i * nw) * a.bytes;
-#pragma unroll
-            for (int y = 0; y < 8; ++y) __builtin_nontemporal_store(acc[i][y], (uint32_t *)(dst + (long long)y * sub));
-        }
-    }
-}
-
 // ---- the computed jump with ONE copy of the table per kernel (round 3).  The wave's JO
-// outputs keep their accumulators in pinned registers v[40 + 8i .. 40 + 8i + 7] (LH_INV_IDX_BASE); the table
-// is written for output 0 and output i reaches it with GPR indexing on (SRC0 and DST
-// relative to index 8i): per row one asm statement builds the JO jump targets from the
-// coefficient bytes, enters the table JO times and returns through s[94:95]
-// (tools/gen_inv_jump.py render_indexed).  17 KiB of table code instead of JO copies.
+// outputs keep their accumulators in pinned registers v[40 + 8i .. 40 + 8i + 7]
+// (LH_INV_IDX_BASE); the table is written for output 0 and output i reaches it with GPR
+// indexing on (SRC0 and DST relative to index 8i): per row one asm statement builds the JO
+// jump targets from the coefficient bytes, enters the table JO times and returns through
+// s[94:95] (tools/gen_inv_jump.py render_indexed).  17 KiB of table code instead of JO
+// copies.
 template <int JO>
 __device__ __forceinline__ void lh_mul_jump_idx(unsigned c0, unsigned c1, uint32_t (&a)[JO][8],
                                                 const uint32_t (&tl)[16], const uint32_t (&th)[16]) {
@@ -816,11 +732,20 @@ __device__ __forceinline__ void lh_mul_jump_idx(unsigned c0, unsigned c1, uint32
     }
 }
 
-template <int JO, int MAXE, int BLK>
-__global__ void __launch_bounds__(1024) lh_inverse_ji_kernel(lh::InverseArgs a) {
-    static_assert(JO == 4 || JO == 8, "indexed table: 4 or 8 outputs per wave");
+// Phase B by computed jump.  One workgroup per (stripe, 256-byte chunk of every
+// sub-block), ceil(e_max / JO) waves; wave g recovers outputs g, g + nw, ... (<= JO).  The
+// chunk's V rows are staged in an LDS tile BLK rows at a time (BLK == 0: all MAXE at once),
+// wave g copying tile rows g, g + nw, ...; per used row every wave builds the 16-entry
+// tables and multiplies by its coefficients (IDX: one table copy reached by GPR indexing,
+// JO = 4 or 8; else one inlined table per output, JO <= 4).  PFR > 0: the first PFR of the
+// wave's rows of the NEXT tile are loaded into registers before the current tile is
+// computed (their HBM latency overlaps the compute) and written to LDS after the tile's
+// closing barrier.  The outputs are stored once every row has been staged (read): they
+// land in the recovery slots, where V is.
+template <int JO, int MAXE, int BLK, int PFR, bool IDX>
+__device__ __forceinline__ void lh_inverse_body(const lh::InverseArgs &a, uint32_t *lv) {
+    static_assert(IDX ? (JO == 4 || JO == 8) : (JO >= 1 && JO <= 4), "outputs per wave");
     constexpr int TILE = BLK > 0 ? BLK : MAXE;
-    __shared__ uint32_t lv[TILE * 8 * 64];  // V rows, [row in tile][sub-block][lane]
     const int nw = (int)(blockDim.x >> 6);
     const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = (int)(threadIdx.x & 63);
@@ -852,23 +777,54 @@ __global__ void __launch_bounds__(1024) lh_inverse_ji_kernel(lh::InverseArgs a) 
     for (int i = 0; i < JO; ++i)
 #pragma unroll
         for (int y = 0; y < 8; ++y) acc[i][y] = 0;
+    auto row_ptr = [&](int r) {
+        const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)rslot, r);
+        return base + (long long)slot * a.bytes;
+    };
+    // Rows of the tile starting at `rest` that this wave stages: tile positions j = g, g + nw, ...
+    uint32_t pf[PFR > 0 ? PFR : 1][8];
+    auto prefetch = [&](unsigned long long rest) {
+        int q = 0;
+        for (int j = 0; rest && j < TILE && q < PFR; ++j, rest &= rest - 1) {
+            if (j % nw != g) continue;
+            const uint8_t *p = row_ptr(__builtin_ctzll(rest));
+#pragma unroll
+            for (int t = 0; t < (PFR > 0 ? PFR : 1); ++t)
+                if (t == q)
+#pragma unroll
+                    for (int y = 0; y < 8; ++y) pf[t][y] = *(const uint32_t *)(p + (long long)y * sub);
+            ++q;
+        }
+    };
+    if (PFR > 0) prefetch(used);
     unsigned long long todo = used;  // rows not yet staged
     while (todo) {  // workgroup-uniform
-        {  // stage the next TILE used rows: wave g copies tile rows g, g + nw, ...
+        {  // stage this tile: prefetched rows from registers, the wave's other rows loaded now
             unsigned long long rest = todo;
+            int q = 0;
             for (int j = 0; rest && j < TILE; ++j, rest &= rest - 1) {
                 if (j % nw != g) continue;
-                const int r = __builtin_ctzll(rest);
-                const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)rslot, r);
-                const uint8_t *p = base + (long long)slot * a.bytes;
                 uint32_t v[8];
+                if (PFR > 0 && q < PFR) {
 #pragma unroll
-                for (int y = 0; y < 8; ++y) v[y] = *(const uint32_t *)(p + (long long)y * sub);
+                    for (int t = 0; t < (PFR > 0 ? PFR : 1); ++t)
+                        if (t == q)
+#pragma unroll
+                            for (int y = 0; y < 8; ++y) v[y] = pf[t][y];
+                } else {
+                    const uint8_t *p = row_ptr(__builtin_ctzll(rest));
+#pragma unroll
+                    for (int y = 0; y < 8; ++y) v[y] = *(const uint32_t *)(p + (long long)y * sub);
+                }
+                ++q;
 #pragma unroll
                 for (int y = 0; y < 8; ++y) lv[(j * 8 + y) * 64 + lane] = v[y];
             }
         }
         __syncthreads();  // this tile is in LDS
+        unsigned long long next = todo;  // rows after this tile
+        for (int j = 0; next && j < TILE; ++j) next &= next - 1;
+        if (PFR > 0 && next) prefetch(next);  // in flight while this tile is computed
         for (int j = 0; todo && j < TILE; ++j, todo &= todo - 1) {
             if (nout == 0) continue;
             const int r = __builtin_ctzll(todo);
@@ -883,13 +839,21 @@ __global__ void __launch_bounds__(1024) lh_inverse_ji_kernel(lh::InverseArgs a) 
                 tl[q] = pre ? (tl[pre] ^ v[low]) : v[low];
                 th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];
             }
-            // unused outputs (i >= nout) have coefficient 0: body 0 leaves them unchanged
             const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)cpk0, r);
-            const uint32_t c1 = JO > 4 ? (uint32_t)__builtin_amdgcn_readlane((int)cpk1, r) : 0u;
-            lh_mul_jump_idx<JO>(c0, c1, acc, tl, th);
+            if constexpr (IDX) {
+                // unused outputs (i >= nout) have coefficient 0: body 0 leaves them unchanged
+                const uint32_t c1 = JO > 4 ? (uint32_t)__builtin_amdgcn_readlane((int)cpk1, r) : 0u;
+                lh_mul_jump_idx<JO>(c0, c1, acc, tl, th);
+            } else {
+#pragma unroll
+                for (int i = 0; i < JO; ++i)
+                    if (i < nout) lh_mul_jump((c0 >> (8 * i)) & 0xFFu, acc[i], tl, th);
+            }
         }
         if (todo) __syncthreads();  // the tile is consumed before the next staging
     }
+    // Every row was staged (read) before the last tile's barrier: the recovery slots may be
+    // overwritten.
 #pragma unroll
     for (int i = 0; i < JO; ++i) {
         if (i < nout) {
@@ -898,6 +862,20 @@ __global__ void __launch_bounds__(1024) lh_inverse_ji_kernel(lh::InverseArgs a) 
             for (int y = 0; y < 8; ++y) __builtin_nontemporal_store(acc[i][y], (uint32_t *)(dst + (long long)y * sub));
         }
     }
+}
+
+// One inlined table per output (JO <= 4 copies of 17 KiB).
+template <int JO, int MAXE, int BLK, int PFR>
+__global__ void __launch_bounds__(1024) lh_inverse_jt_kernel(lh::InverseArgs a) {
+    __shared__ uint32_t lv[(BLK > 0 ? BLK : MAXE) * 8 * 64];  // V rows, [row in tile][sub-block][lane]
+    lh_inverse_body<JO, MAXE, BLK, PFR, false>(a, lv);
+}
+
+// One table copy reached by GPR indexing (JO = 4 or 8).
+template <int JO, int MAXE, int BLK, int PFR>
+__global__ void __launch_bounds__(1024) lh_inverse_ji_kernel(lh::InverseArgs a) {
+    __shared__ uint32_t lv[(BLK > 0 ? BLK : MAXE) * 8 * 64];
+    lh_inverse_body<JO, MAXE, BLK, PFR, true>(a, lv);
 }
 
 // OPW: outputs per wave (8, or 4: twice the waves, half the accumulators).
@@ -1001,60 +979,55 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     const long long blocks = (long long)a.stripes * (a.bytes / 2048);
     if (blocks <= 0) return hipSuccess;
     if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-    // Phase-B kernel, knob LONGHAIR_AMD_INV_JUMP (profiles/r2_tune_split_decode.txt):
-    //    4 (default)  computed jump, 4 outputs per wave: e_max <= 32 stages the V rows 16 at
-    //                 a time (lh_inverse_jt_kernel<4,32,16>; k128/m32 decode 4.10 -> 3.84 ms
-    //                 against all 32 at once), e_max > 32 all at once (<4,64,0>; 16-row
-    //                 staging measured 2 % slower for k200/m56)
-    //   40            e_max <= 32 staged all at once (<4,32,0>); e_max > 32 as 4
-    //    2            two outputs per wave (<2,32,0>, 4.51 ms), e_max <= 32 only; larger
-    //                 e_max falls back to the Horner kernel
-    //    0            the Horner kernel lh_inverse_kernel, LONGHAIR_AMD_INV_OPW = 4 (default)
-    //                 or 8 outputs per wave (k128/m32 decode 4.24 against 4.12 ms)
+    // Phase-B kernel (profiles/r2_tune_split_decode.txt, r3 sessions):
+    //   LONGHAIR_AMD_INV_JUMP  4 (default) computed jump, one inlined table per output, 4
+    //                            outputs per wave
+    //                         40 as 4, e_max <= 32 staged all at once
+    //                          5 / 9  one table copy reached by GPR indexing, 4 / 8 outputs
+    //                            per wave
+    //                          2 two outputs per wave (e_max <= 32; larger: Horner)
+    //                          0 the Horner kernel lh_inverse_kernel, LONGHAIR_AMD_INV_OPW =
+    //                            4 (default) or 8 outputs per wave
+    //   LONGHAIR_AMD_INV_PF    rows of the next tile prefetched per wave (0 or 2, default 2)
+    //   LONGHAIR_AMD_INV_BLK   e_max > 32: rows per tile, 0 (all at once, default) or 16
+    // e_max <= 32 stages 16 rows per tile (32 KiB: k128/m32 decode 4.10 -> 3.84 ms against
+    // all 32 at once).
     const char *jpe = std::getenv("LONGHAIR_AMD_INV_JUMP");
     const int jp = jpe ? std::atoi(jpe) : 4;
+    const char *pfe = std::getenv("LONGHAIR_AMD_INV_PF");
+    const int pf = pfe ? (std::atoi(pfe) ? 2 : 0) : 2;
+    const char *ble = std::getenv("LONGHAIR_AMD_INV_BLK");
+    const int blk = ble && std::atoi(ble) == 16 ? 16 : 0;
     const dim3 grid((unsigned)blocks);
-    if (jp == 2 && a.e_max <= 32) {
-        hipLaunchKernelGGL((lh_inverse_jt_kernel<2, 32, 0>), grid, dim3(64u * (unsigned)((a.e_max + 1) / 2)), 0, st, a);
-        note_launch("lh_inverse_jt_kernel<2,32,0>");
-        return hipGetLastError();
-    }
-    if (jp == 5 || jp == 9) {  // the single-table indexed jump, 4 or 8 outputs per wave
-        const int jo = jp == 5 ? 4 : 8;
-        const dim3 block(64u * (unsigned)((a.e_max + jo - 1) / jo));
-        if (jo == 4) {
-            if (a.e_max > 32) {
-                hipLaunchKernelGGL((lh_inverse_ji_kernel<4, 64, 0>), grid, block, 0, st, a);
-                note_launch("lh_inverse_ji_kernel<4,64,0>");
-            } else {
-                hipLaunchKernelGGL((lh_inverse_ji_kernel<4, 32, 16>), grid, block, 0, st, a);
-                note_launch("lh_inverse_ji_kernel<4,32,16>");
-            }
-        } else {
-            if (a.e_max > 32) {
-                hipLaunchKernelGGL((lh_inverse_ji_kernel<8, 64, 0>), grid, block, 0, st, a);
-                note_launch("lh_inverse_ji_kernel<8,64,0>");
-            } else {
-                hipLaunchKernelGGL((lh_inverse_ji_kernel<8, 32, 16>), grid, block, 0, st, a);
-                note_launch("lh_inverse_ji_kernel<8,32,16>");
-            }
+    const bool small = a.e_max <= 32;
+#define LH_LAUNCH_INV(KERNEL, JO, MAXE, BLK, PF)                                                        \
+    do {                                                                                                \
+        hipLaunchKernelGGL((KERNEL<JO, MAXE, BLK, PF>), grid, dim3(64u * (unsigned)((a.e_max + JO - 1) / JO)), 0, \
+                           st, a);                                                                      \
+        note_launch(#KERNEL "<" #JO "," #MAXE "," #BLK "," #PF ">");                                     \
+        return hipGetLastError();                                                                       \
+    } while (0)
+    if (jp == 2 && small) LH_LAUNCH_INV(lh_inverse_jt_kernel, 2, 32, 0, 0);
+    if (jp == 40 && small) LH_LAUNCH_INV(lh_inverse_jt_kernel, 4, 32, 0, 0);
+    if (jp == 5 || jp == 9) {
+        if (jp == 5) {
+            if (small && pf) LH_LAUNCH_INV(lh_inverse_ji_kernel, 4, 32, 16, 2);
+            if (small) LH_LAUNCH_INV(lh_inverse_ji_kernel, 4, 32, 16, 0);
+            if (blk && pf) LH_LAUNCH_INV(lh_inverse_ji_kernel, 4, 64, 16, 2);
+            LH_LAUNCH_INV(lh_inverse_ji_kernel, 4, 64, 0, 0);
         }
-        return hipGetLastError();
+        if (small && pf) LH_LAUNCH_INV(lh_inverse_ji_kernel, 8, 32, 16, 2);
+        if (small) LH_LAUNCH_INV(lh_inverse_ji_kernel, 8, 32, 16, 0);
+        if (blk && pf) LH_LAUNCH_INV(lh_inverse_ji_kernel, 8, 64, 16, 2);
+        LH_LAUNCH_INV(lh_inverse_ji_kernel, 8, 64, 0, 0);
     }
     if (jp != 0 && jp != 2) {
-        const dim3 block(64u * (unsigned)((a.e_max + 3) / 4));
-        if (a.e_max > 32) {
-            hipLaunchKernelGGL((lh_inverse_jt_kernel<4, 64, 0>), grid, block, 0, st, a);
-            note_launch("lh_inverse_jt_kernel<4,64,0>");
-        } else if (jp == 40) {
-            hipLaunchKernelGGL((lh_inverse_jt_kernel<4, 32, 0>), grid, block, 0, st, a);
-            note_launch("lh_inverse_jt_kernel<4,32,0>");
-        } else {
-            hipLaunchKernelGGL((lh_inverse_jt_kernel<4, 32, 16>), grid, block, 0, st, a);
-            note_launch("lh_inverse_jt_kernel<4,32,16>");
-        }
-        return hipGetLastError();
+        if (small && pf) LH_LAUNCH_INV(lh_inverse_jt_kernel, 4, 32, 16, 2);
+        if (small) LH_LAUNCH_INV(lh_inverse_jt_kernel, 4, 32, 16, 0);
+        if (blk && pf) LH_LAUNCH_INV(lh_inverse_jt_kernel, 4, 64, 16, 2);
+        LH_LAUNCH_INV(lh_inverse_jt_kernel, 4, 64, 0, 0);
     }
+#undef LH_LAUNCH_INV
     const char *o = std::getenv("LONGHAIR_AMD_INV_OPW");
     const int opw = (o && std::atoi(o) == 8) ? 8 : 4;
     const unsigned threads = 64u * (unsigned)((a.e_max + opw - 1) / opw);

@@ -25,8 +25,8 @@ SMALL4 = ["lh_plan_small_kernel<4>", "lh_jit_decode"]
 SMALL8 = ["lh_plan_small_kernel<8>", "lh_jit_decode"]
 GENERIC_CF = ["lh_plan_kernel(closed form)", "lh_apply_generic_kernel", "lh_scatter_kernel"]
 GENERIC_S8 = ["lh_plan_small_kernel<8>", "lh_apply_generic_kernel", "lh_scatter_kernel"]
-WIDE16 = ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_jt_kernel<4,32,16>"]
-WIDE64 = ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_jt_kernel<4,64,0>"]
+WIDE16 = ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_jt_kernel<4,32,16,2>"]
+WIDE64 = ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_jt_kernel<4,64,0,0>"]
 
 # (id, k, m, bytes, stripes, env, encode kernels, decode kernels)
 BOUNDARIES = [
@@ -72,15 +72,22 @@ PHASE_B = [
     ({"LONGHAIR_AMD_INV_JUMP": "0", "LONGHAIR_AMD_INV_OPW": "8"}, 32, "lh_inverse_kernel<8>"),
     ({"LONGHAIR_AMD_INV_JUMP": "0"}, 33, "lh_inverse_kernel<4>"),
     ({"LONGHAIR_AMD_INV_JUMP": "0", "LONGHAIR_AMD_INV_OPW": "8"}, 33, "lh_inverse_kernel<8>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "2"}, 32, "lh_inverse_jt_kernel<2,32,0>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "2"}, 32, "lh_inverse_jt_kernel<2,32,0,0>"),
     ({"LONGHAIR_AMD_INV_JUMP": "2"}, 33, "lh_inverse_kernel<4>"),      # e_max > 32: Horner
-    ({"LONGHAIR_AMD_INV_JUMP": "40"}, 32, "lh_inverse_jt_kernel<4,32,0>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "40"}, 33, "lh_inverse_jt_kernel<4,64,0>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "40"}, 32, "lh_inverse_jt_kernel<4,32,0,0>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "40"}, 33, "lh_inverse_jt_kernel<4,64,0,0>"),
+    # the default kernel without the next-tile prefetch, and 16-row tiles above e_max 32
+    ({"LONGHAIR_AMD_INV_PF": "0"}, 32, "lh_inverse_jt_kernel<4,32,16,0>"),
+    ({"LONGHAIR_AMD_INV_BLK": "16"}, 33, "lh_inverse_jt_kernel<4,64,16,2>"),
     # one table copy reached by GPR indexing, 4 or 8 outputs per wave
-    ({"LONGHAIR_AMD_INV_JUMP": "5"}, 32, "lh_inverse_ji_kernel<4,32,16>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "5"}, 33, "lh_inverse_ji_kernel<4,64,0>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "9"}, 32, "lh_inverse_ji_kernel<8,32,16>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "9"}, 33, "lh_inverse_ji_kernel<8,64,0>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "5"}, 32, "lh_inverse_ji_kernel<4,32,16,2>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "5", "LONGHAIR_AMD_INV_PF": "0"}, 32, "lh_inverse_ji_kernel<4,32,16,0>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "5"}, 33, "lh_inverse_ji_kernel<4,64,0,0>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "5", "LONGHAIR_AMD_INV_BLK": "16"}, 33, "lh_inverse_ji_kernel<4,64,16,2>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "9"}, 32, "lh_inverse_ji_kernel<8,32,16,2>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "9", "LONGHAIR_AMD_INV_PF": "0"}, 32, "lh_inverse_ji_kernel<8,32,16,0>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "9"}, 33, "lh_inverse_ji_kernel<8,64,0,0>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "9", "LONGHAIR_AMD_INV_BLK": "16"}, 33, "lh_inverse_ji_kernel<8,64,16,2>"),
 ]
 
 
@@ -158,7 +165,7 @@ def test_selection_boundary(lh, oracle, monkeypatch, case):
 
 
 @pytest.mark.parametrize("env,m,kernel", PHASE_B,
-                         ids=[f"{'-'.join(v for v in e.values())}-m{m}" for e, m, _ in PHASE_B])
+                         ids=[f"{'-'.join(k[17:] + v for k, v in e.items())}-m{m}" for e, m, _ in PHASE_B])
 def test_phase_b_variant(lh, oracle, monkeypatch, env, m, kernel):
     """Every phase-B kernel of the split large-m decode against the oracle (k = 40, 2048-byte
     blocks, e_max = m), on both sides of e_max = 32."""
