@@ -15,6 +15,7 @@
 #include "field.hpp"
 
 extern "C" const char lh_jit_source[];
+extern "C" const char lh_inv_jump_source[];  // inv_jump.inc (blobs.cpp)
 
 namespace lh {
 
@@ -334,94 +335,59 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
         os << "}\n";
         return;
     }
-    // Phase B: coefficients are workgroup-uniform, so each coefficient bit is a scalar
-    // branch and only set bits cost XORs; V_r is doubled in place (B(2) in bit-sliced
-    // form: (v1..v7, v0^v1^v2^v7)).  (A nibble-windowed variant -- a 16-way uniform switch
-    // per output and nibble with XOR3-paired cases -- measured 1.2-1.3x slower.)
-    os << "#ifndef LH_PB_MASK  // masks: k128/m32 decode 7.0 ms against 6.5 ms with branches\n#define LH_PB_MASK 0\n#endif\n";
-    os << "#ifndef LH_PB_PAIR  // bits in pairs, XOR3 when both set: 7.2 ms against 6.2 (k128/m32 decode)\n#define LH_PB_PAIR 0\n#endif\n";
-    // (Register tables per V row indexed at run time -- s_set_gpr_idx_on / v_mov / off,
-    // 74 instructions per (output, row) -- measured slower: k128/m32 decode 5.89 vs 5.57 ms,
-    // profiles/r2_tune_pb_fr.txt.)
-    // The coefficients of the wave's 8 outputs for used row j sit packed in lane j
-    // (cpk0: outputs 0..3, cpk1: 4..7) and come back as SGPRs through v_readlane, and the
-    // next row's V is read from LDS while the current row is applied, so no LDS round
-    // trip sits between a row's coefficient bits and their branches.
+    // Phase B from the LDS tile of V (round 3): wave g recovers outputs g, g + NG, ... (at
+    // most 8: e <= m <= 8 NG) as D_{E_i} = sum_r B(coef[i][r]) V_r with the computed-jump
+    // multiply of kernels.hip (inv_jump.inc, one table copy reached by GPR indexing, the 8
+    // accumulators of each output pinned to v[40 + 8i ..]): per used row the wave reads V_r
+    // from LDS, builds the 16-entry XOR tables of its sub-blocks 0..3 / 4..7 and enters the
+    // table once per output.  (Round 2 did this by Horner over the coefficient bits, one
+    // scalar branch per bit: k128/m32 decode 5.88 ms against 4.77 for the split kernels.)
+    os << lh_inv_jump_source;
+    os << "__device__ __forceinline__ void lh_mul8(unsigned c0, unsigned c1, unsigned (&a)[8][8],\n"
+       << "    const unsigned (&tl)[16], const unsigned (&th)[16]) {\n"
+       << "  asm volatile(LH_INV_JUMPI8_ASM : LH_INV_JUMPI8_OUTS(a) : [c0] \"s\"(c0), [c1] \"s\"(c1),\n"
+       << "               LH_INV_JUMPI_INS(tl, th) : \"s88\", \"s89\", \"s90\", \"s91\", \"s92\", \"s93\", \"s94\",\n"
+       << "               \"s95\", \"s96\", \"s97\", \"scc\");\n}\n";
     os << "__device__ __forceinline__ void lh_phase_b(const int g, const int e, const int lane,\n"
-       << "    const unsigned int *__restrict__ lv, const unsigned char *__restrict__ cf,\n"
-       << "    const unsigned char *__restrict__ used, const int nu, const unsigned char *__restrict__ pl,\n"
-       << "    unsigned char *__restrict__ base) {\n"
-       << "  const unsigned int ur = lane < nu ? (unsigned int)used[lane] : 0u;  // row of used slot `lane`\n"
-       << "  for (int i0 = g * 8; i0 < e; i0 += " << 8 * NG << ") {  // outputs [i0, i0 + 8) of this wave\n"
-       << "    unsigned int cpk0 = 0, cpk1 = 0;\n"
-       << "    if (lane < nu) {\n"
-       << "#pragma unroll\n      for (int i = 0; i < 4; ++i) {\n"
-       << "        cpk0 |= (i0 + i < e ? (unsigned int)cf[(i0 + i) * " << c.m << " + ur] : 0u) << (8 * i);\n"
-       << "        cpk1 |= (i0 + 4 + i < e ? (unsigned int)cf[(i0 + 4 + i) * " << c.m << " + ur] : 0u) << (8 * i);\n"
-       << "      }\n    }\n"
-       << "    unsigned int acc[8][8];\n"
-       << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n#pragma unroll\n      for (int y = 0; y < 8; ++y) acc[i][y] = 0;\n"
-       << "    unsigned int v[8], vn[8];\n"
-       << "    {\n      const int r = __builtin_amdgcn_readlane((int)ur, 0);\n"
-       << "#pragma unroll\n      for (int y = 0; y < 8; ++y) vn[y] = lv[(r * 8 + y) * 64 + lane];\n    }\n"
-       << "    for (int j = 0; j < nu; ++j) {\n"
-       << "#pragma unroll\n      for (int y = 0; y < 8; ++y) v[y] = vn[y];\n"
-       << "      if (j + 1 < nu) {  // next row's V in flight\n"
-       << "        const int rn = __builtin_amdgcn_readlane((int)ur, j + 1);\n"
-       << "#pragma unroll\n        for (int y = 0; y < 8; ++y) vn[y] = lv[(rn * 8 + y) * 64 + lane];\n"
-       << "      }\n"
-       << "      const unsigned int c0 = (unsigned int)__builtin_amdgcn_readlane((int)cpk0, j);\n"
-       << "      const unsigned int c1 = (unsigned int)__builtin_amdgcn_readlane((int)cpk1, j);\n"
-       << "#if LH_PB_PAIR  // bits (2q, 2q + 1) of a coefficient together: both set -> one XOR3\n"
-       << "#pragma unroll\n      for (int q = 0; q < 4; ++q) {\n"
-       << "        unsigned int w[8];  // w = B(2) v: the ladder entry of bit 2q + 1\n"
-       << "        {\n          const unsigned int t7 = __builtin_amdgcn_bitop3_b32(v[0], v[1], v[2], 0x96) ^ v[7];\n"
-       << "#pragma unroll\n          for (int y = 0; y < 7; ++y) w[y] = v[y + 1];\n"
-       << "          w[7] = t7;\n        }\n"
-       << "#pragma unroll\n        for (int i = 0; i < 8; ++i) {\n"
-       << "          const unsigned int two = ((i < 4 ? c0 : c1) >> (8 * (i & 3) + 2 * q)) & 3u;\n"
-       << "          if (two == 3u) {\n"
-       << "#pragma unroll\n            for (int y = 0; y < 8; ++y) acc[i][y] = __builtin_amdgcn_bitop3_b32(acc[i][y], v[y], w[y], 0x96);\n"
-       << "          } else if (two == 1u) {\n"
-       << "#pragma unroll\n            for (int y = 0; y < 8; ++y) acc[i][y] ^= v[y];\n"
-       << "          } else if (two == 2u) {\n"
-       << "#pragma unroll\n            for (int y = 0; y < 8; ++y) acc[i][y] ^= w[y];\n"
-       << "          }\n        }\n"
-       << "        if (q < 3) {  // v = B(2) w: the entry of bit 2q + 2\n"
-       << "          const unsigned int t7 = __builtin_amdgcn_bitop3_b32(w[0], w[1], w[2], 0x96) ^ w[7];\n"
-       << "#pragma unroll\n          for (int y = 0; y < 7; ++y) v[y] = w[y + 1];\n"
-       << "          v[7] = t7;\n        }\n      }\n"
-       << "#else\n"
-       << "#pragma unroll\n      for (int t = 0; t < 8; ++t) {\n"
-       << "#pragma unroll\n        for (int i = 0; i < 8; ++i) {\n"
-       << "          const unsigned int bit = ((i < 4 ? c0 : c1) >> (8 * (i & 3) + t)) & 1u;\n"
-       << "#if LH_PB_MASK  // uniform 0 / ~0 mask per (output, bit): one v_bitop3 a ^ (v & m) per sub-row\n"
-       << "          const unsigned int msk = 0u - bit;\n"
-       << "#pragma unroll\n          for (int y = 0; y < 8; ++y) acc[i][y] = __builtin_amdgcn_bitop3_b32(acc[i][y], v[y], msk, 0x78);\n"
-       << "#else  // scalar branch per (output, bit): only set bits cost XORs; the XORs stay on the\n"
-       << "       // fall-through path (a clear bit costs one taken branch, a set bit none)\n"
-       << "          if (__builtin_expect(bit, 1))\n"
-       << "#pragma unroll\n            for (int y = 0; y < 8; ++y) acc[i][y] ^= v[y];\n"
-       << "#endif\n        }\n"
-       << "        if (t < 7) {\n"
-       << "          const unsigned int t7 = __builtin_amdgcn_bitop3_b32(v[0], v[1], v[2], 0x96) ^ v[7];\n"
-       << "#pragma unroll\n          for (int y = 0; y < 7; ++y) v[y] = v[y + 1];\n"
-       << "          v[7] = t7;\n        }\n      }\n"
-       << "#endif\n"
-       << "    }\n"
+       << "    const unsigned *__restrict__ lv, const unsigned char *__restrict__ pl, unsigned char *__restrict__ base) {\n"
+       << "  const int nout = g < e ? (e - g + " << NG - 1 << ") / " << NG << " : 0;  // outputs g, g + " << NG << ", ...\n"
+       << "  if (nout == 0) return;  // wave-uniform\n"
+       << "  const unsigned rs = lane < " << c.m << " ? (unsigned)pl[" << 16 + e_max + c.k << " + lane] : 0xFFu;\n"
+       << "  unsigned long long used = __ballot(rs != 0xFFu);  // recovery rows present, ascending\n"
+       << "  unsigned cpk0 = 0, cpk1 = 0;  // lane r: the wave's coefficients for row r\n"
+       << "  if (rs != 0xFFu) {\n"
        << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n"
-       << "      if (i0 + i < e) {\n"
-       << "        unsigned char *dst = base + (long long)pl[16 + i0 + i] * " << c.bytes << ";\n"
-       << "#pragma unroll\n        for (int y = 0; y < 8; ++y) lh_st(dst + y * " << c.sub << ", acc[i][y]);\n"
-       << "      }\n  }\n}\n";
+       << "      if (i < nout) {\n"
+       << "        const unsigned cb = (unsigned)pl[" << coef_off << " + (g + i * " << NG << ") * " << c.m
+       << " + lane] << (8 * (i & 3));\n"
+       << "        if (i < 4) cpk0 |= cb; else cpk1 |= cb;\n"
+       << "      }\n  }\n"
+       << "  unsigned acc[8][8];\n"
+       << "#pragma unroll\n  for (int i = 0; i < 8; ++i)\n#pragma unroll\n    for (int y = 0; y < 8; ++y) acc[i][y] = 0;\n"
+       << "  for (; used; used &= used - 1) {\n"
+       << "    const int r = __builtin_ctzll(used);\n"
+       << "    unsigned v[8];\n"
+       << "#pragma unroll\n    for (int y = 0; y < 8; ++y) v[y] = lv[(r * 8 + y) * 64 + lane];\n"
+       << "    unsigned tl[16], th[16];\n"
+       << "    tl[0] = th[0] = 0;\n"
+       << "#pragma unroll\n    for (int q = 1; q < 16; ++q) {\n"
+       << "      const int low = __builtin_ctz(q), pre = q & (q - 1);\n"
+       << "      tl[q] = pre ? (tl[pre] ^ v[low]) : v[low];\n"
+       << "      th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];\n"
+       << "    }\n"
+       << "    lh_mul8((unsigned)__builtin_amdgcn_readlane((int)cpk0, r), (unsigned)__builtin_amdgcn_readlane((int)cpk1, r),\n"
+       << "            acc, tl, th);\n"
+       << "  }\n"
+       << "#pragma unroll\n  for (int i = 0; i < 8; ++i)\n"
+       << "    if (i < nout) {\n"
+       << "      unsigned char *dst = base + (long long)pl[16 + g + i * " << NG << "] * " << c.bytes << ";\n"
+       << "#pragma unroll\n      for (int y = 0; y < 8; ++y) lh_st(dst + y * " << c.sub << ", acc[i][y]);\n"
+       << "    }\n}\n";
     os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
        << "lh_jit_decode_wide(unsigned char *__restrict__ blocks, long long stride,\n"
        << "                   const unsigned char *__restrict__ plan, long long plan_stride,\n"
        << "                   const unsigned char *__restrict__ zero_page, int stripes) {\n"
        << "  __shared__ unsigned int lv[" << c.m * 8 * 64 << "];\n"
-       << "  __shared__ unsigned char cf[" << e_max * c.m << "];\n"
-       << "  __shared__ unsigned char used[" << c.m << "];\n"
-       << "  __shared__ int n_used;\n"
        << "  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
        << "  const int lane = threadIdx.x & 63;\n"
        << "  const long long stripe = blockIdx.x / " << CPS << ";\n"
@@ -429,17 +395,10 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
        << "  const unsigned char *pl = plan + stripe * plan_stride;\n"
        << "  const int e = pl[0];\n"
        << "  if (e == 0) return;\n"
-       << "  for (int q = threadIdx.x; q < e * " << c.m << "; q += blockDim.x) cf[q] = pl[" << coef_off << " + q];\n"
        << "  unsigned int slv[LH_NQ];\n"
        << "#pragma unroll\n  for (int q = 0; q < LH_NQ; ++q) {\n"
        << "    const int i = q * 64 + lane;\n"
        << "    slv[q] = i < " << km << " ? (unsigned int)pl[" << 16 + e_max << " + i] : 0xFFu;\n"
-       << "  }\n"
-       << "  if (g == 0) {  // recovery rows present in the stripe = the coefficient columns in use\n"
-       << "    const bool u = lane < " << c.m << " && pl[" << 16 + e_max + c.k << " + lane] != 0xFFu;\n"
-       << "    const unsigned long long bal = __ballot(u);\n"
-       << "    if (u) used[__builtin_popcountll(bal & ((1ull << lane) - 1))] = (unsigned char)lane;\n"
-       << "    if (lane == 0) n_used = (int)__builtin_popcountll(bal);\n"
        << "  }\n"
        << "  const int p = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << " + lane * " << c.W << ";\n"
        << "  unsigned char *b = blocks + stripe * stride + p;\n"
@@ -452,9 +411,9 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
         dargs = "(b, z, slv, lv, sb, zb)";
     }
     for (int g = 0; g < NG; ++g) os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << dargs << ";\n";
-    os << "  __syncthreads();\n"
+    os << "  __syncthreads();  // V of every row in LDS; every slot read\n"
        << "#ifndef LH_PB_SKIP  // timing probe only (tools/time_probe.py): phase A alone\n"
-       << "  lh_phase_b(g, e, lane, lv, cf, used, n_used, pl, b);\n"
+       << "  lh_phase_b(g, e, lane, lv, pl, b);\n"
        << "#endif\n"
        << "}\n";
 }

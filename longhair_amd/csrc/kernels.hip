@@ -980,22 +980,26 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     if (blocks <= 0) return hipSuccess;
     if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
     // Phase-B kernel (profiles/r2_tune_split_decode.txt, r3 sessions):
-    //   LONGHAIR_AMD_INV_JUMP  4 (default) computed jump, one inlined table per output, 4
-    //                            outputs per wave
+    //   LONGHAIR_AMD_INV_JUMP  default: e_max <= 32 as 9, above as 4
+    //                          4 computed jump, one inlined table per output, 4 outputs per
+    //                            wave
     //                         40 as 4, e_max <= 32 staged all at once
     //                          5 / 9  one table copy reached by GPR indexing, 4 / 8 outputs
     //                            per wave
     //                          2 two outputs per wave (e_max <= 32; larger: Horner)
     //                          0 the Horner kernel lh_inverse_kernel, LONGHAIR_AMD_INV_OPW =
     //                            4 (default) or 8 outputs per wave
-    //   LONGHAIR_AMD_INV_PF    rows of the next tile prefetched per wave (0 or 2, default 2)
+    //   LONGHAIR_AMD_INV_PF    rows of the next tile prefetched per wave (0, default, or 2)
     //   LONGHAIR_AMD_INV_BLK   e_max > 32: rows per tile, 0 (all at once, default) or 16
     // e_max <= 32 stages 16 rows per tile (32 KiB: k128/m32 decode 4.10 -> 3.84 ms against
-    // all 32 at once).
+    // all 32 at once).  Measured on one box (profiles/r3d_phase_b.txt, decode incl. planner
+    // and phase A): k128/m32 jt<4> 3.97-3.99 ms, indexed JO 8 3.78-3.80, JO 4 with
+    // prefetch 4.80; prefetch costs 0.8 ms on jt<4> (registers); k200/m56 jt<4,64,0> 0.606,
+    // indexed JO 8 0.634-0.672, 16-row tiles 0.64-0.72.
     const char *jpe = std::getenv("LONGHAIR_AMD_INV_JUMP");
-    const int jp = jpe ? std::atoi(jpe) : 4;
+    const int jp = jpe ? std::atoi(jpe) : (a.e_max <= 32 ? 9 : 4);
     const char *pfe = std::getenv("LONGHAIR_AMD_INV_PF");
-    const int pf = pfe ? (std::atoi(pfe) ? 2 : 0) : 2;
+    const int pf = pfe && std::atoi(pfe) ? 2 : 0;
     const char *ble = std::getenv("LONGHAIR_AMD_INV_BLK");
     const int blk = ble && std::atoi(ble) == 16 ? 16 : 0;
     const dim3 grid((unsigned)blocks);
@@ -1007,26 +1011,29 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
         note_launch(#KERNEL "<" #JO "," #MAXE "," #BLK "," #PF ">");                                     \
         return hipGetLastError();                                                                       \
     } while (0)
+#define LH_LAUNCH_INV_PF(KERNEL, JO, MAXE, BLK)                 \
+    do {                                                        \
+        if (pf) LH_LAUNCH_INV(KERNEL, JO, MAXE, BLK, 2);         \
+        LH_LAUNCH_INV(KERNEL, JO, MAXE, BLK, 0);                 \
+    } while (0)
     if (jp == 2 && small) LH_LAUNCH_INV(lh_inverse_jt_kernel, 2, 32, 0, 0);
     if (jp == 40 && small) LH_LAUNCH_INV(lh_inverse_jt_kernel, 4, 32, 0, 0);
-    if (jp == 5 || jp == 9) {
-        if (jp == 5) {
-            if (small && pf) LH_LAUNCH_INV(lh_inverse_ji_kernel, 4, 32, 16, 2);
-            if (small) LH_LAUNCH_INV(lh_inverse_ji_kernel, 4, 32, 16, 0);
-            if (blk && pf) LH_LAUNCH_INV(lh_inverse_ji_kernel, 4, 64, 16, 2);
-            LH_LAUNCH_INV(lh_inverse_ji_kernel, 4, 64, 0, 0);
-        }
-        if (small && pf) LH_LAUNCH_INV(lh_inverse_ji_kernel, 8, 32, 16, 2);
-        if (small) LH_LAUNCH_INV(lh_inverse_ji_kernel, 8, 32, 16, 0);
-        if (blk && pf) LH_LAUNCH_INV(lh_inverse_ji_kernel, 8, 64, 16, 2);
+    if (jp == 5) {
+        if (small) LH_LAUNCH_INV_PF(lh_inverse_ji_kernel, 4, 32, 16);
+        if (blk) LH_LAUNCH_INV_PF(lh_inverse_ji_kernel, 4, 64, 16);
+        LH_LAUNCH_INV(lh_inverse_ji_kernel, 4, 64, 0, 0);
+    }
+    if (jp == 9) {
+        if (small) LH_LAUNCH_INV_PF(lh_inverse_ji_kernel, 8, 32, 16);
+        if (blk) LH_LAUNCH_INV_PF(lh_inverse_ji_kernel, 8, 64, 16);
         LH_LAUNCH_INV(lh_inverse_ji_kernel, 8, 64, 0, 0);
     }
     if (jp != 0 && jp != 2) {
-        if (small && pf) LH_LAUNCH_INV(lh_inverse_jt_kernel, 4, 32, 16, 2);
-        if (small) LH_LAUNCH_INV(lh_inverse_jt_kernel, 4, 32, 16, 0);
-        if (blk && pf) LH_LAUNCH_INV(lh_inverse_jt_kernel, 4, 64, 16, 2);
+        if (small) LH_LAUNCH_INV_PF(lh_inverse_jt_kernel, 4, 32, 16);
+        if (blk) LH_LAUNCH_INV_PF(lh_inverse_jt_kernel, 4, 64, 16);
         LH_LAUNCH_INV(lh_inverse_jt_kernel, 4, 64, 0, 0);
     }
+#undef LH_LAUNCH_INV_PF
 #undef LH_LAUNCH_INV
     const char *o = std::getenv("LONGHAIR_AMD_INV_OPW");
     const int opw = (o && std::atoi(o) == 8) ? 8 : 4;

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round-3 session E: the fused large-m decode (phase A into an LDS tile of V, phase B by the
+# indexed computed jump) against the split kernels, after their parity tests.
+set -o pipefail
+cd "$(dirname "$0")/.."
+OUT=gpurun_out/${1:-r3e}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_boundaries.py tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread -k "phase_b or selection or chunks or wide" > "$OUT/pytest_pb.txt" 2>&1 || { tail -40 "$OUT/pytest_pb.txt"; exit 1; }
+tail -1 "$OUT/pytest_pb.txt"
+run() {  # name cfg env...
+  local name=$1 cfg=$2; shift 2
+  env "$@" timeout -k 10 300 python bench.py --config $cfg --steps 10 --warmup 2 --cpu-baseline off --dropin-calls 0 --pcie off > "$OUT/b_${cfg}_$name.json" 2> "$OUT/b_${cfg}_$name.err" || { tail -20 "$OUT/b_${cfg}_$name.err"; exit 1; }
+  python3 -c "import json; d=json.load(open('$OUT/b_${cfg}_$name.json')); print('$cfg $name', d['value'], d['kernels']['encode']['ms'], d['kernels']['decode']['ms'], d['kernels']['decode']['kernel'])" | tee -a "$OUT/summary.txt"
+}
+for rep in 1 2; do
+  run split k128m32
+  run fused k128m32 LONGHAIR_AMD_WIN_SPLIT=0
+  run split k200m56
+  run fused k200m56 LONGHAIR_AMD_WIN_SPLIT=0
+done
