@@ -141,6 +141,18 @@ def per_rank(world, rank, value, dry=False):
 
 
 # ------------------------------------------------------------------------ workload
+def random_erasures(k, m, stripes, seed):
+    """erasures="random": per stripe (e, the e recovery rows used), e uniform in
+    [1, min(k, m)] -- a CPU generator, so tools can replay a workload's erasure counts."""
+    import torch
+    rng = torch.Generator().manual_seed(seed)
+    out = []
+    for _ in range(stripes):
+        e = int(torch.randint(1, min(k, m) + 1, (1,), generator=rng))
+        out.append((e, torch.randperm(m, generator=rng)[:e]))
+    return out
+
+
 def make_workload(k, m, nbytes, stripes, seed, erasures="max"):
     """Data X [S, k, bytes] and a decode buffer D [S, k, bytes] whose first slots hold the
     surviving originals of each stripe in a shuffled order and whose last e_s slots
@@ -163,13 +175,10 @@ def make_workload(k, m, nbytes, stripes, seed, erasures="max"):
         D[:, : k - e] = torch.gather(X, 1, keep.unsqueeze(-1).expand(-1, -1, nbytes))
         rows0 = torch.cat([keep, torch.arange(k, k + e, device="cuda").expand(stripes, e)], dim=1)
         return X, D, rows0.to(torch.uint8).contiguous(), None
-    rng = torch.Generator().manual_seed(seed)
     rows0 = torch.empty((stripes, k), dtype=torch.long)
     dst, src = [], []
     perm_c = perm.cpu()
-    for s in range(stripes):
-        e = int(torch.randint(1, min(k, m) + 1, (1,), generator=rng))
-        rec_rows = torch.randperm(m, generator=rng)[:e]
+    for s, (e, rec_rows) in enumerate(random_erasures(k, m, stripes, seed)):
         rows0[s, : k - e] = perm_c[s, : k - e]
         rows0[s, k - e:] = k + rec_rows
         for j in range(e):

@@ -234,12 +234,15 @@ def batch_path(k, m, block_bytes, decode=False):
 
 
 def _phase_b_kernel(k, m):
-    """Phase-B kernel of the split large-m decode (kernels.hip launch_inverse)."""
+    """Phase-B kernel of the split large-m decode (kernels.hip launch_inverse); the
+    authoritative record of a call is last_launch()."""
     if os.environ.get("LONGHAIR_AMD_WIN_SPLIT") == "0":
         return []
-    jump = os.environ.get("LONGHAIR_AMD_INV_JUMP", "4")
-    horner = jump == "0" or (jump == "2" and min(k, m) > 32)
-    return ["lh_inverse_kernel" if horner else "lh_inverse_jt_kernel"]
+    e_max = min(k, m)
+    jump = os.environ.get("LONGHAIR_AMD_INV_JUMP", "9" if e_max <= 32 else "4")
+    if jump == "0" or (jump == "2" and e_max > 32):
+        return ["lh_inverse_kernel"]
+    return ["lh_inverse_ji_kernel" if jump in ("5", "9") else "lh_inverse_jt_kernel"]
 
 
 def kernel_names(k, m, block_bytes):

@@ -33,7 +33,13 @@ def main():
     k, m, nbytes, stripes, erasures = bench.CONFIGS[cfg]
     f = per_kernel(os.path.join(out_dir, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     w = per_kernel(os.path.join(out_dir, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
-    e = min(k, m)  # decode bytes for e = min(k, m); random-erasure configs write fewer blocks
+    # decode bytes: read k slots, write e blocks per stripe -- e = min(k, m), or for the
+    # random-erasure configs the mean e of tools/prof_kernels.py's workload (seed 3)
+    if erasures == "random":
+        es = [e for e, _ in bench.random_erasures(k, m, stripes, 3)]
+        e = sum(es) / len(es)
+    else:
+        e = min(k, m)
     alg = {"encode": (k + m) * nbytes * stripes, "decode": (k + e) * nbytes * stripes}
     res = {"config": cfg, "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) of "
                                     f"tools/prof_kernels.py {cfg}",
