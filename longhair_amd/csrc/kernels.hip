@@ -781,42 +781,45 @@ __device__ __forceinline__ void lh_inverse_body(const lh::InverseArgs &a, uint32
         const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)rslot, r);
         return base + (long long)slot * a.bytes;
     };
-    // Rows of the tile starting at `rest` that this wave stages: tile positions j = g, g + nw, ...
+    // This wave stages tile positions j = g, g + nw, ... of each tile.  With PFR > 0 the rows
+    // at positions g + q nw (q < PFR) of the next tile are loaded into pf[q] before the
+    // current tile is computed: unconditional loads into fixed registers (a position past the
+    // tile's rows reloads the tile's first row, unused), so nothing waits for them before the
+    // staging writes.
     uint32_t pf[PFR > 0 ? PFR : 1][8];
+    auto tile_row = [&](unsigned long long rest, int j) {  // row at tile position j, or -1
+        for (int t = 0; t < j && rest; ++t) rest &= rest - 1;
+        return rest ? __builtin_ctzll(rest) : -1;
+    };
     auto prefetch = [&](unsigned long long rest) {
-        int q = 0;
-        for (int j = 0; rest && j < TILE && q < PFR; ++j, rest &= rest - 1) {
-            if (j % nw != g) continue;
-            const uint8_t *p = row_ptr(__builtin_ctzll(rest));
 #pragma unroll
-            for (int t = 0; t < (PFR > 0 ? PFR : 1); ++t)
-                if (t == q)
+        for (int q = 0; q < (PFR > 0 ? PFR : 1); ++q) {
+            const int j = g + q * nw, r = j < TILE ? tile_row(rest, j) : -1;
+            const uint8_t *p = row_ptr(r >= 0 ? r : __builtin_ctzll(rest));
 #pragma unroll
-                    for (int y = 0; y < 8; ++y) pf[t][y] = *(const uint32_t *)(p + (long long)y * sub);
-            ++q;
+            for (int y = 0; y < 8; ++y) pf[q][y] = *(const uint32_t *)(p + (long long)y * sub);
         }
     };
     if (PFR > 0) prefetch(used);
     unsigned long long todo = used;  // rows not yet staged
     while (todo) {  // workgroup-uniform
         {  // stage this tile: prefetched rows from registers, the wave's other rows loaded now
-            unsigned long long rest = todo;
-            int q = 0;
-            for (int j = 0; rest && j < TILE; ++j, rest &= rest - 1) {
-                if (j % nw != g) continue;
-                uint32_t v[8];
-                if (PFR > 0 && q < PFR) {
+            int nrows = 0;  // rows in this tile
+            for (unsigned long long rest = todo; rest && nrows < TILE; rest &= rest - 1) ++nrows;
+            if (PFR > 0) {
 #pragma unroll
-                    for (int t = 0; t < (PFR > 0 ? PFR : 1); ++t)
-                        if (t == q)
+                for (int q = 0; q < (PFR > 0 ? PFR : 1); ++q) {
+                    const int j = g + q * nw;
+                    if (j < nrows)
 #pragma unroll
-                            for (int y = 0; y < 8; ++y) v[y] = pf[t][y];
-                } else {
-                    const uint8_t *p = row_ptr(__builtin_ctzll(rest));
-#pragma unroll
-                    for (int y = 0; y < 8; ++y) v[y] = *(const uint32_t *)(p + (long long)y * sub);
+                        for (int y = 0; y < 8; ++y) lv[(j * 8 + y) * 64 + lane] = pf[q][y];
                 }
-                ++q;
+            }
+            for (int j = g + PFR * nw; j < nrows; j += nw) {
+                const uint8_t *p = row_ptr(tile_row(todo, j));
+                uint32_t v[8];
+#pragma unroll
+                for (int y = 0; y < 8; ++y) v[y] = *(const uint32_t *)(p + (long long)y * sub);
 #pragma unroll
                 for (int y = 0; y < 8; ++y) lv[(j * 8 + y) * 64 + lane] = v[y];
             }
