@@ -80,6 +80,9 @@ def parse(argv=None):
                     help="PCIe-inclusive leg: cauchy_256_*_host_batch from pinned host memory on every rank")
     ap.add_argument("--pcie-stripes", type=int, default=0,
                     help="stripes per rank in the PCIe leg (default: the workload, capped at ~640 MB)")
+    ap.add_argument("--align", type=int, default=0,
+                    help="decode buffer: pad the stripe stride so the recovery slots start on this byte "
+                         "boundary (0 = contiguous [S, k, bytes])")
     ap.add_argument("--dry-run", action="store_true", help="no HIP work: CPU stand-in step over gloo")
     return ap.parse_args(argv)
 
@@ -153,7 +156,21 @@ def random_erasures(k, m, stripes, seed):
     return out
 
 
-def make_workload(k, m, nbytes, stripes, seed, erasures="max"):
+def decode_buffer(k, m, nbytes, stripes, align):
+    """The decode buffer D [S, k, bytes]: contiguous (align 0), or with a padded stripe
+    stride (a multiple of `align`) and a leading offset chosen so that every stripe's
+    recovery slots k - m .. k - 1 -- the blocks the encode writes and the decode overwrites
+    -- start on an `align`-byte boundary.  Returns (D, stripe stride)."""
+    import torch
+    if not align or ((k - m) * nbytes % align == 0 and k * nbytes % align == 0):
+        return torch.empty((stripes, k, nbytes), dtype=torch.uint8, device="cuda"), k * nbytes
+    stride = -(-k * nbytes // align) * align
+    off = (-(k - m) * nbytes) % align
+    buf = torch.empty(off + stride * stripes, dtype=torch.uint8, device="cuda")
+    return buf[off:].as_strided((stripes, k, nbytes), (stride, nbytes, 1)), stride
+
+
+def make_workload(k, m, nbytes, stripes, seed, erasures="max", align=0):
     """Data X [S, k, bytes] and a decode buffer D [S, k, bytes] whose first slots hold the
     surviving originals of each stripe in a shuffled order and whose last e_s slots
     receive recovery blocks; rows0 = the matching Block.row bytes.
@@ -167,7 +184,7 @@ def make_workload(k, m, nbytes, stripes, seed, erasures="max"):
     g = torch.Generator(device="cuda").manual_seed(seed)
     X = torch.randint(0, 256, (stripes, k, nbytes), dtype=torch.uint8, device="cuda", generator=g)
     perm = torch.argsort(torch.rand(stripes, k, device="cuda", generator=g), dim=1)
-    D = torch.empty_like(X)
+    D, _ = decode_buffer(k, m, nbytes, stripes, align if erasures == "max" else 0)
     if erasures == "max":
         e = min(k, m)
         assert e == m, "erasures='max' writes all m recovery rows into the decode buffer"
@@ -489,7 +506,8 @@ def main():
         import longhair_amd as lh
         assert lh.cauchy_256_init() == 0, lh.lib().cauchy_256_last_error()
         lh.prepare(k, m, nbytes, stripes)
-        X, D, rows0, rec_index = make_workload(k, m, nbytes, stripes, seed=1234 + lo, erasures=erasures)
+        X, D, rows0, rec_index = make_workload(k, m, nbytes, stripes, seed=1234 + lo, erasures=erasures,
+                                               align=args.align)
         e_mean = float((rows0 >= k).sum()) / max(1, stripes)
         if rec_index is None:
             rec_view = D[:, k - m:]     # the encode writes straight into D's recovery slots
@@ -564,6 +582,7 @@ def main():
         "config": {"workload": workload, "k": k, "m": m, "block_bytes": nbytes,
                    "stripes_per_gpu": stripes if scaling == "weak" else None,
                    "global_stripes": total_stripes,
+                   "decode_buffer_stripe_stride": None if dry else int(D.stride(0)),
                    "parallelism": f"stripes sharded over {world} rank(s), no collective"},
         "per_gpu_GBps": per_gpu,
         "node_GBps": round(value, 2),
