@@ -116,6 +116,8 @@ def test_inv_jump_table_is_generated():
     spec.loader.exec_module(gen)
     committed = open(os.path.join(REPO, "longhair_amd", "csrc", "inv_jump.inc")).read()
     assert committed == gen.render()
-    # 256 bodies of 8 v_bitop3_b32 + a branch: the fixed 68-byte stride the jump assumes
-    assert committed.count("v_bitop3_b32") == 256 * 8
+    # three tables (per-output copies; indexed for 4 and for 8 outputs) of 256 bodies of
+    # 8 v_bitop3_b32 + a branch or return: the fixed 68-byte stride the jump assumes
+    assert committed.count("v_bitop3_b32") == 3 * 256 * 8
     assert committed.count("s_branch 3f") == 256
+    assert committed.count("s_setpc_b64 s[94:95]") == 2 * 256
