@@ -156,17 +156,24 @@ def random_erasures(k, m, stripes, seed):
     return out
 
 
-def decode_buffer(k, m, nbytes, stripes, align):
-    """The decode buffer D [S, k, bytes]: contiguous (align 0), or with a padded stripe
-    stride (a multiple of `align`) and a leading offset chosen so that every stripe's
-    recovery slots k - m .. k - 1 -- the blocks the encode writes and the decode overwrites
-    -- start on an `align`-byte boundary.  Returns (D, stripe stride)."""
-    import torch
+def aligned_layout(k, m, nbytes, align):
+    """(offset, stripe stride) of a decode buffer whose every stripe's recovery slots
+    k - m .. k - 1 -- the blocks the encode writes and the decode overwrites -- start on an
+    `align`-byte boundary: the stride is k * bytes rounded up to a multiple of `align`, the
+    buffer starts `offset` bytes into an aligned allocation.  align 0: (0, k * bytes)."""
     if not align or ((k - m) * nbytes % align == 0 and k * nbytes % align == 0):
-        return torch.empty((stripes, k, nbytes), dtype=torch.uint8, device="cuda"), k * nbytes
-    stride = -(-k * nbytes // align) * align
-    off = (-(k - m) * nbytes) % align
-    buf = torch.empty(off + stride * stripes, dtype=torch.uint8, device="cuda")
+        return 0, k * nbytes
+    return (-(k - m) * nbytes) % align, -(-k * nbytes // align) * align
+
+
+def decode_buffer(k, m, nbytes, stripes, align):
+    """The decode buffer D [S, k, bytes]: contiguous, or laid out by
+    aligned_layout.  Returns (D, stripe stride)."""
+    import torch
+    off, stride = aligned_layout(k, m, nbytes, align)
+    if stride == k * nbytes:
+        return torch.empty((stripes, k, nbytes), dtype=torch.uint8, device="cuda"), stride
+    buf = torch.empty(off + stride * stripes, dtype=torch.uint8, device="cuda")  # 256-B aligned
     return buf[off:].as_strided((stripes, k, nbytes), (stride, nbytes, 1)), stride
 
 

@@ -143,3 +143,19 @@ def test_cpu_baseline_uses_the_workload_patterns():
     out = bench.cpu_baseline(k, m, nbytes, 0.3, stripes=10, patterns=rows)
     assert out["ok"], out
     assert f"mean e {e_of.mean():.1f}" in out["sample"]
+
+
+@pytest.mark.parametrize("k,m,nbytes,align", [(29, 4, 1296, 128), (29, 4, 1296, 64), (17, 6, 520, 128),
+                                              (128, 32, 8192, 128), (29, 4, 1296, 0)])
+def test_bench_aligned_decode_buffer_layout(k, m, nbytes, align):
+    """bench.py --align: every stripe's recovery slots start on an `align`-byte boundary, the
+    stripe stride holds the k slots and is a multiple of `align`, the padding stays small."""
+    import bench
+    off, stride = bench.aligned_layout(k, m, nbytes, align)
+    assert stride >= k * nbytes and off >= 0
+    if not align:
+        assert (off, stride) == (0, k * nbytes)
+        return
+    assert stride % align == 0 and stride - k * nbytes < align and off < align
+    for s in range(5):
+        assert (off + s * stride + (k - m) * nbytes) % align == 0
