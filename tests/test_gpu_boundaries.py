@@ -290,3 +290,41 @@ def test_wide_decode_in_stripe_chunks(lh, oracle, monkeypatch, overlap):
     for k, m, nbytes in ((40, 20, 4096), (40, 33, 2048)):
         enc, dec = roundtrip(lh, oracle, k, m, nbytes, 10, seed=k + m + int(overlap))
         assert dec[:2] == ["lh_plan_kernel(closed form)", "lh_jit_decode_wide"], dec
+
+
+@pytest.mark.parametrize("align", [128, 64])
+def test_aligned_decode_buffer(lh, oracle, align):
+    """bench.py's aligned decode buffer (a padded stripe stride and an offset that put every
+    stripe's recovery slots on an `align`-byte boundary) through the specialised k29/m4
+    kernels: the encode writes straight into the recovery slots, the decode runs in place;
+    every stripe against the oracle and the padding bytes untouched."""
+    import torch
+    import bench
+    k, m, nbytes, stripes = 29, 4, 1296, 99
+    off, stride = bench.aligned_layout(k, m, nbytes, align)
+    buf = torch.full((off + stride * stripes,), 0x5A, dtype=torch.uint8, device="cuda")
+    D = buf[off:].as_strided((stripes, k, nbytes), (stride, nbytes, 1))
+    data = lhutil.fill(align + 1, stripes * k * nbytes).reshape(stripes, k, nbytes)
+    scen = [lhutil.erasure_case(align * 1000 + s, k, m, m, shuffle=False) for s in range(stripes)]
+    rows = np.array([rw for _, rw in scen], dtype=np.uint8)
+    for s, (slots, _) in enumerate(scen):      # survivors first, the m recovery slots last
+        D[s, : k - m] = torch.from_numpy(np.stack([data[s, x] for kind, x in slots if kind == "d"])).cuda()
+    lh.encode_batch(_gpu(data), m, recovery=D[:, k - m:])
+    assert lh.last_launch() == ["lh_jit_encode"]
+    d_rows = _gpu(rows)
+    status = lh.decode_batch(D, d_rows, m)
+    torch.cuda.synchronize()
+    assert lh.last_launch() == FUSED and (status.cpu() == 0).all()
+    got, got_rows = D.cpu().numpy(), d_rows.cpu().numpy()
+    for s in range(stripes):
+        rc, rec = oracle.encode(k, m, data[s], nbytes)
+        rec = rec.reshape(m, nbytes)
+        bufs = [data[s, x].copy() if kind == "d" else rec[x].copy() for kind, x in scen[s][0]]
+        rc, exp_rows = oracle.decode(k, m, bufs, list(rows[s]), nbytes)
+        assert list(got_rows[s]) == exp_rows, s
+        assert all(got[s, i].tobytes() == bufs[i].tobytes() for i in range(k)), s
+    raw = buf.cpu().numpy()
+    pad = np.ones(raw.size, dtype=bool)
+    for s in range(stripes):
+        pad[off + s * stride: off + s * stride + k * nbytes] = False
+    assert (raw[pad] == 0x5A).all()
