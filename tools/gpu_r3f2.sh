@@ -30,3 +30,8 @@ if [ -n "$have" ]; then
   timeout -s KILL 240 rocprofv3 --pmc $have --kernel-trace -d "$OUT/sq2_k128m32" -o run --output-format csv -- python3 tools/prof_kernels.py k128m32 > "$OUT/sq2_k128m32.log" 2>&1 || { tail -20 "$OUT/sq2_k128m32.log"; exit 1; }
   python3 tools/sq_summary.py "$(find "$OUT/sq2_k128m32" -name '*counter_collection.csv' | head -1)" k128m32_scalar > "$OUT/sq2_k128m32.json" || exit 1
 fi
+# pinned-host pipeline timeline (kernel + memory-copy trace, no counters)
+timeout -k 10 300 python tools/pcie_bench.py k29m4 > "$OUT/pcie.json" 2> "$OUT/pcie.err" || { tail -20 "$OUT/pcie.err"; exit 1; }
+cut -c1-300 "$OUT/pcie.json"
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT/pcie_prof" -o run --output-format csv -- python3 tools/pcie_bench.py k29m4 > "$OUT/pcie_prof.log" 2>&1 || { tail -20 "$OUT/pcie_prof.log"; exit 1; }
+find "$OUT/pcie_prof" -name "*.csv" | head
