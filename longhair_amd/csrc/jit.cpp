@@ -122,6 +122,8 @@ bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
         cfg->rows_per_wave = (m + ng - 1) / ng;
     }
     if (const char *r = std::getenv("LONGHAIR_AMD_WIN_ROWS")) cfg->rows_per_wave = std::atoi(r);
+    if (!decode)  // tuning knob for the encode alone (the decode's phase A keeps its rows)
+        if (const char *r = std::getenv("LONGHAIR_AMD_WIN_ROWS_ENC")) cfg->rows_per_wave = std::atoi(r);
     cfg->win_pf = 3;
     if (const char *f = std::getenv("LONGHAIR_AMD_WIN_PF")) cfg->win_pf = std::max(1, std::atoi(f));
     cfg->win_lds = 1;
