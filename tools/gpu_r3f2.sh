@@ -29,7 +29,7 @@ done
 [ "$PART" = a ] && exit 0
 # scalar / LDS issue of the large-m kernels (names checked against the available list)
 [ -f "$OUT/sq_names.txt" ] || { timeout -k 10 120 rocprofv3 --list-avail > "$OUT/avail.txt" 2>&1 || true; grep -oE "SQ_[A-Z0-9_]+" "$OUT/avail.txt" | sort -u | tr '\n' ' ' > "$OUT/sq_names.txt"; }
-want="SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INST_CYCLES_SALU SQ_WAVES"
+want="SQ_INSTS_SALU SQ_IFETCH SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INST_CYCLES_SALU SQ_WAVES"
 have=""; for c in $want; do grep -qw "$c" "$OUT/sq_names.txt" && have="$have $c"; done
 echo "SQ pass 2:$have"
 if [ -n "$have" ]; then
