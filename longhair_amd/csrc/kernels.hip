@@ -867,6 +867,136 @@ __device__ __forceinline__ void lh_inverse_body(const lh::InverseArgs &a, uint32
     }
 }
 
+// Phase B with the V rows staged by LDS-DMA (round 3): double-buffered tiles of TILE rows,
+// 2 global_load_lds_dwordx4 per row (16 B per lane: lane l moves bytes (l % 16) * 16 of
+// sub-block 4 h + l / 16, so each instruction fills 1 KiB of the row's [sub-block][256 B]
+// image in lane order).  The DMA of tile t + 1 is issued right after the barrier that
+// publishes tile t and lands while tile t is computed; one counted wait + a raw barrier per
+// tile (no __syncthreads, whose fence would drain the DMA).  Same multiply and outputs as
+// lh_inverse_body.
+template <int JO, int TILE, bool IDX>
+__device__ __forceinline__ void lh_inverse_dma_body(const lh::InverseArgs &a, uint32_t *__restrict__ lvA,
+                                                    uint32_t *__restrict__ lvB) {
+    static_assert(IDX ? (JO == 4 || JO == 8) : (JO >= 1 && JO <= 4), "outputs per wave");
+    const int nw = (int)(blockDim.x >> 6);
+    const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = (int)(threadIdx.x & 63);
+    const int cps = a.bytes >> 11;
+    const long long stripe = blockIdx.x / cps;
+    if (stripe >= a.stripes) return;  // workgroup-uniform
+    const uint8_t *pl = a.plan + stripe * a.plan_stride;
+    const int e = pl[0];
+    if (e == 0) return;  // workgroup-uniform
+    const int m = a.m, sub = a.bytes >> 3;
+    const lh::PlanView pv(pl, a.k, m, a.e_max);
+    const uint32_t rslot = lane < m ? (uint32_t)pv.rec_slot(lane) : 0xFFu;
+    const unsigned long long used = __ballot(rslot != 0xFFu);
+    const int chunk = (int)(blockIdx.x % cps) * 256;
+    uint8_t *sbase = a.blocks + stripe * a.stride + chunk;  // wave-uniform
+    uint8_t *base = sbase + lane * 4;
+    const int dof0 = (lane >> 4) * sub + (lane & 15) * 16, dof1 = dof0 + 4 * sub;
+    const int nout = g < e ? (e - g + nw - 1) / nw : 0;  // outputs g, g + nw, ... (<= JO)
+    uint32_t cpk0 = 0, cpk1 = 0;  // lane r: this wave's coefficients for recovery row r
+    if (rslot != 0xFFu) {
+        const uint8_t *cf = pv.coef_ptr();
+#pragma unroll
+        for (int i = 0; i < JO; ++i)
+            if (i < nout) {
+                const uint32_t c = (uint32_t)cf[(g + i * nw) * m + lane] << (8 * (i & 3));
+                if (i < 4) cpk0 |= c;
+                else cpk1 |= c;
+            }
+    }
+    uint32_t acc[JO][8];
+#pragma unroll
+    for (int i = 0; i < JO; ++i)
+#pragma unroll
+        for (int y = 0; y < 8; ++y) acc[i][y] = 0;
+    // DMA of the tile starting at `rest` into `buf`: this wave moves tile positions g, g + nw, ...
+    auto issue = [&](unsigned long long rest, uint32_t *buf) {
+        for (int t = 0; t < g && rest; ++t) rest &= rest - 1;  // position g
+        for (int j = g; rest && j < TILE; j += nw) {
+            const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)rslot, __builtin_ctzll(rest));
+            const uint8_t *src = sbase + (long long)slot * a.bytes;
+            uint8_t *dst = (uint8_t *)buf + j * 2048;
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + dof0),
+                                             (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + dof1),
+                                             (__attribute__((address_space(3))) void *)(dst + 1024), 16, 0, 0);
+            for (int t = 0; t < nw && rest; ++t) rest &= rest - 1;
+        }
+    };
+    auto skip_tile = [](unsigned long long rest) {
+        for (int j = 0; rest && j < TILE; ++j) rest &= rest - 1;
+        return rest;
+    };
+    auto compute = [&](unsigned long long rest, const uint32_t *buf) {
+        for (int j = 0; rest && j < TILE; ++j, rest &= rest - 1) {
+            if (nout == 0) continue;
+            const int r = __builtin_ctzll(rest);
+            uint32_t v[8];
+#pragma unroll
+            for (int y = 0; y < 8; ++y) v[y] = buf[(j * 8 + y) * 64 + lane];
+            uint32_t tl[16], th[16];
+            tl[0] = th[0] = 0;
+#pragma unroll
+            for (int q = 1; q < 16; ++q) {
+                const int low = __builtin_ctz(q), pre = q & (q - 1);
+                tl[q] = pre ? (tl[pre] ^ v[low]) : v[low];
+                th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];
+            }
+            const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)cpk0, r);
+            if constexpr (IDX) {
+                const uint32_t c1 = JO > 4 ? (uint32_t)__builtin_amdgcn_readlane((int)cpk1, r) : 0u;
+                lh_mul_jump_idx<JO>(c0, c1, acc, tl, th);
+            } else {
+#pragma unroll
+                for (int i = 0; i < JO; ++i)
+                    if (i < nout) lh_mul_jump((c0 >> (8 * i)) & 0xFFu, acc[i], tl, th);
+            }
+        }
+    };
+    // s_waitcnt vmcnt(0) with expcnt / lgkmcnt untouched; then lgkmcnt(0) (gfx9 encodings)
+    auto publish = [] {
+        __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));   // vmcnt(0): this wave's DMAs landed
+        __builtin_amdgcn_s_waitcnt(0xF | (7 << 4) | (3 << 14));  // lgkmcnt(0): its LDS reads done
+        __builtin_amdgcn_s_barrier();
+    };
+    unsigned long long todo = used;
+    issue(todo, lvA);
+    while (true) {  // workgroup-uniform
+        publish();  // tile in A; every wave is done with B
+        unsigned long long next = skip_tile(todo);
+        if (next) issue(next, lvB);
+        compute(todo, lvA);
+        todo = next;
+        if (!todo) break;
+        publish();  // tile in B; every wave is done with A
+        next = skip_tile(todo);
+        if (next) issue(next, lvA);
+        compute(todo, lvB);
+        todo = next;
+        if (!todo) break;
+    }
+    // Every wave waited for its DMAs before the last barrier: every V row has been read, so
+    // the recovery slots may be overwritten.
+#pragma unroll
+    for (int i = 0; i < JO; ++i) {
+        if (i < nout) {
+            uint8_t *dst = base + (long long)pv.out_slot(g + i * nw) * a.bytes;
+#pragma unroll
+            for (int y = 0; y < 8; ++y) __builtin_nontemporal_store(acc[i][y], (uint32_t *)(dst + (long long)y * sub));
+        }
+    }
+}
+
+template <int JO, int TILE, bool IDX>
+__global__ void __launch_bounds__(1024) lh_inverse_dma_kernel(lh::InverseArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lvA[TILE * 8 * 64];
+    __shared__ __attribute__((aligned(16))) uint32_t lvB[TILE * 8 * 64];
+    lh_inverse_dma_body<JO, TILE, IDX>(a, lvA, lvB);
+}
+
 // One inlined table per output (JO <= 4 copies of 17 KiB).
 template <int JO, int MAXE, int BLK, int PFR>
 __global__ void __launch_bounds__(1024) lh_inverse_jt_kernel(lh::InverseArgs a) {
@@ -1019,6 +1149,26 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
         if (pf) LH_LAUNCH_INV(KERNEL, JO, MAXE, BLK, 2);         \
         LH_LAUNCH_INV(KERNEL, JO, MAXE, BLK, 0);                 \
     } while (0)
+    // LONGHAIR_AMD_INV_DMA = tile rows (8 or 16): stage V by LDS-DMA, double-buffered
+    if (const char *dm = std::getenv("LONGHAIR_AMD_INV_DMA")) {
+        const int t = std::atoi(dm);
+        const bool idx = jp == 9 || (jpe == nullptr && small);
+        const int jo = idx ? 8 : 4;
+        const dim3 block(64u * (unsigned)((a.e_max + jo - 1) / jo));
+#define LH_LAUNCH_DMA(JO, T, IDX)                                                              \
+        do {                                                                                   \
+            hipLaunchKernelGGL((lh_inverse_dma_kernel<JO, T, IDX>), grid, block, 0, st, a);   \
+            note_launch("lh_inverse_dma_kernel<" #JO "," #T "," #IDX ">");                       \
+            return hipGetLastError();                                                          \
+        } while (0)
+        if (t == 8 || t == 16) {
+            if (idx && t == 8) LH_LAUNCH_DMA(8, 8, true);
+            if (idx) LH_LAUNCH_DMA(8, 16, true);
+            if (t == 8) LH_LAUNCH_DMA(4, 8, false);
+            LH_LAUNCH_DMA(4, 16, false);
+        }
+#undef LH_LAUNCH_DMA
+    }
     if (jp == 2 && small) LH_LAUNCH_INV(lh_inverse_jt_kernel, 2, 32, 0, 0);
     if (jp == 40 && small) LH_LAUNCH_INV(lh_inverse_jt_kernel, 4, 32, 0, 0);
     if (jp == 5) {

@@ -93,6 +93,12 @@ PHASE_B = [
     ({"LONGHAIR_AMD_INV_JUMP": "9", "LONGHAIR_AMD_INV_BLK": "16"}, 33, "lh_inverse_ji_kernel<8,64,16,0>"),
     ({"LONGHAIR_AMD_INV_JUMP": "9", "LONGHAIR_AMD_INV_BLK": "16", "LONGHAIR_AMD_INV_PF": "1"}, 33,
      "lh_inverse_ji_kernel<8,64,16,2>"),
+    # V staged by LDS-DMA into double-buffered tiles of 8 or 16 rows
+    ({"LONGHAIR_AMD_INV_DMA": "8"}, 32, "lh_inverse_dma_kernel<8,8,true>"),
+    ({"LONGHAIR_AMD_INV_DMA": "16"}, 32, "lh_inverse_dma_kernel<8,16,true>"),
+    ({"LONGHAIR_AMD_INV_DMA": "8"}, 33, "lh_inverse_dma_kernel<4,8,false>"),
+    ({"LONGHAIR_AMD_INV_DMA": "16"}, 33, "lh_inverse_dma_kernel<4,16,false>"),
+    ({"LONGHAIR_AMD_INV_DMA": "8", "LONGHAIR_AMD_INV_JUMP": "9"}, 33, "lh_inverse_dma_kernel<8,8,true>"),
 ]
 
 
