@@ -1113,6 +1113,7 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     if (blocks <= 0) return hipSuccess;
     if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
     // Phase-B kernel (profiles/r2_tune_split_decode.txt, r3 sessions):
+    // Register-staged phase B (LONGHAIR_AMD_INV_DMA=0, or the variants below):
     //   LONGHAIR_AMD_INV_JUMP  default: e_max <= 32 as 9, above as 4
     //                          4 computed jump, one inlined table per output, 4 outputs per
     //                            wave
@@ -1149,10 +1150,17 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
         if (pf) LH_LAUNCH_INV(KERNEL, JO, MAXE, BLK, 2);         \
         LH_LAUNCH_INV(KERNEL, JO, MAXE, BLK, 0);                 \
     } while (0)
-    // LONGHAIR_AMD_INV_DMA = tile rows (8 or 16): stage V by LDS-DMA, double-buffered
-    if (const char *dm = std::getenv("LONGHAIR_AMD_INV_DMA")) {
-        const int t = std::atoi(dm);
-        const bool idx = jp == 9 || (jpe == nullptr && small);
+    // Default (round 3): V staged by LDS-DMA into double-buffered 8-row tiles, the indexed
+    // single-table jump with 8 outputs per wave, at every e_max (profiles/r3i_phase_b_dma.txt:
+    // k128/m32 decode 3.87-3.88 -> 3.71 ms, k200/m56 0.615-0.622 -> 0.604-0.605; 16-row tiles
+    // 4.59 ms: 64 KiB of LDS per workgroup).  LONGHAIR_AMD_INV_DMA = 0 selects the register-
+    // staged kernels below (LONGHAIR_AMD_INV_JUMP etc.), 8 / 16 the tile rows; with
+    // LONGHAIR_AMD_INV_JUMP = 4 the DMA kernel uses one inlined table per output.
+    const char *dm = std::getenv("LONGHAIR_AMD_INV_DMA");
+    const int dma_rows = dm ? std::atoi(dm) : 8;
+    if ((dma_rows == 8 || dma_rows == 16) && (jpe == nullptr || jp == 4 || jp == 9)) {
+        const int t = dma_rows;
+        const bool idx = jpe == nullptr || jp == 9;
         const int jo = idx ? 8 : 4;
         const dim3 block(64u * (unsigned)((a.e_max + jo - 1) / jo));
 #define LH_LAUNCH_DMA(JO, T, IDX)                                                              \

@@ -25,8 +25,8 @@ SMALL4 = ["lh_plan_small_kernel<4>", "lh_jit_decode"]
 SMALL8 = ["lh_plan_small_kernel<8>", "lh_jit_decode"]
 GENERIC_CF = ["lh_plan_kernel(closed form)", "lh_apply_generic_kernel", "lh_scatter_kernel"]
 GENERIC_S8 = ["lh_plan_small_kernel<8>", "lh_apply_generic_kernel", "lh_scatter_kernel"]
-WIDE16 = ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_ji_kernel<8,32,16,0>"]
-WIDE64 = ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_jt_kernel<4,64,0,0>"]
+WIDE16 = ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_dma_kernel<8,8,true>"]
+WIDE64 = WIDE16  # (one phase-B kernel for every e_max since round 3)
 
 # (id, k, m, bytes, stripes, env, encode kernels, decode kernels)
 BOUNDARIES = [
@@ -68,6 +68,7 @@ BOUNDARIES = [
 
 # Phase-B kernel variants (kernels.hip launch_inverse, LONGHAIR_AMD_INV_JUMP / _INV_OPW).
 PHASE_B = [
+    # register-staged V tiles (LONGHAIR_AMD_INV_DMA=0): Horner, per-output tables, indexed
     ({"LONGHAIR_AMD_INV_JUMP": "0"}, 32, "lh_inverse_kernel<4>"),
     ({"LONGHAIR_AMD_INV_JUMP": "0", "LONGHAIR_AMD_INV_OPW": "8"}, 32, "lh_inverse_kernel<8>"),
     ({"LONGHAIR_AMD_INV_JUMP": "0"}, 33, "lh_inverse_kernel<4>"),
@@ -76,29 +77,30 @@ PHASE_B = [
     ({"LONGHAIR_AMD_INV_JUMP": "2"}, 33, "lh_inverse_kernel<4>"),      # e_max > 32: Horner
     ({"LONGHAIR_AMD_INV_JUMP": "40"}, 32, "lh_inverse_jt_kernel<4,32,0,0>"),
     ({"LONGHAIR_AMD_INV_JUMP": "40"}, 33, "lh_inverse_jt_kernel<4,64,0,0>"),
-    # one inlined table per output (the default above e_max 32), with the next-tile
-    # prefetch, and 16-row tiles above e_max 32
-    ({"LONGHAIR_AMD_INV_JUMP": "4"}, 32, "lh_inverse_jt_kernel<4,32,16,0>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "4", "LONGHAIR_AMD_INV_PF": "1"}, 32, "lh_inverse_jt_kernel<4,32,16,2>"),
-    ({"LONGHAIR_AMD_INV_BLK": "16"}, 33, "lh_inverse_jt_kernel<4,64,16,0>"),
-    ({"LONGHAIR_AMD_INV_BLK": "16", "LONGHAIR_AMD_INV_PF": "1"}, 33, "lh_inverse_jt_kernel<4,64,16,2>"),
-    # one table copy reached by GPR indexing, 4 or 8 outputs per wave (8: the default up to
-    # e_max 32)
+    ({"LONGHAIR_AMD_INV_DMA": "0", "LONGHAIR_AMD_INV_JUMP": "4"}, 32, "lh_inverse_jt_kernel<4,32,16,0>"),
+    ({"LONGHAIR_AMD_INV_DMA": "0", "LONGHAIR_AMD_INV_JUMP": "4", "LONGHAIR_AMD_INV_PF": "1"}, 32,
+     "lh_inverse_jt_kernel<4,32,16,2>"),
+    ({"LONGHAIR_AMD_INV_DMA": "0"}, 33, "lh_inverse_jt_kernel<4,64,0,0>"),
+    ({"LONGHAIR_AMD_INV_DMA": "0", "LONGHAIR_AMD_INV_BLK": "16"}, 33, "lh_inverse_jt_kernel<4,64,16,0>"),
+    ({"LONGHAIR_AMD_INV_DMA": "0", "LONGHAIR_AMD_INV_BLK": "16", "LONGHAIR_AMD_INV_PF": "1"}, 33,
+     "lh_inverse_jt_kernel<4,64,16,2>"),
     ({"LONGHAIR_AMD_INV_JUMP": "5"}, 32, "lh_inverse_ji_kernel<4,32,16,0>"),
     ({"LONGHAIR_AMD_INV_JUMP": "5", "LONGHAIR_AMD_INV_PF": "1"}, 32, "lh_inverse_ji_kernel<4,32,16,2>"),
     ({"LONGHAIR_AMD_INV_JUMP": "5"}, 33, "lh_inverse_ji_kernel<4,64,0,0>"),
     ({"LONGHAIR_AMD_INV_JUMP": "5", "LONGHAIR_AMD_INV_BLK": "16"}, 33, "lh_inverse_ji_kernel<4,64,16,0>"),
-    ({"LONGHAIR_AMD_INV_PF": "1"}, 32, "lh_inverse_ji_kernel<8,32,16,2>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "9"}, 33, "lh_inverse_ji_kernel<8,64,0,0>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "9", "LONGHAIR_AMD_INV_BLK": "16"}, 33, "lh_inverse_ji_kernel<8,64,16,0>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "9", "LONGHAIR_AMD_INV_BLK": "16", "LONGHAIR_AMD_INV_PF": "1"}, 33,
-     "lh_inverse_ji_kernel<8,64,16,2>"),
-    # V staged by LDS-DMA into double-buffered tiles of 8 or 16 rows
-    ({"LONGHAIR_AMD_INV_DMA": "8"}, 32, "lh_inverse_dma_kernel<8,8,true>"),
+    ({"LONGHAIR_AMD_INV_DMA": "0"}, 32, "lh_inverse_ji_kernel<8,32,16,0>"),
+    ({"LONGHAIR_AMD_INV_DMA": "0", "LONGHAIR_AMD_INV_PF": "1"}, 32, "lh_inverse_ji_kernel<8,32,16,2>"),
+    ({"LONGHAIR_AMD_INV_DMA": "0", "LONGHAIR_AMD_INV_JUMP": "9"}, 33, "lh_inverse_ji_kernel<8,64,0,0>"),
+    ({"LONGHAIR_AMD_INV_DMA": "0", "LONGHAIR_AMD_INV_JUMP": "9", "LONGHAIR_AMD_INV_BLK": "16"}, 33,
+     "lh_inverse_ji_kernel<8,64,16,0>"),
+    ({"LONGHAIR_AMD_INV_DMA": "0", "LONGHAIR_AMD_INV_JUMP": "9", "LONGHAIR_AMD_INV_BLK": "16",
+      "LONGHAIR_AMD_INV_PF": "1"}, 33, "lh_inverse_ji_kernel<8,64,16,2>"),
+    # V staged by LDS-DMA into double-buffered tiles (default: 8 rows, indexed, 8 outputs)
     ({"LONGHAIR_AMD_INV_DMA": "16"}, 32, "lh_inverse_dma_kernel<8,16,true>"),
-    ({"LONGHAIR_AMD_INV_DMA": "8"}, 33, "lh_inverse_dma_kernel<4,8,false>"),
-    ({"LONGHAIR_AMD_INV_DMA": "16"}, 33, "lh_inverse_dma_kernel<4,16,false>"),
-    ({"LONGHAIR_AMD_INV_DMA": "8", "LONGHAIR_AMD_INV_JUMP": "9"}, 33, "lh_inverse_dma_kernel<8,8,true>"),
+    ({"LONGHAIR_AMD_INV_DMA": "16"}, 33, "lh_inverse_dma_kernel<8,16,true>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "4"}, 32, "lh_inverse_dma_kernel<4,8,false>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "4"}, 33, "lh_inverse_dma_kernel<4,8,false>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "4", "LONGHAIR_AMD_INV_DMA": "16"}, 33, "lh_inverse_dma_kernel<4,16,false>"),
 ]
 
 
