@@ -149,6 +149,7 @@ struct Device {
     std::mutex pipe_mu;
     hipStream_t pipe_stream[3] = {nullptr, nullptr, nullptr};
     DevBuf pipe_blocks[3], pipe_out[3], pipe_rows[3], pipe_rows0[3], pipe_status[3];
+    HostPinned pipe_meta;  // decode: the call's Block.row bytes and status, pinned
 };
 
 static std::mutex g_devices_mu;
@@ -704,6 +705,15 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
         if (kernel_wb) LH_HIP(d->pipe_rows0[i].reserve((size_t)chunk * k));
         LH_HIP(d->pipe_status[i].reserve((size_t)chunk));
     }
+    // The rows and status travel through pinned staging: a copy into pageable memory (numpy
+    // arrays, the status vector callers typically allocate) is synchronous, and one per
+    // chunk serialised the whole pipeline -- every chunk's H2D waited for the previous
+    // chunk's kernels and write-back (decode 48 GB/s against 56 for the encode;
+    // profiles/r3_pcie_timeline.txt).
+    LH_HIP(d->pipe_meta.reserve((size_t)stripes * k + (size_t)stripes));
+    uint8_t *prows = d->pipe_meta.ptr;
+    int8_t *pstatus = (int8_t *)(prows + (size_t)stripes * k);
+    std::memcpy(prows, h_rows, (size_t)stripes * k);
     for (int s0 = 0, c = 0; s0 < stripes; s0 += chunk, ++c) {
         const int n = stripes - s0 < chunk ? stripes - s0 : chunk;
         const int i = c % 3;
@@ -726,7 +736,7 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
         }
         LH_HIP(hipMemcpy2DAsync(d->pipe_blocks[i].ptr, sz, h_blocks + (long long)s0 * stride, stride, sz, n,
                                 hipMemcpyHostToDevice, st));
-        LH_HIP(hipMemcpyAsync(d->pipe_rows[i].ptr, h_rows + (long long)s0 * k, (size_t)n * k, hipMemcpyHostToDevice, st));
+        LH_HIP(hipMemcpyAsync(d->pipe_rows[i].ptr, prows + (long long)s0 * k, (size_t)n * k, hipMemcpyHostToDevice, st));
         if (kernel_wb)
             LH_HIP(hipMemcpyAsync(d->pipe_rows0[i].ptr, d->pipe_rows[i].ptr, (size_t)n * k, hipMemcpyDeviceToDevice, st));
         const int rc = decode_batch(k, m, bytes, n, d->pipe_blocks[i].ptr, sz, d->pipe_rows[i].ptr,
@@ -748,10 +758,12 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
             LH_HIP(hipMemcpy2DAsync(h_blocks + (long long)s0 * stride + off, stride, d->pipe_blocks[i].ptr + off, sz, w,
                                     n, hipMemcpyDeviceToHost, st));
         }
-        LH_HIP(hipMemcpyAsync(h_rows + (long long)s0 * k, d->pipe_rows[i].ptr, (size_t)n * k, hipMemcpyDeviceToHost, st));
-        if (h_status) LH_HIP(hipMemcpyAsync(h_status + s0, d->pipe_status[i].ptr, n, hipMemcpyDeviceToHost, st));
+        LH_HIP(hipMemcpyAsync(prows + (long long)s0 * k, d->pipe_rows[i].ptr, (size_t)n * k, hipMemcpyDeviceToHost, st));
+        LH_HIP(hipMemcpyAsync(pstatus + s0, d->pipe_status[i].ptr, n, hipMemcpyDeviceToHost, st));
     }
     for (auto s : d->pipe_stream) LH_HIP(hipStreamSynchronize(s));
+    std::memcpy(h_rows, prows, (size_t)stripes * k);
+    if (h_status) std::memcpy(h_status, pstatus, (size_t)stripes);
     return kOk;
 }
 
