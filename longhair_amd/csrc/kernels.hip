@@ -997,6 +997,220 @@ __global__ void __launch_bounds__(1024) lh_inverse_dma_kernel(lh::InverseArgs a)
     lh_inverse_dma_body<JO, TILE, IDX>(a, lvA, lvB);
 }
 
+// ---- phase B through ONE table per code object (round 3): the 256 bodies sit in the
+// never-launched kernel below under the hidden symbol lh_inv_gtab, every register they
+// touch fixed (tools/gen_inv_jump.py render_global_table).  A wave holds, per output slot i,
+// the absolute low address of the body for row r's coefficient in lane r of t[i] (computed
+// once), so per (output, row) only v_readlane + s_set_gpr_idx_idx + s_swappc_b64 + the
+// body's s_setpc_b64 issue on the scalar unit (3 SALU, against 7 for the in-asm table,
+// whose SALU count exceeded its VALU count: profiles/sq_k128m32.json).
+__global__ void lh_inv_gtab_holder() { asm volatile(LH_INV_GTAB_TEXT); }
+
+template <int N>
+__device__ __forceinline__ void lh_mul_jump_g(uint32_t (&acc)[8][8], const uint32_t (&tl)[16],
+                                              const uint32_t (&th)[16], const uint32_t (&t)[8], int r,
+                                              uint32_t hi) {
+#define LH_GT_CASE(n)                                                                                       \
+    if constexpr (N == n)                                                                                   \
+        asm volatile(LH_INV_JUMPG##n##_ASM : LH_INV_JUMPG##n##_OUTS(acc) : LH_INV_JUMPG_INS(tl, th, t),      \
+                     [r] "s"(r), [hi] "s"(hi) : "s92", "s93", "s94", "s95", "s97", "scc");
+    LH_GT_CASE(1) LH_GT_CASE(2) LH_GT_CASE(3) LH_GT_CASE(4) LH_GT_CASE(5) LH_GT_CASE(6) LH_GT_CASE(7)
+    LH_GT_CASE(8)
+#undef LH_GT_CASE
+}
+
+template <int N>
+__device__ __forceinline__ void lh_mul_chain(uint32_t (&acc)[8][8], const uint32_t (&tl)[16],
+                                             const uint32_t (&th)[16], const uint32_t (&t)[8], int r,
+                                             uint32_t hi) {
+#define LH_CH_CASE(n)                                                                                        \
+    if constexpr (N == n)                                                                                    \
+        asm volatile(LH_INV_JUMPC##n##_ASM : LH_INV_JUMPC##n##_OUTS(acc) : LH_INV_JUMPC##n##_INS(tl, th, t), \
+                     [r] "s"(r), [hi] "s"(hi) : LH_INV_JUMPC##n##_CLOBBER, "s92", "s93", "s94", "s95", "s96",  \
+                     "s97", "scc");
+    LH_CH_CASE(1) LH_CH_CASE(2) LH_CH_CASE(3) LH_CH_CASE(4) LH_CH_CASE(5) LH_CH_CASE(6) LH_CH_CASE(7)
+    LH_CH_CASE(8)
+#undef LH_CH_CASE
+}
+
+// Same staging as lh_inverse_dma_body (double-buffered LDS-DMA tiles); the multiply jumps
+// into lh_inv_gtab.  Outputs: PACK ? wave g recovers outputs 8g .. 8g + 7 (fewer waves build
+// the row tables) : g, g + nw, ... as in lh_inverse_dma_body.  The row loop is instantiated
+// per output count (1..8, wave-uniform) so no slot jumps for an unused output.
+template <int TILE, bool CH>
+__device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uint32_t *__restrict__ lvA,
+                                                   uint32_t *__restrict__ lvB, uint32_t tlo, uint32_t thi) {
+    const int nw = (int)(blockDim.x >> 6);
+    const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = (int)(threadIdx.x & 63);
+    const int cps = a.bytes >> 11;
+    const long long stripe = blockIdx.x / cps;
+    if (stripe >= a.stripes) return;  // workgroup-uniform
+    const uint8_t *pl = a.plan + stripe * a.plan_stride;
+    const int e = pl[0];
+    if (e == 0) return;  // workgroup-uniform
+    const int m = a.m, sub = a.bytes >> 3;
+    const lh::PlanView pv(pl, a.k, m, a.e_max);
+    const uint32_t rslot = lane < m ? (uint32_t)pv.rec_slot(lane) : 0xFFu;
+    const unsigned long long used = __ballot(rslot != 0xFFu);
+    const int chunk = (int)(blockIdx.x % cps) * 256;
+    uint8_t *sbase = a.blocks + stripe * a.stride + chunk;  // wave-uniform
+    uint8_t *base = sbase + lane * 4;
+    const int dof0 = (lane >> 4) * sub + (lane & 15) * 16, dof1 = dof0 + 4 * sub;
+    const bool pack = a.pack != 0;
+    int nout = pack ? e - 8 * g : (g < e ? (e - g + nw - 1) / nw : 0);
+    nout = nout < 0 ? 0 : (nout > 8 ? 8 : nout);
+    auto out_of = [&](int i) { return pack ? 8 * g + i : g + i * nw; };
+    uint32_t t[8];  // lane r: body address of output slot i for recovery row r
+    {
+        const uint8_t *cf = pv.coef_ptr();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t c = (rslot != 0xFFu && i < nout) ? cf[out_of(i) * m + lane] : 0u;
+            t[i] = tlo + c * (CH ? 84u : 68u);
+        }
+    }
+    auto issue = [&](unsigned long long rest, uint32_t *buf) {
+        for (int q = 0; q < g && rest; ++q) rest &= rest - 1;  // position g
+        for (int j = g; rest && j < TILE; j += nw) {
+            const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)rslot, __builtin_ctzll(rest));
+            const uint8_t *src = sbase + (long long)slot * a.bytes;
+            uint8_t *dst = (uint8_t *)buf + j * 2048;
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + dof0),
+                                             (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + dof1),
+                                             (__attribute__((address_space(3))) void *)(dst + 1024), 16, 0, 0);
+            for (int q = 0; q < nw && rest; ++q) rest &= rest - 1;
+        }
+    };
+    auto skip_tile = [](unsigned long long rest) {
+        for (int j = 0; rest && j < TILE; ++j) rest &= rest - 1;
+        return rest;
+    };
+    auto publish = [] {
+        __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));        // vmcnt(0)
+        __builtin_amdgcn_s_waitcnt(0xF | (7 << 4) | (3 << 14));  // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+    };
+    auto run = [&](auto no) {
+        constexpr int N = decltype(no)::value;
+        uint32_t acc[8][8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int y = 0; y < 8; ++y) acc[i][y] = 0;
+        auto compute = [&](unsigned long long rest, const uint32_t *buf) {
+            if constexpr (N > 0) {
+                for (int j = 0; rest && j < TILE; ++j, rest &= rest - 1) {
+                    const int r = __builtin_ctzll(rest);
+                    uint32_t v[8];
+#pragma unroll
+                    for (int y = 0; y < 8; ++y) v[y] = buf[(j * 8 + y) * 64 + lane];
+                    uint32_t tl[16], th[16];
+                    tl[0] = th[0] = 0;
+#pragma unroll
+                    for (int q = 1; q < 16; ++q) {
+                        const int low = __builtin_ctz(q), pre = q & (q - 1);
+                        tl[q] = pre ? (tl[pre] ^ v[low]) : v[low];
+                        th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];
+                    }
+                    if constexpr (CH) lh_mul_chain<N>(acc, tl, th, t, r, thi);
+                    else lh_mul_jump_g<N>(acc, tl, th, t, r, thi);
+                }
+            }
+        };
+        unsigned long long todo = used;
+        issue(todo, lvA);
+        while (true) {  // workgroup-uniform
+            publish();
+            unsigned long long next = skip_tile(todo);
+            if (next) issue(next, lvB);
+            compute(todo, lvA);
+            todo = next;
+            if (!todo) break;
+            publish();
+            next = skip_tile(todo);
+            if (next) issue(next, lvA);
+            compute(todo, lvB);
+            todo = next;
+            if (!todo) break;
+        }
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            uint8_t *dst = base + (long long)pv.out_slot(out_of(i)) * a.bytes;
+#pragma unroll
+            for (int y = 0; y < 8; ++y) __builtin_nontemporal_store(acc[i][y], (uint32_t *)(dst + (long long)y * sub));
+        }
+    };
+    switch (nout) {  // wave-uniform
+        case 0: run(std::integral_constant<int, 0>{}); break;
+        case 1: run(std::integral_constant<int, 1>{}); break;
+        case 2: run(std::integral_constant<int, 2>{}); break;
+        case 3: run(std::integral_constant<int, 3>{}); break;
+        case 4: run(std::integral_constant<int, 4>{}); break;
+        case 5: run(std::integral_constant<int, 5>{}); break;
+        case 6: run(std::integral_constant<int, 6>{}); break;
+        case 7: run(std::integral_constant<int, 7>{}); break;
+        default: run(std::integral_constant<int, 8>{}); break;
+    }
+}
+
+// The table's address comes from a PC-relative relocation.  A table that would straddle a
+// 4 GiB boundary (the body addresses' high word differs; never seen) or a.jump_fallback
+// (tests) takes the in-asm table instead.
+template <int TILE>
+__global__ void __launch_bounds__(1024) lh_inverse_gt_kernel(lh::InverseArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lvA[TILE * 8 * 64];
+    __shared__ __attribute__((aligned(16))) uint32_t lvB[TILE * 8 * 64];
+    uint32_t tlo, thi;
+    asm volatile(
+        "s_getpc_b64 s[92:93]\n"
+        "s_add_u32 s92, s92, lh_inv_gtab@rel32@lo+4\n"
+        "s_addc_u32 s93, s93, lh_inv_gtab@rel32@hi+12\n"
+        "s_mov_b32 %0, s92\n"
+        "s_mov_b32 %1, s93\n"
+        : "=s"(tlo), "=s"(thi)
+        :
+        : "s92", "s93", "scc");
+    if (a.jump_fallback || tlo > 0xFFFFFFFFu - 256u * 68u) {
+        lh_inverse_dma_body<8, TILE, true>(a, lvA, lvB);
+        return;
+    }
+    lh_inverse_gt_body<TILE, false>(a, lvA, lvB, tlo, thi);
+}
+
+// ---- chained bodies (round 3): a body jumps straight to the next output's body instead of
+// returning (tools/gen_inv_jump.py render_chain_table): one branch and two SALU per
+// (output, row).  The row's code and the table must share the high word of their addresses
+// (checked here with the kernel's own PC; otherwise, or with a.jump_fallback, the in-asm
+// table runs).
+__global__ void lh_inv_ctab_holder() { asm volatile(LH_INV_CTAB_TEXT); }
+
+template <int TILE>
+__global__ void __launch_bounds__(1024) lh_inverse_ch_kernel(lh::InverseArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lvA[TILE * 8 * 64];
+    __shared__ __attribute__((aligned(16))) uint32_t lvB[TILE * 8 * 64];
+    uint32_t tlo, thi, plo, phi;
+    asm volatile(
+        "s_getpc_b64 s[92:93]\n"
+        "s_mov_b32 %2, s92\n"
+        "s_mov_b32 %3, s93\n"
+        "s_add_u32 s92, s92, lh_inv_ctab@rel32@lo+4\n"
+        "s_addc_u32 s93, s93, lh_inv_ctab@rel32@hi+12\n"
+        "s_mov_b32 %0, s92\n"
+        "s_mov_b32 %1, s93\n"
+        : "=s"(tlo), "=s"(thi), "=s"(plo), "=s"(phi)
+        :
+        : "s92", "s93", "scc");
+    // this kernel's code lies within 1 MiB of plo
+    if (a.jump_fallback || phi != thi || tlo > 0xFFFFFFFFu - 256u * 84u || plo < (1u << 20) ||
+        plo > 0xFFFFFFFFu - (1u << 20)) {
+        lh_inverse_dma_body<8, TILE, true>(a, lvA, lvB);
+        return;
+    }
+    lh_inverse_gt_body<TILE, true>(a, lvA, lvB, tlo, thi);
+}
+
 // One inlined table per output (JO <= 4 copies of 17 KiB).
 template <int JO, int MAXE, int BLK, int PFR>
 __global__ void __launch_bounds__(1024) lh_inverse_jt_kernel(lh::InverseArgs a) {
@@ -1158,6 +1372,34 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     // LONGHAIR_AMD_INV_JUMP = 4 the DMA kernel uses one inlined table per output.
     const char *dm = std::getenv("LONGHAIR_AMD_INV_DMA");
     const int dma_rows = dm ? std::atoi(dm) : 8;
+    // LONGHAIR_AMD_INV_JUMP = 10: the DMA staging with the per-code-object table
+    // (lh_inverse_gt_kernel), 11: its chained form (lh_inverse_ch_kernel);
+    // LONGHAIR_AMD_INV_PACK = 1 packs 8 consecutive outputs per wave,
+    // LONGHAIR_AMD_INV_FALLBACK = 1 forces the in-asm-table path inside that kernel (tests).
+    if ((jp == 10 || jp == 11) && (dma_rows == 8 || dma_rows == 16)) {
+        InverseArgs g = a;
+        const char *pk = std::getenv("LONGHAIR_AMD_INV_PACK");
+        const char *fb = std::getenv("LONGHAIR_AMD_INV_FALLBACK");
+        g.pack = pk && std::atoi(pk) ? 1 : 0;
+        g.jump_fallback = fb && std::atoi(fb) ? 1 : 0;
+        const dim3 block(64u * (unsigned)((a.e_max + 7) / 8));
+        if (jp == 11) {
+            if (dma_rows == 8) {
+                hipLaunchKernelGGL((lh_inverse_ch_kernel<8>), grid, block, 0, st, g);
+                note_launch(g.jump_fallback ? "lh_inverse_ch_kernel<8>(fallback)" : "lh_inverse_ch_kernel<8>");
+            } else {
+                hipLaunchKernelGGL((lh_inverse_ch_kernel<16>), grid, block, 0, st, g);
+                note_launch(g.jump_fallback ? "lh_inverse_ch_kernel<16>(fallback)" : "lh_inverse_ch_kernel<16>");
+            }
+        } else if (dma_rows == 8) {
+            hipLaunchKernelGGL((lh_inverse_gt_kernel<8>), grid, block, 0, st, g);
+            note_launch(g.jump_fallback ? "lh_inverse_gt_kernel<8>(fallback)" : "lh_inverse_gt_kernel<8>");
+        } else {
+            hipLaunchKernelGGL((lh_inverse_gt_kernel<16>), grid, block, 0, st, g);
+            note_launch(g.jump_fallback ? "lh_inverse_gt_kernel<16>(fallback)" : "lh_inverse_gt_kernel<16>");
+        }
+        return hipGetLastError();
+    }
     if ((dma_rows == 8 || dma_rows == 16) && (jpe == nullptr || jp == 4 || jp == 9)) {
         const int t = dma_rows;
         const bool idx = jpe == nullptr || jp == 9;

@@ -109,6 +109,8 @@ struct InverseArgs {
     const uint8_t *plan;          // PlanView records
     long long plan_stride;
     int k, m, e_max, bytes, stripes;
+    int pack;                     // lh_inverse_gt_kernel: 8 consecutive outputs per wave
+    int jump_fallback;            // lh_inverse_gt_kernel: take the in-asm table (tests)
 };
 
 hipError_t launch_inverse(const InverseArgs &a, hipStream_t st);

@@ -101,6 +101,20 @@ PHASE_B = [
     ({"LONGHAIR_AMD_INV_JUMP": "4"}, 32, "lh_inverse_dma_kernel<4,8,false>"),
     ({"LONGHAIR_AMD_INV_JUMP": "4"}, 33, "lh_inverse_dma_kernel<4,8,false>"),
     ({"LONGHAIR_AMD_INV_JUMP": "4", "LONGHAIR_AMD_INV_DMA": "16"}, 33, "lh_inverse_dma_kernel<4,16,false>"),
+    # one table per code object (lh_inv_gtab), outputs spread or packed 8 per wave
+    ({"LONGHAIR_AMD_INV_JUMP": "10"}, 32, "lh_inverse_gt_kernel<8>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "10"}, 33, "lh_inverse_gt_kernel<8>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "10", "LONGHAIR_AMD_INV_PACK": "1"}, 32, "lh_inverse_gt_kernel<8>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "10", "LONGHAIR_AMD_INV_PACK": "1"}, 64, "lh_inverse_gt_kernel<8>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "10", "LONGHAIR_AMD_INV_DMA": "16"}, 33, "lh_inverse_gt_kernel<16>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "10", "LONGHAIR_AMD_INV_FALLBACK": "1"}, 33, "lh_inverse_gt_kernel<8>(fallback)"),
+    # chained bodies (each body jumps to the next output's)
+    ({"LONGHAIR_AMD_INV_JUMP": "11"}, 32, "lh_inverse_ch_kernel<8>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "11"}, 33, "lh_inverse_ch_kernel<8>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "11", "LONGHAIR_AMD_INV_PACK": "1"}, 32, "lh_inverse_ch_kernel<8>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "11", "LONGHAIR_AMD_INV_PACK": "1"}, 64, "lh_inverse_ch_kernel<8>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "11", "LONGHAIR_AMD_INV_DMA": "16"}, 33, "lh_inverse_ch_kernel<16>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "11", "LONGHAIR_AMD_INV_FALLBACK": "1"}, 33, "lh_inverse_ch_kernel<8>(fallback)"),
 ]
 
 

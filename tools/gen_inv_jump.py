@@ -54,6 +54,106 @@ def render_indexed(jo):
     return lines
 
 
+# Global-table variant (lh_inverse_gt_kernel): the 256 bodies live once per code object, in
+# the never-launched kernel lh_inv_gtab_holder, under the hidden symbol lh_inv_gtab; every
+# register they touch is fixed: tl[q] in v[GT_TL + q], th[q] in v[GT_TH + q] (q = 1..15),
+# the accumulators of output i in v[IDX_BASE + 8i ..] reached by GPR indexing on VSRC2 and
+# VDST (the accumulator is the bitop's third source, so v_readlane's VGPR source is not
+# moved by the index).  The caller holds the absolute low address of each output's body in a
+# VGPR (lane r: row r's coefficient), so per output only v_readlane + the index + s_swappc
+# run: 3 SALU with the body's s_setpc_b64, against 7 for LH_INV_JUMPI.
+GT_TL, GT_TH = 8, 24
+GT_MAX = 8
+
+
+def render_global_table():
+    """Asm text of LH_INV_GTAB_TEXT: s_endpgm (the holder kernel's own code), then the table."""
+    body = ["s_endpgm", ".p2align 8", ".hidden lh_inv_gtab", ".globl lh_inv_gtab", "lh_inv_gtab:"]
+    for c in range(256):
+        v = c
+        for y in range(8):
+            lo, hi = v & 15, v >> 4
+            a = f"v{IDX_BASE + y}"
+            s1 = f"v{GT_TL + lo}" if lo else "0"
+            s2 = f"v{GT_TH + hi}" if hi else "0"
+            body.append(f"v_bitop3_b32 {a}, {s1}, {s2}, {a} bitop3:0x96")
+            v = xt(v)
+        body.append("s_setpc_b64 s[94:95]")
+    lines = ["#define LH_INV_GTAB_TEXT \\"]
+    for i, b in enumerate(body):
+        lines.append(f'    "{b}\\n"' + (" \\" if i + 1 < len(body) else ""))
+    return lines
+
+
+def render_global_call(n):
+    """Asm text of LH_INV_JUMPG<n>_ASM: outputs 0 .. n-1 of one row.  Operands: [a0]..[a7]
+    the outputs' body addresses (VGPRs, lane r = row r), [r] the row (SGPR), [hi] the high
+    word of the table address (SGPR), the pinned tables and accumulators (not named)."""
+    body = ["s_mov_b32 s97, m0", "s_mov_b32 s93, %[hi]"]
+    for i in range(n):
+        body.append(f"v_readlane_b32 s92, %[a{i}], %[r]")
+        body.append("s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)" if i == 0 else f"s_set_gpr_idx_idx {8 * i}")
+        body.append("s_swappc_b64 s[94:95], s[92:93]")
+    body += ["s_set_gpr_idx_off", "s_mov_b32 m0, s97"]
+    lines = [f"#define LH_INV_JUMPG{n}_ASM \\"]
+    for i, b in enumerate(body):
+        lines.append(f'    "{b}\\n"' + (" \\" if i + 1 < len(body) else ""))
+    outs = ", ".join(f'"+{{v{IDX_BASE + 8 * i + y}}}"(acc[{i}][{y}])' for i in range(n) for y in range(8))
+    lines.append(f"#define LH_INV_JUMPG{n}_OUTS(acc) {outs}")
+    return lines
+
+
+# Chained variant (lh_inverse_ch_kernel): a body does not return to the row's code but jumps
+# straight to the next output's body.  Output i's registers are 9 apart: its body address
+# t[i] (lane r: row r) in v[CH_T + 9i], its accumulators in v[CH_T + 1 + 9i ..]; GPR
+# indexing on VSRC0 and VDST.  Body c: 8 v_bitop3_b32 on v[CH_T + 1 ..] (relative), then
+# m0 += 9 (the next output), v_readlane_b32 s94 <- v[CH_T] lane s96 (relative: t[i + 1] of
+# row s96), s_setpc_b64 s[94:95].  The row's code puts its own return address in the slot
+# after the last output, so the last body jumps back: 1 branch and 2 SALU per output.
+CH_TL, CH_TH, CH_T = 8, 23, 39
+CH_BODY = 84
+
+
+def render_chain_table():
+    """Asm text of LH_INV_CTAB_TEXT: s_endpgm, then the 256 chained bodies (84 bytes each)."""
+    body = ["s_endpgm", ".p2align 8", ".hidden lh_inv_ctab", ".globl lh_inv_ctab", "lh_inv_ctab:"]
+    for c in range(256):
+        v = c
+        for y in range(8):
+            lo, hi = v & 15, v >> 4
+            a = f"v{CH_T + 1 + y}"
+            s1 = f"v{CH_TL + lo}" if lo else "0"
+            s2 = f"v{CH_TH + hi}" if hi else "0"
+            body.append(f"v_bitop3_b32 {a}, {a}, {s1}, {s2} bitop3:0x96")
+            v = xt(v)
+        body += ["s_add_u32 m0, m0, 9", "s_nop 0", f"v_readlane_b32 s94, v{CH_T}, s96", "s_setpc_b64 s[94:95]"]
+    lines = ["#define LH_INV_CTAB_TEXT \\"]
+    for i, b in enumerate(body):
+        lines.append(f'    "{b}\\n"' + (" \\" if i + 1 < len(body) else ""))
+    return lines
+
+
+def render_chain_call(n):
+    """Asm text of LH_INV_JUMPC<n>_ASM: one row through outputs 0 .. n-1.  Operands: [r] the
+    row (SGPR), [hi] the high word shared by the table and this code (SGPR), the pinned
+    tables, body addresses and accumulators (not named)."""
+    body = ["s_mov_b32 s97, m0", "s_mov_b32 s96, %[r]", "s_mov_b32 s95, %[hi]", "s_getpc_b64 s[92:93]", "1:",
+            "s_add_u32 s92, s92, (2f-1b)", f"v_mov_b32 v{CH_T + 9 * n}, s92", f"v_readlane_b32 s94, v{CH_T}, s96",
+            "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)", "s_nop 0", "s_setpc_b64 s[94:95]", "2:",
+            "s_set_gpr_idx_off", "s_mov_b32 m0, s97"]
+    lines = [f"#define LH_INV_JUMPC{n}_ASM \\"]
+    for i, b in enumerate(body):
+        lines.append(f'    "{b}\\n"' + (" \\" if i + 1 < len(body) else ""))
+    outs = ", ".join(f'"+{{v{CH_T + 1 + 9 * i + y}}}"(acc[{i}][{y}])' for i in range(n) for y in range(8))
+    lines.append(f"#define LH_INV_JUMPC{n}_OUTS(acc) {outs}")
+    ins = ", ".join([f'"{{v{CH_TL + q}}}"(tl[{q}])' for q in range(1, 16)]
+                    + [f'"{{v{CH_TH + q}}}"(th[{q}])' for q in range(1, 16)]
+                    + [f'"{{v{CH_T + 9 * i}}}"(t[{i}])' for i in range(n)])
+    lines.append(f"#define LH_INV_JUMPC{n}_INS(tl, th, t) {ins}")
+    lines.append(f'#define LH_INV_JUMPC{n}_CLOBBER "v{CH_T + 9 * n}"')
+    return lines
+
+
 def render():
     """The text of inv_jump.inc."""
     lines = ["// generated by tools/gen_inv_jump.py -- do not edit",
@@ -81,6 +181,16 @@ def render():
         lines.append(f"#define LH_INV_JUMPI{jo}_OUTS(a) {outs}")
     ins = ", ".join([f'[t{q}] "v"(tl[{q}])' for q in range(1, 16)] + [f'[h{q}] "v"(th[{q}])' for q in range(1, 16)])
     lines.append(f"#define LH_INV_JUMPI_INS(tl, th) {ins}")
+    lines += render_global_table()
+    for n in range(1, GT_MAX + 1):
+        lines += render_global_call(n)
+    gins = ", ".join([f'"{{v{GT_TL + q}}}"(tl[{q}])' for q in range(1, 16)]
+                     + [f'"{{v{GT_TH + q}}}"(th[{q}])' for q in range(1, 16)]
+                     + [f'[a{i}] "v"(t[{i}])' for i in range(GT_MAX)])
+    lines.append(f"#define LH_INV_JUMPG_INS(tl, th, t) {gins}")
+    lines += render_chain_table()
+    for n in range(1, GT_MAX + 1):
+        lines += render_chain_call(n)
     return "\n".join(lines) + "\n"
 
 
