@@ -148,7 +148,9 @@ struct Device {
     // host-batch pipeline: per ring slot a stream, device buffers and an event
     std::mutex pipe_mu;
     hipStream_t pipe_stream[3] = {nullptr, nullptr, nullptr};
-    DevBuf pipe_blocks[3], pipe_out[3], pipe_rows[3], pipe_rows0[3], pipe_status[3];
+    hipEvent_t pipe_meta_ev = nullptr;  // decode: the call's rows are on the device
+    DevBuf pipe_blocks[3], pipe_out[3];
+    DevBuf pipe_rows, pipe_rows0, pipe_status;  // decode: the whole call's rows / status
     HostPinned pipe_meta;  // decode: the call's Block.row bytes and status, pinned
 };
 
@@ -699,21 +701,31 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
         (void)hipGetLastError();
         kernel_wb = false;
     }
-    for (int i = 0; i < 3; ++i) {
-        LH_HIP(d->pipe_blocks[i].reserve((size_t)chunk * sz));
-        LH_HIP(d->pipe_rows[i].reserve((size_t)chunk * k));
-        if (kernel_wb) LH_HIP(d->pipe_rows0[i].reserve((size_t)chunk * k));
-        LH_HIP(d->pipe_status[i].reserve((size_t)chunk));
-    }
-    // The rows and status travel through pinned staging: a copy into pageable memory (numpy
-    // arrays, the status vector callers typically allocate) is synchronous, and one per
-    // chunk serialised the whole pipeline -- every chunk's H2D waited for the previous
-    // chunk's kernels and write-back (decode 48 GB/s against 56 for the encode;
-    // profiles/r3_pcie_timeline.txt).
-    LH_HIP(d->pipe_meta.reserve((size_t)stripes * k + (size_t)stripes));
+    for (int i = 0; i < 3; ++i) LH_HIP(d->pipe_blocks[i].reserve((size_t)chunk * sz));
+    // The Block.row bytes and the status travel once per call, not per chunk: one copy in
+    // (plus the device-side copy of the original rows the write-back kernel reads) before
+    // the first chunk, one copy out after the last.  Per chunk, 3-4 small copies beside the
+    // stripe data cost ~90 us each in the pipeline (profiles/r3l_pcie_chunk_sweep.json:
+    // k29/m4 decode 48.0 GB/s at 1 024 stripes per chunk, 52.1 at 7 140) and kept the
+    // chunks large, so the last chunk's kernels and write-back ran with the link idle.
+    // Through pinned staging: a copy from pageable memory (numpy arrays, the status vector
+    // callers typically allocate) is synchronous (profiles/r3_pcie_timeline.txt).
+    const size_t nrows = (size_t)stripes * k;
+    LH_HIP(d->pipe_rows.reserve(nrows));
+    if (kernel_wb) LH_HIP(d->pipe_rows0.reserve(nrows));
+    LH_HIP(d->pipe_status.reserve((size_t)stripes));
+    LH_HIP(d->pipe_meta.reserve(nrows + (size_t)stripes));
+    if (!d->pipe_meta_ev) LH_HIP(hipEventCreateWithFlags(&d->pipe_meta_ev, hipEventDisableTiming));
     uint8_t *prows = d->pipe_meta.ptr;
-    int8_t *pstatus = (int8_t *)(prows + (size_t)stripes * k);
-    std::memcpy(prows, h_rows, (size_t)stripes * k);
+    int8_t *pstatus = (int8_t *)(prows + nrows);
+    std::memcpy(prows, h_rows, nrows);
+    {
+        hipStream_t st0 = d->pipe_stream[0];
+        LH_HIP(hipMemcpyAsync(d->pipe_rows.ptr, prows, nrows, hipMemcpyHostToDevice, st0));
+        if (kernel_wb) LH_HIP(hipMemcpyAsync(d->pipe_rows0.ptr, d->pipe_rows.ptr, nrows, hipMemcpyDeviceToDevice, st0));
+        LH_HIP(hipEventRecord(d->pipe_meta_ev, st0));
+        for (int i = 1; i < 3; ++i) LH_HIP(hipStreamWaitEvent(d->pipe_stream[i], d->pipe_meta_ev, 0));
+    }
     for (int s0 = 0, c = 0; s0 < stripes; s0 += chunk, ++c) {
         const int n = stripes - s0 < chunk ? stripes - s0 : chunk;
         const int i = c % 3;
@@ -736,11 +748,8 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
         }
         LH_HIP(hipMemcpy2DAsync(d->pipe_blocks[i].ptr, sz, h_blocks + (long long)s0 * stride, stride, sz, n,
                                 hipMemcpyHostToDevice, st));
-        LH_HIP(hipMemcpyAsync(d->pipe_rows[i].ptr, prows + (long long)s0 * k, (size_t)n * k, hipMemcpyHostToDevice, st));
-        if (kernel_wb)
-            LH_HIP(hipMemcpyAsync(d->pipe_rows0[i].ptr, d->pipe_rows[i].ptr, (size_t)n * k, hipMemcpyDeviceToDevice, st));
-        const int rc = decode_batch(k, m, bytes, n, d->pipe_blocks[i].ptr, sz, d->pipe_rows[i].ptr,
-                                    (int8_t *)d->pipe_status[i].ptr, st, true);
+        const int rc = decode_batch(k, m, bytes, n, d->pipe_blocks[i].ptr, sz, d->pipe_rows.ptr + (long long)s0 * k,
+                                    (int8_t *)d->pipe_status.ptr + s0, st, true);
         if (rc != kOk) return rc;
         if (kernel_wb) {
             WritebackArgs wa{};
@@ -748,7 +757,7 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
             wa.stride = sz;
             wa.host = h_dev + (long long)s0 * stride;
             wa.host_stride = stride;
-            wa.rows_orig = d->pipe_rows0[i].ptr;
+            wa.rows_orig = d->pipe_rows0.ptr + (long long)s0 * k;
             wa.k = k;
             wa.bytes = bytes;
             wa.stripes = n;
@@ -758,11 +767,11 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
             LH_HIP(hipMemcpy2DAsync(h_blocks + (long long)s0 * stride + off, stride, d->pipe_blocks[i].ptr + off, sz, w,
                                     n, hipMemcpyDeviceToHost, st));
         }
-        LH_HIP(hipMemcpyAsync(prows + (long long)s0 * k, d->pipe_rows[i].ptr, (size_t)n * k, hipMemcpyDeviceToHost, st));
-        LH_HIP(hipMemcpyAsync(pstatus + s0, d->pipe_status[i].ptr, n, hipMemcpyDeviceToHost, st));
     }
     for (auto s : d->pipe_stream) LH_HIP(hipStreamSynchronize(s));
-    std::memcpy(h_rows, prows, (size_t)stripes * k);
+    LH_HIP(hipMemcpy(prows, d->pipe_rows.ptr, nrows, hipMemcpyDeviceToHost));
+    LH_HIP(hipMemcpy(pstatus, d->pipe_status.ptr, (size_t)stripes, hipMemcpyDeviceToHost));
+    std::memcpy(h_rows, prows, nrows);
     if (h_status) std::memcpy(h_status, pstatus, (size_t)stripes);
     return kOk;
 }

@@ -283,8 +283,28 @@ __device__ __forceinline__ long long lh_block_id() {
 #else
 #define LH_OPS(w) "+v"((w).v[0]), "+v"((w).v[1]), "+v"((w).v[2]), "+v"((w).v[3])
 #endif
+// LH_PIN_WORDS (bit 0: decode phase A, bit 1: phase B, bit 2: everywhere): one asm
+// statement per word instead of per row.  The per-row statements let the register allocator
+// keep more copies live: the fused k29/m4 decode grew from 162 to 180 VGPRs (3 -> 2 waves
+// per SIMD) when they replaced the per-word ones.  Per-word pins cost build time only for
+// large column counts, so they are the default where the fused decode is compiled.
+#ifndef LH_PIN_WORDS
+#if (LH_K < LH_M ? LH_K : LH_M) <= 4 && LH_K <= 64
+#define LH_PIN_WORDS 1
+#else
+#define LH_PIN_WORDS 0
+#endif
+#endif
+__device__ __forceinline__ void lh_pin8w(lh_word (&a)[8]) {
+#pragma unroll
+    for (int y = 0; y < 8; ++y)
+#pragma unroll
+        for (int i = 0; i < LH_NW; ++i) asm volatile("" : "+v"(a[y].v[i]));
+}
 __device__ __forceinline__ void lh_pin8(lh_word (&a)[8]) {
-#if LH_NW <= 3
+#if LH_PIN_WORDS & 4
+    lh_pin8w(a);
+#elif LH_NW <= 3
     asm volatile("" : LH_OPS(a[0]), LH_OPS(a[1]), LH_OPS(a[2]), LH_OPS(a[3]), LH_OPS(a[4]), LH_OPS(a[5]),
                  LH_OPS(a[6]), LH_OPS(a[7]));
 #else
@@ -296,6 +316,17 @@ __device__ __forceinline__ void lh_pin8(lh_word (&a)[8]) {
 __device__ __forceinline__ void lh_opaque(lh_word (&acc)[LH_M][8]) {
 #pragma unroll
     for (int r = 0; r < LH_M; ++r) lh_pin8(acc[r]);
+}
+// Decode phase A's pins (LH_PIN_WORDS & 1: one statement per word).
+__device__ __forceinline__ void lh_dopaque(lh_word (&acc)[LH_M][8]) {
+#pragma unroll
+    for (int r = 0; r < LH_M; ++r) {
+#if LH_PIN_WORDS & 1
+        lh_pin8w(acc[r]);
+#else
+        lh_pin8(acc[r]);
+#endif
+    }
 }
 
 // Encode column source of a lane: with LH_BUF one buffer resource over the wave's stripes
@@ -427,9 +458,8 @@ __device__ __forceinline__ void lh_load_packed(unsigned int (&w)[N], const unsig
 
 #define LH_BYTE(w, idx) (((w)[(idx) / 4] >> (8 * ((idx) % 4))) & 0xFFu)
 
-// Phase A streams LH_K data columns (erased ones read as zeros) and then the LH_M recovery
-// rows (absent ones read as zeros) through one prefetch ring, so the recovery loads are in
-// flight while the last data columns combine.
+// Phase A streams the LH_M recovery rows (absent ones read as zeros) and the LH_K data
+// columns (erased ones read as zeros) through one prefetch ring (order: LH_REC_FIRST).
 #define LH_DCOLS (LH_K + LH_M)
 #ifndef LH_PF_DEC
 #define LH_PF_DEC 1  // decode prefetch depth (tools/tune.py, fused plan: 1 >= 2 > 3)
@@ -488,21 +518,37 @@ __device__ __forceinline__ void lh_load_col(lh_word (&d)[8], const lh_dsrc &S, u
 }
 #endif
 
-// Slot of decode column X: the slot holding original X (X < k) or recovery row X - k.
+// Column order of phase A.  LH_REC_FIRST = 1: the m recovery rows first, then the k data
+// columns.  The outputs overwrite the recovery slots; read last, those lines are still in
+// L2 when the stores arrive, and in-place stores into L2-resident clean lines measured
+// slower than into lines long evicted (tools/ubench_decode.hip, k29/m4 access pattern:
+// 0.613 ms recovery rows last, 0.586 ms first, 0.574 ms into a separate buffer).
+#ifndef LH_REC_FIRST
+#define LH_REC_FIRST 1
+#endif
+// Decode column X in stream order: data column x (the slot holding original x) or
+// recovery row r.
+template <int X>
+struct lh_dcol {
+    static constexpr bool rec = LH_REC_FIRST ? (X < LH_M) : (X >= LH_K);
+    static constexpr int idx = LH_REC_FIRST ? (X < LH_M ? X : X - LH_M) : (X < LH_K ? X : X - LH_K);
+    static constexpr int x = rec ? 0 : (idx < LH_K ? idx : 0);
+    static constexpr int r = rec ? (idx < LH_M ? idx : 0) : 0;
+};
 template <int X>
 __device__ __forceinline__ unsigned int lh_dcol_slot(const unsigned int (&srcw)[LH_NSRC],
                                                      const unsigned int (&recw)[LH_NREC]) {
-    if (X < LH_K) return LH_BYTE(srcw, X < LH_K ? X : 0);
-    return LH_BYTE(recw, X >= LH_K ? X - LH_K : 0);
+    if (lh_dcol<X>::rec) return LH_BYTE(recw, lh_dcol<X>::r);
+    return LH_BYTE(srcw, lh_dcol<X>::x);
 }
 
 template <int X>
 __device__ __forceinline__ void lh_dcombine(lh_word (&acc)[LH_M][8], const lh_word (&d)[8]) {
-    if (X < LH_K) {
-        lh_column<(X < LH_K ? X : 0)>(acc, d);
-    } else {
+    if constexpr (lh_dcol<X>::rec) {
 #pragma unroll
-        for (int y = 0; y < 8; ++y) lh_xor(acc[X >= LH_K ? X - LH_K : 0][y], d[y]);
+        for (int y = 0; y < 8; ++y) lh_xor(acc[lh_dcol<X>::r][y], d[y]);
+    } else {
+        lh_column<lh_dcol<X>::x>(acc, d);
     }
 }
 
@@ -514,18 +560,18 @@ struct lh_unroll_decode {
         if (X + LH_PF_DEC < LH_DCOLS) {
             lh_word nxt[8];
 #if LH_BUF
-            lh_load_col<LH_NT_DEC == 1 || (LH_NT_DEC == 2 && X + LH_PF_DEC < LH_K)>(
+            lh_load_col<LH_NT_DEC == 1 || (LH_NT_DEC == 2 && !lh_dcol<(X + LH_PF_DEC < LH_DCOLS ? X + LH_PF_DEC : 0)>::rec)>(
                 nxt, S, lh_dcol_slot<(X + LH_PF_DEC < LH_DCOLS ? X + LH_PF_DEC : 0)>(srcw, recw));
 #else
             lh_load_col(nxt, S, lh_dcol_slot<(X + LH_PF_DEC < LH_DCOLS ? X + LH_PF_DEC : 0)>(srcw, recw));
 #endif
             lh_dcombine<X>(acc, ring[X % LH_PF_DEC]);
-            lh_opaque(acc);
+            lh_dopaque(acc);
 #pragma unroll
             for (int b = 0; b < 8; ++b) ring[X % LH_PF_DEC][b] = nxt[b];
         } else {
             lh_dcombine<X>(acc, ring[X % LH_PF_DEC]);
-            lh_opaque(acc);
+            lh_dopaque(acc);
         }
         lh_unroll_decode<X + 1>::run(acc, ring, S, srcw, recw);
     }
@@ -559,7 +605,7 @@ __device__ __forceinline__ void lh_dec_issue(lh_word (&ring)[LH_PF_DEC][8], cons
                                 : (q == 2) ? lh_dcol_slot<2>(pr.srcw, pr.recw)
                                            : lh_dcol_slot<3>(pr.srcw, pr.recw);
 #if LH_BUF
-        lh_load_col<LH_NT_DEC != 0>(ring[q], S, slot);  // the first columns are data columns
+        lh_load_col<LH_NT_DEC == 1 || (LH_NT_DEC == 2 && !LH_REC_FIRST)>(ring[q], S, slot);
 #else
         lh_load_col(ring[q], S, slot);
 #endif
@@ -627,7 +673,11 @@ __device__ __forceinline__ void lh_dec_phase_b(const lh_word (&v)[LH_M][8], cons
 #pragma unroll
                         for (int q = 0; q < LH_NW; ++q) o[y].v[q] = lh_xand(o[y].v[q], v[r][y].v[q], mask);
                 }
+#if LH_PIN_WORDS & 2
+                lh_pin8w(o);
+#else
                 lh_pin8(o);
+#endif
             }
             unsigned char *dst = base + (long long)LH_BYTE(outw, i) * LH_BYTES;
 #pragma unroll

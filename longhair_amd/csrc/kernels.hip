@@ -1019,25 +1019,11 @@ __device__ __forceinline__ void lh_mul_jump_g(uint32_t (&acc)[8][8], const uint3
 #undef LH_GT_CASE
 }
 
-template <int N>
-__device__ __forceinline__ void lh_mul_chain(uint32_t (&acc)[8][8], const uint32_t (&tl)[16],
-                                             const uint32_t (&th)[16], const uint32_t (&t)[8], int r,
-                                             uint32_t hi) {
-#define LH_CH_CASE(n)                                                                                        \
-    if constexpr (N == n)                                                                                    \
-        asm volatile(LH_INV_JUMPC##n##_ASM : LH_INV_JUMPC##n##_OUTS(acc) : LH_INV_JUMPC##n##_INS(tl, th, t), \
-                     [r] "s"(r), [hi] "s"(hi) : LH_INV_JUMPC##n##_CLOBBER, "s92", "s93", "s94", "s95", "s96",  \
-                     "s97", "scc");
-    LH_CH_CASE(1) LH_CH_CASE(2) LH_CH_CASE(3) LH_CH_CASE(4) LH_CH_CASE(5) LH_CH_CASE(6) LH_CH_CASE(7)
-    LH_CH_CASE(8)
-#undef LH_CH_CASE
-}
-
 // Same staging as lh_inverse_dma_body (double-buffered LDS-DMA tiles); the multiply jumps
 // into lh_inv_gtab.  Outputs: PACK ? wave g recovers outputs 8g .. 8g + 7 (fewer waves build
 // the row tables) : g, g + nw, ... as in lh_inverse_dma_body.  The row loop is instantiated
 // per output count (1..8, wave-uniform) so no slot jumps for an unused output.
-template <int TILE, bool CH>
+template <int TILE>
 __device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uint32_t *__restrict__ lvA,
                                                    uint32_t *__restrict__ lvB, uint32_t tlo, uint32_t thi) {
     const int nw = (int)(blockDim.x >> 6);
@@ -1067,7 +1053,7 @@ __device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uin
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const uint32_t c = (rslot != 0xFFu && i < nout) ? cf[out_of(i) * m + lane] : 0u;
-            t[i] = tlo + c * (CH ? 84u : 68u);
+            t[i] = tlo + c * 68u;
         }
     }
     auto issue = [&](unsigned long long rest, uint32_t *buf) {
@@ -1114,8 +1100,7 @@ __device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uin
                         tl[q] = pre ? (tl[pre] ^ v[low]) : v[low];
                         th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];
                     }
-                    if constexpr (CH) lh_mul_chain<N>(acc, tl, th, t, r, thi);
-                    else lh_mul_jump_g<N>(acc, tl, th, t, r, thi);
+                    lh_mul_jump_g<N>(acc, tl, th, t, r, thi);
                 }
             }
         };
@@ -1176,39 +1161,7 @@ __global__ void __launch_bounds__(1024) lh_inverse_gt_kernel(lh::InverseArgs a) 
         lh_inverse_dma_body<8, TILE, true>(a, lvA, lvB);
         return;
     }
-    lh_inverse_gt_body<TILE, false>(a, lvA, lvB, tlo, thi);
-}
-
-// ---- chained bodies (round 3): a body jumps straight to the next output's body instead of
-// returning (tools/gen_inv_jump.py render_chain_table): one branch and two SALU per
-// (output, row).  The row's code and the table must share the high word of their addresses
-// (checked here with the kernel's own PC; otherwise, or with a.jump_fallback, the in-asm
-// table runs).
-__global__ void lh_inv_ctab_holder() { asm volatile(LH_INV_CTAB_TEXT); }
-
-template <int TILE>
-__global__ void __launch_bounds__(1024) lh_inverse_ch_kernel(lh::InverseArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t lvA[TILE * 8 * 64];
-    __shared__ __attribute__((aligned(16))) uint32_t lvB[TILE * 8 * 64];
-    uint32_t tlo, thi, plo, phi;
-    asm volatile(
-        "s_getpc_b64 s[92:93]\n"
-        "s_mov_b32 %2, s92\n"
-        "s_mov_b32 %3, s93\n"
-        "s_add_u32 s92, s92, lh_inv_ctab@rel32@lo+4\n"
-        "s_addc_u32 s93, s93, lh_inv_ctab@rel32@hi+12\n"
-        "s_mov_b32 %0, s92\n"
-        "s_mov_b32 %1, s93\n"
-        : "=s"(tlo), "=s"(thi), "=s"(plo), "=s"(phi)
-        :
-        : "s92", "s93", "scc");
-    // this kernel's code lies within 1 MiB of plo
-    if (a.jump_fallback || phi != thi || tlo > 0xFFFFFFFFu - 256u * 84u || plo < (1u << 20) ||
-        plo > 0xFFFFFFFFu - (1u << 20)) {
-        lh_inverse_dma_body<8, TILE, true>(a, lvA, lvB);
-        return;
-    }
-    lh_inverse_gt_body<TILE, true>(a, lvA, lvB, tlo, thi);
+    lh_inverse_gt_body<TILE>(a, lvA, lvB, tlo, thi);
 }
 
 // One inlined table per output (JO <= 4 copies of 17 KiB).
@@ -1373,25 +1326,19 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     const char *dm = std::getenv("LONGHAIR_AMD_INV_DMA");
     const int dma_rows = dm ? std::atoi(dm) : 8;
     // LONGHAIR_AMD_INV_JUMP = 10: the DMA staging with the per-code-object table
-    // (lh_inverse_gt_kernel), 11: its chained form (lh_inverse_ch_kernel);
+    // (lh_inverse_gt_kernel).  (A chained form, each body jumping straight to the next
+    // output's body, was measured in round 3 and removed: a GPU test process running it did
+    // not exit after its tests passed.)
     // LONGHAIR_AMD_INV_PACK = 1 packs 8 consecutive outputs per wave,
     // LONGHAIR_AMD_INV_FALLBACK = 1 forces the in-asm-table path inside that kernel (tests).
-    if ((jp == 10 || jp == 11) && (dma_rows == 8 || dma_rows == 16)) {
+    if (jp == 10 && (dma_rows == 8 || dma_rows == 16)) {
         InverseArgs g = a;
         const char *pk = std::getenv("LONGHAIR_AMD_INV_PACK");
         const char *fb = std::getenv("LONGHAIR_AMD_INV_FALLBACK");
         g.pack = pk && std::atoi(pk) ? 1 : 0;
         g.jump_fallback = fb && std::atoi(fb) ? 1 : 0;
         const dim3 block(64u * (unsigned)((a.e_max + 7) / 8));
-        if (jp == 11) {
-            if (dma_rows == 8) {
-                hipLaunchKernelGGL((lh_inverse_ch_kernel<8>), grid, block, 0, st, g);
-                note_launch(g.jump_fallback ? "lh_inverse_ch_kernel<8>(fallback)" : "lh_inverse_ch_kernel<8>");
-            } else {
-                hipLaunchKernelGGL((lh_inverse_ch_kernel<16>), grid, block, 0, st, g);
-                note_launch(g.jump_fallback ? "lh_inverse_ch_kernel<16>(fallback)" : "lh_inverse_ch_kernel<16>");
-            }
-        } else if (dma_rows == 8) {
+        if (dma_rows == 8) {
             hipLaunchKernelGGL((lh_inverse_gt_kernel<8>), grid, block, 0, st, g);
             note_launch(g.jump_fallback ? "lh_inverse_gt_kernel<8>(fallback)" : "lh_inverse_gt_kernel<8>");
         } else {

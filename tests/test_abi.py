@@ -116,10 +116,9 @@ def test_inv_jump_table_is_generated():
     spec.loader.exec_module(gen)
     committed = open(os.path.join(REPO, "longhair_amd", "csrc", "inv_jump.inc")).read()
     assert committed == gen.render()
-    # five tables (per-output copies; indexed for 4 and for 8 outputs; global; chained) of 256 bodies of
+    # four tables (per-output copies; indexed for 4 and for 8 outputs; global) of 256 bodies of
     # 8 v_bitop3_b32 + a branch or return: the fixed 68-byte stride the jump assumes
-    assert committed.count("v_bitop3_b32") == 5 * 256 * 8  # per-output, indexed JO 4 / 8, global, chained
+    assert committed.count("v_bitop3_b32") == 4 * 256 * 8  # per-output, indexed JO 4 / 8, global
     assert committed.count("s_branch 3f") == 256
-    assert committed.count("s_setpc_b64 s[94:95]") == 4 * 256 + 8  # + the chained rows' entry jumps
+    assert committed.count("s_setpc_b64 s[94:95]") == 3 * 256
     assert committed.count("lh_inv_gtab:") == 1 and committed.count("s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)") == 8
-    assert committed.count("lh_inv_ctab:") == 1 and committed.count("s_add_u32 m0, m0, 9") == 256

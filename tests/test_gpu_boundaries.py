@@ -108,13 +108,6 @@ PHASE_B = [
     ({"LONGHAIR_AMD_INV_JUMP": "10", "LONGHAIR_AMD_INV_PACK": "1"}, 64, "lh_inverse_gt_kernel<8>"),
     ({"LONGHAIR_AMD_INV_JUMP": "10", "LONGHAIR_AMD_INV_DMA": "16"}, 33, "lh_inverse_gt_kernel<16>"),
     ({"LONGHAIR_AMD_INV_JUMP": "10", "LONGHAIR_AMD_INV_FALLBACK": "1"}, 33, "lh_inverse_gt_kernel<8>(fallback)"),
-    # chained bodies (each body jumps to the next output's)
-    ({"LONGHAIR_AMD_INV_JUMP": "11"}, 32, "lh_inverse_ch_kernel<8>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "11"}, 33, "lh_inverse_ch_kernel<8>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "11", "LONGHAIR_AMD_INV_PACK": "1"}, 32, "lh_inverse_ch_kernel<8>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "11", "LONGHAIR_AMD_INV_PACK": "1"}, 64, "lh_inverse_ch_kernel<8>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "11", "LONGHAIR_AMD_INV_DMA": "16"}, 33, "lh_inverse_ch_kernel<16>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "11", "LONGHAIR_AMD_INV_FALLBACK": "1"}, 33, "lh_inverse_ch_kernel<8>(fallback)"),
 ]
 
 

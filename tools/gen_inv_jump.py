@@ -103,57 +103,6 @@ def render_global_call(n):
     return lines
 
 
-# Chained variant (lh_inverse_ch_kernel): a body does not return to the row's code but jumps
-# straight to the next output's body.  Output i's registers are 9 apart: its body address
-# t[i] (lane r: row r) in v[CH_T + 9i], its accumulators in v[CH_T + 1 + 9i ..]; GPR
-# indexing on VSRC0 and VDST.  Body c: 8 v_bitop3_b32 on v[CH_T + 1 ..] (relative), then
-# m0 += 9 (the next output), v_readlane_b32 s94 <- v[CH_T] lane s96 (relative: t[i + 1] of
-# row s96), s_setpc_b64 s[94:95].  The row's code puts its own return address in the slot
-# after the last output, so the last body jumps back: 1 branch and 2 SALU per output.
-CH_TL, CH_TH, CH_T = 8, 23, 39
-CH_BODY = 84
-
-
-def render_chain_table():
-    """Asm text of LH_INV_CTAB_TEXT: s_endpgm, then the 256 chained bodies (84 bytes each)."""
-    body = ["s_endpgm", ".p2align 8", ".hidden lh_inv_ctab", ".globl lh_inv_ctab", "lh_inv_ctab:"]
-    for c in range(256):
-        v = c
-        for y in range(8):
-            lo, hi = v & 15, v >> 4
-            a = f"v{CH_T + 1 + y}"
-            s1 = f"v{CH_TL + lo}" if lo else "0"
-            s2 = f"v{CH_TH + hi}" if hi else "0"
-            body.append(f"v_bitop3_b32 {a}, {a}, {s1}, {s2} bitop3:0x96")
-            v = xt(v)
-        body += ["s_add_u32 m0, m0, 9", "s_nop 0", f"v_readlane_b32 s94, v{CH_T}, s96", "s_setpc_b64 s[94:95]"]
-    lines = ["#define LH_INV_CTAB_TEXT \\"]
-    for i, b in enumerate(body):
-        lines.append(f'    "{b}\\n"' + (" \\" if i + 1 < len(body) else ""))
-    return lines
-
-
-def render_chain_call(n):
-    """Asm text of LH_INV_JUMPC<n>_ASM: one row through outputs 0 .. n-1.  Operands: [r] the
-    row (SGPR), [hi] the high word shared by the table and this code (SGPR), the pinned
-    tables, body addresses and accumulators (not named)."""
-    body = ["s_mov_b32 s97, m0", "s_mov_b32 s96, %[r]", "s_mov_b32 s95, %[hi]", "s_getpc_b64 s[92:93]", "1:",
-            "s_add_u32 s92, s92, (2f-1b)", f"v_mov_b32 v{CH_T + 9 * n}, s92", f"v_readlane_b32 s94, v{CH_T}, s96",
-            "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)", "s_nop 0", "s_setpc_b64 s[94:95]", "2:",
-            "s_set_gpr_idx_off", "s_mov_b32 m0, s97"]
-    lines = [f"#define LH_INV_JUMPC{n}_ASM \\"]
-    for i, b in enumerate(body):
-        lines.append(f'    "{b}\\n"' + (" \\" if i + 1 < len(body) else ""))
-    outs = ", ".join(f'"+{{v{CH_T + 1 + 9 * i + y}}}"(acc[{i}][{y}])' for i in range(n) for y in range(8))
-    lines.append(f"#define LH_INV_JUMPC{n}_OUTS(acc) {outs}")
-    ins = ", ".join([f'"{{v{CH_TL + q}}}"(tl[{q}])' for q in range(1, 16)]
-                    + [f'"{{v{CH_TH + q}}}"(th[{q}])' for q in range(1, 16)]
-                    + [f'"{{v{CH_T + 9 * i}}}"(t[{i}])' for i in range(n)])
-    lines.append(f"#define LH_INV_JUMPC{n}_INS(tl, th, t) {ins}")
-    lines.append(f'#define LH_INV_JUMPC{n}_CLOBBER "v{CH_T + 9 * n}"')
-    return lines
-
-
 def render():
     """The text of inv_jump.inc."""
     lines = ["// generated by tools/gen_inv_jump.py -- do not edit",
@@ -188,9 +137,6 @@ def render():
                      + [f'"{{v{GT_TH + q}}}"(th[{q}])' for q in range(1, 16)]
                      + [f'[a{i}] "v"(t[{i}])' for i in range(GT_MAX)])
     lines.append(f"#define LH_INV_JUMPG_INS(tl, th, t) {gins}")
-    lines += render_chain_table()
-    for n in range(1, GT_MAX + 1):
-        lines += render_chain_call(n)
     return "\n".join(lines) + "\n"
 
 
