@@ -638,6 +638,24 @@ static int auto_chunk(long long stripe_bytes, int stripes, int chunk, bool decod
     return (int)(c < stripes ? c : stripes);
 }
 
+// Chunk sizes of one pipelined call.  The last chunk's kernels and copy back run with the
+// host-to-device link idle, so with automatic sizing the final stretch is cut into halving
+// chunks (down to 1/8 of the regular size): the tail shrinks from one regular chunk's
+// write-back (k29/m4 decode: ~0.7 ms of ~47) to a small one's, at the cost of a few more
+// chunks.  An explicit chunk size is used as given.
+static std::vector<int> chunk_list(int stripes, int chunk, bool tail) {
+    std::vector<int> v;
+    const int minc = std::max(1, chunk / 8);
+    for (int rem = stripes; rem > 0;) {
+        int n = rem < chunk ? rem : chunk;
+        if (tail && rem <= 2 * chunk && rem > minc) n = std::max((rem + 1) / 2, minc);
+        if (n > rem) n = rem;
+        v.push_back(n);
+        rem -= n;
+    }
+    return v;
+}
+
 static int host_encode_batch(int k, int m, int bytes, int stripes, const uint8_t *h_data, long long data_stride,
                              uint8_t *h_rec, long long rec_stride, int chunk) {
     if (k < 1 || m < 1 || bytes <= 0 || stripes < 0) return fail(kInvalid, "invalid k, m, block_bytes or stripes");
@@ -650,14 +668,16 @@ static int host_encode_batch(int k, int m, int bytes, int stripes, const uint8_t
     if (int rc = pipe_streams(d)) return rc;
     PipeDrain drain{d};
     const long long in_sz = (long long)k * bytes, out_sz = (long long)m * bytes;
+    const bool tail = chunk <= 0;
     chunk = auto_chunk(in_sz + out_sz, stripes, chunk);
+    const std::vector<int> sizes = chunk_list(stripes, chunk, tail);
     for (int i = 0; i < 3; ++i) {
         LH_HIP(d->pipe_blocks[i].reserve((size_t)chunk * in_sz));
         LH_HIP(d->pipe_out[i].reserve((size_t)chunk * out_sz));
     }
     int rc_all = kOk;
-    for (int s0 = 0, c = 0; s0 < stripes; s0 += chunk, ++c) {
-        const int n = stripes - s0 < chunk ? stripes - s0 : chunk;
+    for (int s0 = 0, c = 0; c < (int)sizes.size(); s0 += sizes[c], ++c) {
+        const int n = sizes[c];
         const int i = c % 3;
         hipStream_t st = d->pipe_stream[i];
         LH_HIP(hipMemcpy2DAsync(d->pipe_blocks[i].ptr, in_sz, h_data + (long long)s0 * data_stride, data_stride, in_sz,
@@ -684,7 +704,9 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
     if (int rc = pipe_streams(d)) return rc;
     PipeDrain drain{d};
     const long long sz = (long long)k * bytes;
+    const bool tail = chunk <= 0;
     chunk = auto_chunk(sz, stripes, chunk, true);
+    const std::vector<int> sizes = chunk_list(stripes, chunk, tail);
     // Only the slots decode can write travel back: the recovery slots (for m == 1 the
     // last one, or slot 0 when there is none: cauchy_decode_m1's quirk).  For k, m > 1 a
     // kernel writes exactly those blocks into the caller's pinned buffer through its
@@ -726,8 +748,8 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
         LH_HIP(hipEventRecord(d->pipe_meta_ev, st0));
         for (int i = 1; i < 3; ++i) LH_HIP(hipStreamWaitEvent(d->pipe_stream[i], d->pipe_meta_ev, 0));
     }
-    for (int s0 = 0, c = 0; s0 < stripes; s0 += chunk, ++c) {
-        const int n = stripes - s0 < chunk ? stripes - s0 : chunk;
+    for (int s0 = 0, c = 0; c < (int)sizes.size(); s0 += sizes[c], ++c) {
+        const int n = sizes[c];
         const int i = c % 3;
         hipStream_t st = d->pipe_stream[i];
         int lo = k, hi = -1;  // slot range [lo, hi] decode may write in this chunk

@@ -1331,11 +1331,15 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     // not exit after its tests passed.)
     // LONGHAIR_AMD_INV_PACK = 1 packs 8 consecutive outputs per wave,
     // LONGHAIR_AMD_INV_FALLBACK = 1 forces the in-asm-table path inside that kernel (tests).
-    if (jp == 10 && (dma_rows == 8 || dma_rows == 16)) {
+    // Default since the end of round 3 (no LONGHAIR_AMD_INV_JUMP): this kernel, outputs
+    // packed 8 per wave for e_max <= 32 and spread above (profiles/r3m_phase_b_gtab.txt, one
+    // box, two rounds: k128/m32 decode 3.56 -> 3.51-3.52 ms packed, k200/m56 0.583-0.584 ->
+    // 0.567-0.568 spread, against lh_inverse_dma_kernel<8,8,true>).
+    if ((jp == 10 || jpe == nullptr) && (dma_rows == 8 || dma_rows == 16)) {
         InverseArgs g = a;
         const char *pk = std::getenv("LONGHAIR_AMD_INV_PACK");
         const char *fb = std::getenv("LONGHAIR_AMD_INV_FALLBACK");
-        g.pack = pk && std::atoi(pk) ? 1 : 0;
+        g.pack = pk ? (std::atoi(pk) ? 1 : 0) : (a.e_max <= 32 ? 1 : 0);
         g.jump_fallback = fb && std::atoi(fb) ? 1 : 0;
         const dim3 block(64u * (unsigned)((a.e_max + 7) / 8));
         if (dma_rows == 8) {

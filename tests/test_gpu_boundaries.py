@@ -25,7 +25,7 @@ SMALL4 = ["lh_plan_small_kernel<4>", "lh_jit_decode"]
 SMALL8 = ["lh_plan_small_kernel<8>", "lh_jit_decode"]
 GENERIC_CF = ["lh_plan_kernel(closed form)", "lh_apply_generic_kernel", "lh_scatter_kernel"]
 GENERIC_S8 = ["lh_plan_small_kernel<8>", "lh_apply_generic_kernel", "lh_scatter_kernel"]
-WIDE16 = ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_dma_kernel<8,8,true>"]
+WIDE16 = ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_gt_kernel<8>"]
 WIDE64 = WIDE16  # (one phase-B kernel for every e_max since round 3)
 
 # (id, k, m, bytes, stripes, env, encode kernels, decode kernels)
@@ -95,13 +95,20 @@ PHASE_B = [
      "lh_inverse_ji_kernel<8,64,16,0>"),
     ({"LONGHAIR_AMD_INV_DMA": "0", "LONGHAIR_AMD_INV_JUMP": "9", "LONGHAIR_AMD_INV_BLK": "16",
       "LONGHAIR_AMD_INV_PF": "1"}, 33, "lh_inverse_ji_kernel<8,64,16,2>"),
-    # V staged by LDS-DMA into double-buffered tiles (default: 8 rows, indexed, 8 outputs)
-    ({"LONGHAIR_AMD_INV_DMA": "16"}, 32, "lh_inverse_dma_kernel<8,16,true>"),
-    ({"LONGHAIR_AMD_INV_DMA": "16"}, 33, "lh_inverse_dma_kernel<8,16,true>"),
+    # V staged by LDS-DMA into double-buffered tiles, in-asm tables: indexed 8 outputs per
+    # wave (the default until the end of round 3) or one inlined table per output
+    ({"LONGHAIR_AMD_INV_JUMP": "9"}, 32, "lh_inverse_dma_kernel<8,8,true>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "9"}, 33, "lh_inverse_dma_kernel<8,8,true>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "9", "LONGHAIR_AMD_INV_DMA": "16"}, 32, "lh_inverse_dma_kernel<8,16,true>"),
+    ({"LONGHAIR_AMD_INV_JUMP": "9", "LONGHAIR_AMD_INV_DMA": "16"}, 33, "lh_inverse_dma_kernel<8,16,true>"),
     ({"LONGHAIR_AMD_INV_JUMP": "4"}, 32, "lh_inverse_dma_kernel<4,8,false>"),
     ({"LONGHAIR_AMD_INV_JUMP": "4"}, 33, "lh_inverse_dma_kernel<4,8,false>"),
     ({"LONGHAIR_AMD_INV_JUMP": "4", "LONGHAIR_AMD_INV_DMA": "16"}, 33, "lh_inverse_dma_kernel<4,16,false>"),
-    # one table per code object (lh_inv_gtab), outputs spread or packed 8 per wave
+    # one table per code object (lh_inv_gtab), outputs spread or packed 8 per wave (the
+    # default: packed for e_max <= 32, spread above; 16-row tiles by LONGHAIR_AMD_INV_DMA)
+    ({"LONGHAIR_AMD_INV_DMA": "16"}, 32, "lh_inverse_gt_kernel<16>"),
+    ({"LONGHAIR_AMD_INV_PACK": "0"}, 32, "lh_inverse_gt_kernel<8>"),
+    ({"LONGHAIR_AMD_INV_PACK": "1"}, 33, "lh_inverse_gt_kernel<8>"),
     ({"LONGHAIR_AMD_INV_JUMP": "10"}, 32, "lh_inverse_gt_kernel<8>"),
     ({"LONGHAIR_AMD_INV_JUMP": "10"}, 33, "lh_inverse_gt_kernel<8>"),
     ({"LONGHAIR_AMD_INV_JUMP": "10", "LONGHAIR_AMD_INV_PACK": "1"}, 32, "lh_inverse_gt_kernel<8>"),
