@@ -240,7 +240,10 @@ def _phase_b_kernel(k, m):
         return []
     e_max = min(k, m)
     jump_env = os.environ.get("LONGHAIR_AMD_INV_JUMP")
-    if os.environ.get("LONGHAIR_AMD_INV_DMA", "8") in ("8", "16") and jump_env in (None, "4", "9"):
+    dma = os.environ.get("LONGHAIR_AMD_INV_DMA", "8") in ("8", "16")
+    if dma and jump_env in (None, "10"):
+        return ["lh_inverse_gt_kernel"]
+    if dma and jump_env in ("4", "9"):
         return ["lh_inverse_dma_kernel"]
     jump = jump_env or ("9" if e_max <= 32 else "4")
     if jump == "0" or (jump == "2" and e_max > 32):
