@@ -676,12 +676,22 @@ static int host_encode_batch(int k, int m, int bytes, int stripes, const uint8_t
         LH_HIP(d->pipe_out[i].reserve((size_t)chunk * out_sz));
     }
     int rc_all = kOk;
-    for (int s0 = 0, c = 0; c < (int)sizes.size(); s0 += sizes[c], ++c) {
+    const int nc = (int)sizes.size();
+    std::vector<long long> first(nc);
+    for (int c = 0, s0 = 0; c < nc; s0 += sizes[c], ++c) first[c] = s0;
+    auto h2d = [&](int c) {
+        return hipMemcpy2DAsync(d->pipe_blocks[c % 3].ptr, in_sz, h_data + first[c] * data_stride, data_stride, in_sz,
+                                sizes[c], hipMemcpyHostToDevice, d->pipe_stream[c % 3]);
+    };
+    LH_HIP(h2d(0));
+    for (int c = 0; c < nc; ++c) {
+        const long long s0 = first[c];
         const int n = sizes[c];
         const int i = c % 3;
         hipStream_t st = d->pipe_stream[i];
-        LH_HIP(hipMemcpy2DAsync(d->pipe_blocks[i].ptr, in_sz, h_data + (long long)s0 * data_stride, data_stride, in_sz,
-                                n, hipMemcpyHostToDevice, st));
+        // The next chunk's host-to-device copy is enqueued before this chunk's kernel and
+        // copy back (see host_decode_batch).
+        if (c + 1 < nc) LH_HIP(h2d(c + 1));
         const int rc = encode_batch(k, m, bytes, n, d->pipe_blocks[i].ptr, in_sz, d->pipe_out[i].ptr, out_sz, st, true);
         if (rc != kOk && rc != kInvalid) return rc;
         if (rc == kInvalid) rc_all = kInvalid;
@@ -748,10 +758,25 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
         LH_HIP(hipEventRecord(d->pipe_meta_ev, st0));
         for (int i = 1; i < 3; ++i) LH_HIP(hipStreamWaitEvent(d->pipe_stream[i], d->pipe_meta_ev, 0));
     }
-    for (int s0 = 0, c = 0; c < (int)sizes.size(); s0 += sizes[c], ++c) {
+    // Enqueue order: the host-to-device copy of chunk c + 1 before the kernels of chunk c.
+    // Streams beyond the device's hardware queues (GPU_MAX_HW_QUEUES, 4 by default) share
+    // one in FIFO order; enqueued after chunk c's write-back, chunk c + 1's copy on a stream
+    // sharing chunk c's queue waited for that write-back with the link idle (~0.75 ms, once
+    // every three chunks: rocprofv3 copy trace of tools/pcie_bench.py, session R).
+    const int nc = (int)sizes.size();
+    std::vector<long long> first(nc);
+    for (int c = 0, s0 = 0; c < nc; s0 += sizes[c], ++c) first[c] = s0;
+    auto h2d = [&](int c) {
+        return hipMemcpy2DAsync(d->pipe_blocks[c % 3].ptr, sz, h_blocks + first[c] * stride, stride, sz, sizes[c],
+                                hipMemcpyHostToDevice, d->pipe_stream[c % 3]);
+    };
+    LH_HIP(h2d(0));
+    for (int c = 0; c < nc; ++c) {
+        const long long s0 = first[c];
         const int n = sizes[c];
         const int i = c % 3;
         hipStream_t st = d->pipe_stream[i];
+        if (c + 1 < nc) LH_HIP(h2d(c + 1));
         int lo = k, hi = -1;  // slot range [lo, hi] decode may write in this chunk
         if (k > 1 && !kernel_wb) {
             for (int s = s0; s < s0 + n; ++s) {
@@ -768,8 +793,6 @@ static int host_decode_batch(int k, int m, int bytes, int stripes, uint8_t *h_bl
                 hi = last > hi ? last : hi;
             }
         }
-        LH_HIP(hipMemcpy2DAsync(d->pipe_blocks[i].ptr, sz, h_blocks + (long long)s0 * stride, stride, sz, n,
-                                hipMemcpyHostToDevice, st));
         const int rc = decode_batch(k, m, bytes, n, d->pipe_blocks[i].ptr, sz, d->pipe_rows.ptr + (long long)s0 * k,
                                     (int8_t *)d->pipe_status.ptr + s0, st, true);
         if (rc != kOk) return rc;

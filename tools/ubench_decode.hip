@@ -45,8 +45,8 @@ struct cols {
   }
 };
 
-// MODE 0 in place, 1 separate output buffer.
-template <int PF, int LAUX, int MODE>
+// MODE 0 in place, 1 separate output buffer; SAUX: cache policy of the in-place stores.
+template <int PF, int LAUX, int MODE, int SAUX = 2>
 __global__ void __launch_bounds__(256) dec_reg(uint8_t *__restrict__ in, uint8_t *__restrict__ out, long long in_stride,
                                                 const uint8_t *__restrict__ colmap, const uint8_t *__restrict__ outs,
                                                 int stripes) {
@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(256) dec_reg(uint8_t *__restrict__ in, uint8_t
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       const u32x2 v = acc[b] ^ u32x2{(uint32_t)r, 0};
-      if (MODE == 0) __builtin_amdgcn_raw_buffer_store_b64(v, rs, lbase + slot * BYTES + b * SUB, 0, 2);
+      if (MODE == 0) __builtin_amdgcn_raw_buffer_store_b64(v, rs, lbase + slot * BYTES + b * SUB, 0, SAUX);
       else __builtin_nontemporal_store(v, (u32x2 *)(out + s * (long long)(M * BYTES) + r * BYTES + b * SUB + p));
     }
   }
@@ -151,6 +151,11 @@ int main() {
     setup(true);
     run("reg recfirst inplace def PF1", dec_reg<1, 0, 0>);
     run("reg recfirst inplace def PF3", dec_reg<3, 0, 0>);
+    run("reg recfirst inplace st-def PF1", dec_reg<1, 0, 0, 0>);
+    run("reg recfirst inplace st-sc1 PF1", dec_reg<1, 0, 0, 16>);
+    run("reg recfirst inplace ld-nt PF1", dec_reg<1, 2, 0>);
+    setup(false);
+    run("reg inplace st-def PF1", dec_reg<1, 0, 0, 0>);
   }
   CK(hipGetLastError());
   return 0;
