@@ -127,7 +127,7 @@ bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
     cfg->win_pf = 3;
     if (const char *f = std::getenv("LONGHAIR_AMD_WIN_PF")) cfg->win_pf = std::max(1, std::atoi(f));
     cfg->win_lds = 1;
-    if (const char *l = std::getenv("LONGHAIR_AMD_WIN_LDS")) cfg->win_lds = std::atoi(l) ? 1 : 0;
+    if (const char *l = std::getenv("LONGHAIR_AMD_WIN_LDS")) cfg->win_lds = std::min(2, std::max(0, std::atoi(l)));
     if ((m + cfg->rows_per_wave - 1) / cfg->rows_per_wave > 16) return false;  // <= 1024 threads
     if (decode && m > 64) return false;  // the plan's used-row mask is one 64-lane ballot
     cfg->defines.clear();
@@ -159,8 +159,13 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
     // column crosses HBM once per workgroup, at 16 B per lane, instead of once per wave at
     // 4 B per lane (a 4-byte-lane stream reads at 4.1 TB/s against 6.3 for 16-byte lanes).
     const bool lds = c.win_lds != 0;
+    // c.win_lds == 2: every wave stages the whole column tile into a ring of its own (2 DMA
+    // instructions per column) and waits only for its own DMA: no workgroup barrier per
+    // column, twice the L2 -> LDS traffic and LDS.
+    const bool priv = c.win_lds == 2;
     const int NG = (m + R - 1) / R, D = PF + 1;
-    const int ndma = NG == 1 ? 2 : (g < 2 ? 1 : 0);  // DMA instructions per column, this wave
+    const int ndma = (NG == 1 || priv) ? 2 : (g < 2 ? 1 : 0);  // DMA instructions per column, this wave
+    const std::string toff = priv ? " + " + std::to_string(g * 2048) : "";  // this wave's ring slot
     const bool split = elim && c.win_split;  // V_r goes back in place of R_r (lh_inverse_kernel follows)
     os << "__device__ __forceinline__ void lh_wg" << g << "(" << (split ? "" : "const ") << "unsigned char *__restrict__ base, "
        << (elim ? "const unsigned char *__restrict__ zero, const unsigned int (&slv)[LH_NQ], unsigned int *__restrict__ lv"
@@ -180,14 +185,14 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
     };
     auto dma = [&](int x, const char *ind) {
         for (int h = 0; h < 2; ++h) {
-            if (!(NG == 1 || g == h)) continue;
-            os << ind << "lh_dma(" << dcol(x) << " + dof" << h << ", tile" << x % D << " + " << h * 1024 << ");\n";
+            if (!(NG == 1 || priv || g == h)) continue;
+            os << ind << "lh_dma(" << dcol(x) << " + dof" << h << ", tile" << x % D << toff << " + " << h * 1024 << ");\n";
         }
     };
     if (lds) {
         os << "  const int lane = threadIdx.x & 63;\n";
         for (int h = 0; h < 2; ++h)
-            if (NG == 1 || g == h)
+            if (NG == 1 || priv || g == h)
                 os << "  const unsigned int dof" << h << " = ((" << 64 * h << " + lane) >> 4) * " << c.sub
                    << "u + ((lane & 15) << 4);\n";
         for (int q = 0; q < PF && q < k; ++q) dma(q, "  ");
@@ -204,7 +209,7 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
         if (lds) {
             const int ahead = std::min(PF - 1, k - 1 - x);  // this wave's DMAs issued after column x
             if (ndma) os << "    lh_wait_vm(" << ndma * ahead << ");\n";
-            os << "    __builtin_amdgcn_s_barrier();\n";
+            if (!priv) os << "    __builtin_amdgcn_s_barrier();\n";
             if (x + PF < k) dma(x + PF, "    ");
         } else if (x + PF < k) {
             os << "    const unsigned char *cn = " << col(x + PF) << ";\n";
@@ -217,7 +222,7 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
             os << "    if (__builtin_amdgcn_readlane((int)slv[" << x / 64 << "], " << x % 64 << ") != 0xFF) {\n";
         if (lds)
             for (int b = 0; b < 8; ++b)
-                os << "    const unsigned int d0_" << b << " = ((const unsigned int *)(tile" << x % D << " + " << b * 256
+                os << "    const unsigned int d0_" << b << " = ((const unsigned int *)(tile" << x % D << toff << " + " << b * 256
                    << "))[lane];\n";
         // Which nibble-table entries (lo: sub-blocks 0..3, hi: 4..7) this group needs.
         bool need[2][16] = {};
@@ -442,7 +447,8 @@ static std::string win_source_for(const JitConfig &c) {
     // distinct objects apart, so reading tile x % D does not wait for the DMA into another.
     if (c.win_lds)
         for (int q = 0; q <= c.win_pf; ++q)
-            os << "__shared__ __attribute__((aligned(16))) unsigned char tile" << q << "[2048];\n";
+            os << "__shared__ __attribute__((aligned(16))) unsigned char tile" << q << "["
+               << (c.win_lds == 2 ? 2048 * NG : 2048) << "];\n";
     // LH_PINn: keep the accumulators in registers between columns (no re-association).
     // One asm statement per row (8 operands): every volatile asm is a memory side effect
     // to LLVM, and the IR sinking pass's cost grows with their number times the loads of
