@@ -552,34 +552,33 @@ __device__ __forceinline__ void lh_dcombine(lh_word (&acc)[LH_M][8], const lh_wo
     }
 }
 
-template <int X>
+template <int X, int PF>
 struct lh_unroll_decode {
-    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], lh_word (&ring)[LH_PF_DEC][8],
+    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], lh_word (&ring)[PF][8],
                                                const lh_dsrc &S, const unsigned int (&srcw)[LH_NSRC],
                                                const unsigned int (&recw)[LH_NREC]) {
-        if (X + LH_PF_DEC < LH_DCOLS) {
-            lh_word nxt[8];
-#if LH_BUF
-            lh_load_col<LH_NT_DEC == 1 || (LH_NT_DEC == 2 && !lh_dcol<(X + LH_PF_DEC < LH_DCOLS ? X + LH_PF_DEC : 0)>::rec)>(
-                nxt, S, lh_dcol_slot<(X + LH_PF_DEC < LH_DCOLS ? X + LH_PF_DEC : 0)>(srcw, recw));
-#else
-            lh_load_col(nxt, S, lh_dcol_slot<(X + LH_PF_DEC < LH_DCOLS ? X + LH_PF_DEC : 0)>(srcw, recw));
-#endif
-            lh_dcombine<X>(acc, ring[X % LH_PF_DEC]);
-            lh_dopaque(acc);
-#pragma unroll
-            for (int b = 0; b < 8; ++b) ring[X % LH_PF_DEC][b] = nxt[b];
+        if constexpr (X >= LH_DCOLS) {
+            return;
         } else {
-            lh_dcombine<X>(acc, ring[X % LH_PF_DEC]);
-            lh_dopaque(acc);
+            if (X + PF < LH_DCOLS) {
+                lh_word nxt[8];
+#if LH_BUF
+                lh_load_col<LH_NT_DEC == 1 || (LH_NT_DEC == 2 && !lh_dcol<(X + PF < LH_DCOLS ? X + PF : 0)>::rec)>(
+                    nxt, S, lh_dcol_slot<(X + PF < LH_DCOLS ? X + PF : 0)>(srcw, recw));
+#else
+                lh_load_col(nxt, S, lh_dcol_slot<(X + PF < LH_DCOLS ? X + PF : 0)>(srcw, recw));
+#endif
+                lh_dcombine<X>(acc, ring[X % PF]);
+                lh_dopaque(acc);
+#pragma unroll
+                for (int b = 0; b < 8; ++b) ring[X % PF][b] = nxt[b];
+            } else {
+                lh_dcombine<X>(acc, ring[X % PF]);
+                lh_dopaque(acc);
+            }
+            lh_unroll_decode<X + 1, PF>::run(acc, ring, S, srcw, recw);
         }
-        lh_unroll_decode<X + 1>::run(acc, ring, S, srcw, recw);
     }
-};
-template <>
-struct lh_unroll_decode<LH_DCOLS> {
-    __device__ __forceinline__ static void run(lh_word (&)[LH_M][8], lh_word (&)[LH_PF_DEC][8], const lh_dsrc &,
-                                               const unsigned int (&)[LH_NSRC], const unsigned int (&)[LH_NREC]) {}
 };
 
 // Per-stripe decode plan in registers: e, packed src/rec slot maps, coef, out slots.
@@ -596,10 +595,12 @@ struct lh_no_prep {
 // recovery row r.  Phase B: D_{E_i} = sum_r B(coef[i][r]) V_r with the per-stripe inverse,
 // by Horner over the coefficient bits: B(c) v = B(2)(...B(2)(c_7 v)...) + c_0 v.
 // `prep` runs while the first columns are in flight (the fused kernel solves its plan there).
-// Decode pieces.  Ring issue: the first LH_PF_DEC columns of a stripe group.
-__device__ __forceinline__ void lh_dec_issue(lh_word (&ring)[LH_PF_DEC][8], const lh_plan_regs &pr, const lh_dsrc &S) {
+// Decode pieces.  Ring issue: the first PF columns of a stripe group (PF <= 4).
+template <int PF>
+__device__ __forceinline__ void lh_dec_issue(lh_word (&ring)[PF][8], const lh_plan_regs &pr, const lh_dsrc &S) {
+    static_assert(PF >= 1 && PF <= 4, "decode prefetch depth");
 #pragma unroll
-    for (int q = 0; q < LH_PF_DEC; ++q) {
+    for (int q = 0; q < PF; ++q) {
         const unsigned int slot = (q == 0) ? lh_dcol_slot<0>(pr.srcw, pr.recw)
                                 : (q == 1) ? lh_dcol_slot<1>(pr.srcw, pr.recw)
                                 : (q == 2) ? lh_dcol_slot<2>(pr.srcw, pr.recw)
@@ -614,7 +615,8 @@ __device__ __forceinline__ void lh_dec_issue(lh_word (&ring)[LH_PF_DEC][8], cons
 
 // Phase A: V_r = R_r + sum_{x present} B(G[r][x]) D_x for every recovery row r, streaming
 // the ring (already issued) through all k + m columns.
-__device__ __forceinline__ void lh_dec_phase_a(lh_word (&v)[LH_M][8], lh_word (&ring)[LH_PF_DEC][8],
+template <int PF>
+__device__ __forceinline__ void lh_dec_phase_a(lh_word (&v)[LH_M][8], lh_word (&ring)[PF][8],
                                                const lh_plan_regs &pr, const lh_dsrc &S) {
 #pragma unroll
     for (int r = 0; r < LH_M; ++r)
@@ -622,7 +624,7 @@ __device__ __forceinline__ void lh_dec_phase_a(lh_word (&v)[LH_M][8], lh_word (&
         for (int y = 0; y < 8; ++y)
 #pragma unroll
             for (int i = 0; i < LH_NW; ++i) v[r][y].v[i] = 0;
-    lh_unroll_decode<0>::run(v, ring, S, pr.srcw, pr.recw);
+    lh_unroll_decode<0, PF>::run(v, ring, S, pr.srcw, pr.recw);
 }
 
 // Phase B: D_{E_i} = sum_r B(coef[i][r]) V_r with the per-stripe inverse, by Horner over
@@ -710,7 +712,7 @@ __device__ __forceinline__ lh_dsrc lh_make_dsrc(const lh_lane &l, long long wave
 
 // In-place erasure decode of one stripe group: ring issue, `prep` (the fused kernel
 // solves its plan there, while the first columns are in flight), phase A, phase B.
-template <class PREP>
+template <int PF, class PREP>
 __device__ __forceinline__ void lh_decode_body(const lh_lane &l, long long wave, unsigned char *__restrict__ blocks,
                                                long long stripe_stride, lh_plan_regs &pr,
                                                const unsigned char *__restrict__ zero_page, int stripes,
@@ -721,12 +723,12 @@ __device__ __forceinline__ void lh_decode_body(const lh_lane &l, long long wave,
 #if LH_PREP_FIRST
         prep(pr);  // solve before the first loads: the ring is not live across the solve
 #endif
-        lh_word ring[LH_PF_DEC][8];
-        lh_dec_issue(ring, pr, S);
+        lh_word ring[PF][8];
+        lh_dec_issue<PF>(ring, pr, S);
 #if !LH_PREP_FIRST
         prep(pr);
 #endif
-        lh_dec_phase_a(v, ring, pr, S);
+        lh_dec_phase_a<PF>(v, ring, pr, S);
     }
     lh_dec_phase_b(v, pr, blocks + l.stripe * stripe_stride + l.p);
 }
@@ -745,7 +747,7 @@ __device__ __forceinline__ void lh_decode_wave(long long wave, unsigned char *__
     lh_load_packed(pr.recw, pl + LH_P_REC);
     lh_load_packed(pr.coefw, pl + LH_P_COEF);
     lh_load_packed(pr.outw, pl + LH_P_OUT);
-    lh_decode_body(l, wave, blocks, stripe_stride, pr, zero_page, stripes, lh_no_prep());
+    lh_decode_body<LH_PF_DEC>(l, wave, blocks, stripe_stride, pr, zero_page, stripes, lh_no_prep());
 }
 
 #if 1
@@ -1028,10 +1030,12 @@ __device__ __forceinline__ void lh_fused_solve::operator()(lh_plan_regs &pr) con
 #ifndef LH_DEC_LB
 #define LH_DEC_LB 1  // min waves per SIMD the register allocator must allow (tools/tune.py)
 #endif
-extern "C" __global__ void __launch_bounds__(256, LH_DEC_LB)
-lh_jit_decode_fused(unsigned char *__restrict__ blocks, long long stripe_stride, unsigned char *__restrict__ rows,
-                    signed char *__restrict__ status, const unsigned char *__restrict__ zero_page,
-                    const unsigned char *__restrict__ gf_exp, const short *__restrict__ gf_log, int stripes) {
+template <int PF>
+__device__ __forceinline__ void lh_fused_body(unsigned char *__restrict__ blocks, long long stripe_stride,
+                                              unsigned char *__restrict__ rows, signed char *__restrict__ status,
+                                              const unsigned char *__restrict__ zero_page,
+                                              const unsigned char *__restrict__ gf_exp,
+                                              const short *__restrict__ gf_log, int stripes) {
     __shared__ unsigned char gexp[1024];  // exp(i mod 255) for i < 1024 (lh_inv_adj)
     __shared__ short glog[256];
     __shared__ __attribute__((aligned(16))) unsigned char scratch[4][LH_SPW > 0 ? LH_SPW : 1][LH_SR];
@@ -1054,7 +1058,28 @@ lh_jit_decode_fused(unsigned char *__restrict__ blocks, long long stripe_stride,
         unsigned int rowv[LH_NRW];
         lh_fused_rows(l, c, rows, rowv);
         if (l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr))
-            lh_decode_body(l, lh_w, blocks, stripe_stride, pr, zero_page, stripes, sv);
+            lh_decode_body<PF>(l, lh_w, blocks, stripe_stride, pr, zero_page, stripes, sv);
     }
+}
+
+extern "C" __global__ void __launch_bounds__(256, LH_DEC_LB)
+lh_jit_decode_fused(unsigned char *__restrict__ blocks, long long stripe_stride, unsigned char *__restrict__ rows,
+                    signed char *__restrict__ status, const unsigned char *__restrict__ zero_page,
+                    const unsigned char *__restrict__ gf_exp, const short *__restrict__ gf_log, int stripes) {
+    lh_fused_body<LH_PF_DEC>(blocks, stripe_stride, rows, status, zero_page, gf_exp, gf_log, stripes);
+}
+
+// The same decode with LH_PF_TAIL columns in flight, for a last partial round of waves: a
+// grid that does not fill whole rounds of resident waves ends with a few waves alone on the
+// chip, each waiting one memory round trip per column at depth 1 (codec.cpp launches the
+// stripes past the last whole round with this kernel).
+#ifndef LH_PF_TAIL
+#define LH_PF_TAIL 3
+#endif
+extern "C" __global__ void __launch_bounds__(256, 1)
+lh_jit_decode_fused_tail(unsigned char *__restrict__ blocks, long long stripe_stride, unsigned char *__restrict__ rows,
+                         signed char *__restrict__ status, const unsigned char *__restrict__ zero_page,
+                         const unsigned char *__restrict__ gf_exp, const short *__restrict__ gf_log, int stripes) {
+    lh_fused_body<LH_PF_TAIL>(blocks, stripe_stride, rows, status, zero_page, gf_exp, gf_log, stripes);
 }
 #endif  // LH_EMAX <= 4 && LH_NCH <= 64 && LH_K <= 64

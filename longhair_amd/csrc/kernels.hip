@@ -1237,6 +1237,9 @@ __global__ void __launch_bounds__(1024) lh_inverse_kernel(lh::InverseArgs a) {
 // the slots decode may have written (its outputs; an invalid stripe is untouched, so the
 // copy is the host's own bytes).  16 B per lane when the block size allows, else 8 B
 // (bytes % 8 == 0 for m > 1).  Vector stores over PCIe into the mapped host buffer.
+// Grid: x = stripe, y = segment of the block (large blocks are split over gridDim.y
+// workgroups, so a chunk of a few large stripes -- the pipeline's last, k200/m56: 2 stripes --
+// still has enough workgroups writing over the link: one per stripe took 0.31 ms for 7 MB).
 __global__ void __launch_bounds__(256) lh_writeback_kernel(lh::WritebackArgs a) {
     const long long s = blockIdx.x;
     if (s >= a.stripes) return;
@@ -1244,14 +1247,17 @@ __global__ void __launch_bounds__(256) lh_writeback_kernel(lh::WritebackArgs a) 
     const uint8_t *src = a.blocks + s * a.stride;
     uint8_t *dst = a.host + s * a.host_stride;
     const bool wide = ((a.bytes | a.host_stride | (long long)(uintptr_t)a.host) & 15) == 0;
+    const int unit = wide ? 16 : 8, n = a.bytes / unit;  // lanes' units per block
+    const int per = (n + (int)gridDim.y - 1) / (int)gridDim.y;
+    const int q0 = (int)blockIdx.y * per, q1 = q0 + per < n ? q0 + per : n;
     for (int j = 0; j < a.k; ++j) {
         if (rows[j] < a.k) continue;  // workgroup-uniform
         const long long off = (long long)j * a.bytes;
         if (wide) {
-            for (int q = threadIdx.x; q < (a.bytes >> 4); q += blockDim.x)
+            for (int q = q0 + (int)threadIdx.x; q < q1; q += blockDim.x)
                 ((uint4 *)(dst + off))[q] = ((const uint4 *)(src + off))[q];
         } else {
-            for (int q = threadIdx.x; q < (a.bytes >> 3); q += blockDim.x)
+            for (int q = q0 + (int)threadIdx.x; q < q1; q += blockDim.x)
                 ((uint2 *)(dst + off))[q] = ((const uint2 *)(src + off))[q];
         }
     }
@@ -1404,7 +1410,11 @@ hipError_t launch_writeback(const WritebackArgs &a, hipStream_t st) {
     // 8-byte lanes need 8-byte aligned blocks on the host side (16-byte lanes when aligned)
     if (((a.bytes | a.host_stride | (long long)(uintptr_t)a.host) & 7) != 0 || a.k < 1 || a.k > 255)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(lh_writeback_kernel, dim3((unsigned)a.stripes), dim3(256), 0, st, a);
+    // One segment per 4 KiB of block (256 lanes x 16 B), at most 16, and only while the
+    // chunk has fewer than 1 024 stripes.
+    int seg = a.stripes >= 1024 ? 1 : a.bytes / 4096;
+    seg = seg < 1 ? 1 : (seg > 16 ? 16 : seg);
+    hipLaunchKernelGGL(lh_writeback_kernel, dim3((unsigned)a.stripes, (unsigned)seg), dim3(256), 0, st, a);
     note_launch("lh_writeback_kernel");
     return hipGetLastError();
 }
