@@ -416,10 +416,10 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         // 21 846 waves over 3 072 slots) leaves its last waves alone on the chip, each
         // waiting one memory round trip per column at prefetch depth 1.  Those stripes go to
         // lh_jit_decode_fused_tail (3 columns in flight) after the whole rounds
-        // (LONGHAIR_AMD_DEC_TAIL=0 disables the split).
+        // (LONGHAIR_AMD_DEC_TAIL=1; off by default until measured).
         int n_main = stripes;
         const char *te = std::getenv("LONGHAIR_AMD_DEC_TAIL");
-        if (jk->decode_fused_tail && cfg.spw > 0 && !(te && std::atoi(te) == 0) &&
+        if (jk->decode_fused_tail && cfg.spw > 0 && te && std::atoi(te) != 0 &&
             std::getenv("LONGHAIR_AMD_GRID") == nullptr) {
             int bpc = 0;
             if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, 256, 0) == hipSuccess && bpc > 0) {

@@ -10,10 +10,10 @@ export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest.txt" 2>&1 || { tail -40 "$OUT/pytest.txt"; exit 1; }
 tail -1 "$OUT/pytest.txt"
 for s in 65536 64512 55296; do
-  TUNE_VARIANTS="notail=LONGHAIR_AMD_DEC_TAIL:0|b2=|notail2=LONGHAIR_AMD_DEC_TAIL:0" timeout -k 10 300 python -u tools/tune.py 29 4 1296 $s > "$OUT/tune_$s.txt" 2> "$OUT/tune_$s.err" || { tail -20 "$OUT/tune_$s.err"; exit 1; }
-  grep -E "^base|^b2|^notail" "$OUT/tune_$s.txt" | sed "s/^/$s /"
+  TUNE_VARIANTS="tail=LONGHAIR_AMD_DEC_TAIL:1|b2=|tail2=LONGHAIR_AMD_DEC_TAIL:1" timeout -k 10 300 python -u tools/tune.py 29 4 1296 $s > "$OUT/tune_$s.txt" 2> "$OUT/tune_$s.err" || { tail -20 "$OUT/tune_$s.err"; exit 1; }
+  grep -E "^base|^b2|^tail" "$OUT/tune_$s.txt" | sed "s/^/$s /"
 done
-timeout -k 10 400 python bench.py > "$OUT/bench_k29m4.json" 2> "$OUT/bench_k29m4.err" || { tail -20 "$OUT/bench_k29m4.err"; exit 1; }
+LONGHAIR_AMD_DEC_TAIL=1 timeout -k 10 400 python bench.py > "$OUT/bench_k29m4.json" 2> "$OUT/bench_k29m4.err" || { tail -20 "$OUT/bench_k29m4.err"; exit 1; }
 cut -c1-400 "$OUT/bench_k29m4.json"
 for rep in 1 2; do
   for c in k200m56 k29m4; do
