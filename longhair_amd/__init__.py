@@ -257,7 +257,7 @@ def kernel_names(k, m, block_bytes):
            "jit-win": ["lh_jit_encode_win"]}[batch_path(k, m, block_bytes)]
     dec = {"generic": ["lh_plan_kernel", "lh_apply_generic_kernel", "lh_scatter_kernel"],
            "jit": ["lh_plan_small_kernel" if min(k, m) <= 8 else "lh_plan_kernel", "lh_jit_decode"],
-           "jit-fused": ["lh_jit_decode_fused", "lh_jit_decode_fused_tail"],  # (the tail kernel: large grids only)
+           "jit-fused": ["lh_jit_decode_fused"],
            "jit-wide": ["lh_plan_kernel", "lh_jit_decode_wide"] + _phase_b_kernel(k, m),
            }[batch_path(k, m, block_bytes, True)]
     if m == 1 or k == 1:

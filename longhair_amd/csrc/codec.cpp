@@ -412,42 +412,14 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         long long s1 = stride;
         const uint8_t *gexp = d->gf_exp;
         const int16_t *glog = d->gf_log;
-        // A grid that ends in a thin partial round of resident waves (k29/m4 x 65 536:
-        // 21 846 waves over 3 072 slots) leaves its last waves alone on the chip, each
-        // waiting one memory round trip per column at prefetch depth 1.  Those stripes go to
-        // lh_jit_decode_fused_tail (3 columns in flight) after the whole rounds
-        // (LONGHAIR_AMD_DEC_TAIL=1; off by default until measured).
-        int n_main = stripes;
-        const char *te = std::getenv("LONGHAIR_AMD_DEC_TAIL");
-        if (jk->decode_fused_tail && cfg.spw > 0 && te && std::atoi(te) != 0 &&
-            std::getenv("LONGHAIR_AMD_GRID") == nullptr) {
-            int bpc = 0;
-            if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, 256, 0) == hipSuccess && bpc > 0) {
-                const long long resident = (long long)bpc * d->cus * 4;  // waves (4 per block)
-                const long long waves = ((long long)stripes + cfg.spw - 1) / cfg.spw;
-                const long long rem = waves % resident;
-                if (waves > resident && rem > 0 && 2 * rem < resident) n_main = (int)((waves - rem) * cfg.spw);
-            } else {
-                (void)hipGetLastError();
-            }
-        }
-        {
-            int n = n_main;
-            void *args[] = {(void *)&d_blocks, &s1, (void *)&d_rows, (void *)&d_status, (void *)&zero,
-                            (void *)&gexp, (void *)&glog, &n};
-            LH_HIP(hipModuleLaunchKernel(fn, (unsigned)jit_blocks(cfg, n_main), 1, 1, 256, 1, 1, 0, st, args, nullptr));
-            note_launch("lh_jit_decode_fused");
-        }
-        if (n_main < stripes) {
-            uint8_t *tb = d_blocks + (long long)n_main * stride;
-            uint8_t *tr = d_rows + (long long)n_main * k;
-            int8_t *ts = d_status ? d_status + n_main : nullptr;
-            int n = stripes - n_main;
-            void *args[] = {(void *)&tb, &s1, (void *)&tr, (void *)&ts, (void *)&zero, (void *)&gexp, (void *)&glog, &n};
-            LH_HIP(hipModuleLaunchKernel(jk->decode_fused_tail, (unsigned)jit_blocks(cfg, n), 1, 1, 256, 1, 1, 0, st,
-                                         args, nullptr));
-            note_launch("lh_jit_decode_fused_tail");
-        }
+        // (Stripes past the last whole round of resident waves on a prefetch-depth-3 copy of
+        // this kernel measured slower, 0.627 vs 0.610 ms at k29/m4 x 65 536: the partial round
+        // costs < 1 %, the second launch more; profiles/r3w_decode_tail.txt.)
+        int n = stripes;
+        void *args[] = {(void *)&d_blocks, &s1, (void *)&d_rows, (void *)&d_status, (void *)&zero,
+                        (void *)&gexp, (void *)&glog, &n};
+        LH_HIP(hipModuleLaunchKernel(fn, (unsigned)jit_blocks(cfg, stripes), 1, 1, 256, 1, 1, 0, st, args, nullptr));
+        note_launch("lh_jit_decode_fused");
         return kOk;
     }
     // Large m (<= 64), sub % (64 W) == 0, after the planner: the windowed phase-A kernel

@@ -706,7 +706,6 @@ const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err, bool com
     kern.encode = fn("lh_jit_encode");
     kern.decode = fn("lh_jit_decode");
     kern.decode_fused = fn("lh_jit_decode_fused");
-    kern.decode_fused_tail = fn("lh_jit_decode_fused_tail");
     kern.encode_win = fn("lh_jit_encode_win");
     kern.decode_wide = fn("lh_jit_decode_wide");
     if (!kern.encode && !kern.encode_win && !kern.decode_wide) {

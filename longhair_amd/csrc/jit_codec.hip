@@ -1069,17 +1069,4 @@ lh_jit_decode_fused(unsigned char *__restrict__ blocks, long long stripe_stride,
     lh_fused_body<LH_PF_DEC>(blocks, stripe_stride, rows, status, zero_page, gf_exp, gf_log, stripes);
 }
 
-// The same decode with LH_PF_TAIL columns in flight, for a last partial round of waves: a
-// grid that does not fill whole rounds of resident waves ends with a few waves alone on the
-// chip, each waiting one memory round trip per column at depth 1 (codec.cpp launches the
-// stripes past the last whole round with this kernel).
-#ifndef LH_PF_TAIL
-#define LH_PF_TAIL 3
-#endif
-extern "C" __global__ void __launch_bounds__(256, 1)
-lh_jit_decode_fused_tail(unsigned char *__restrict__ blocks, long long stripe_stride, unsigned char *__restrict__ rows,
-                         signed char *__restrict__ status, const unsigned char *__restrict__ zero_page,
-                         const unsigned char *__restrict__ gf_exp, const short *__restrict__ gf_log, int stripes) {
-    lh_fused_body<LH_PF_TAIL>(blocks, stripe_stride, rows, status, zero_page, gf_exp, gf_log, stripes);
-}
 #endif  // LH_EMAX <= 4 && LH_NCH <= 64 && LH_K <= 64

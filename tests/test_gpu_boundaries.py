@@ -32,12 +32,6 @@ WIDE64 = WIDE16  # (one phase-B kernel for every e_max since round 3)
 BOUNDARIES = [
     # fused in-kernel plan <-> separate planner: k <= 64
     ("k64-fused", 64, 4, 1296, 48, {}, ["lh_jit_encode"], FUSED),
-    # fused decode split into whole rounds of resident waves + a thin last round on the
-    # deeper-prefetch tail kernel (MI355X: 256 CUs x 3 blocks of 4 waves = 3 072 waves; 9 246
-    # stripes = 3 082 waves: 9 216 stripes + 30 on the tail kernel), and with the split off
-    ("fused-tail", 29, 4, 1296, 9246, {"LONGHAIR_AMD_DEC_TAIL": "1"}, ["lh_jit_encode"],
-     FUSED + ["lh_jit_decode_fused_tail"]),
-    ("fused-tail-off", 29, 4, 1296, 9246, {}, ["lh_jit_encode"], FUSED),
     ("k65-planned", 65, 4, 1296, 48, {}, ["lh_jit_encode"], SMALL4),
     # ... and one stripe per <= 64 lanes (nch = 64 with 8-byte lanes; 65 with W pinned to 8)
     ("nch64-fused", 8, 4, 4096, 24, {}, ["lh_jit_encode"], FUSED),
