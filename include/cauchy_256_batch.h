@@ -42,8 +42,10 @@ int cauchy_256_decode_batch(int k, int m, int block_bytes, int stripes,
 
 /* Host-memory batches: the same operations on stripes that live
  * in host memory, pipelined in chunks of `chunk_stripes` (0 = about 64 MiB for encode,
- * up to 256 MiB with at least 4 chunks for decode) over three streams so the PCIe copies
- * overlap the kernels.  Host buffers should be pinned (hipHostMalloc / hipHostRegister).
+ * up to 256 MiB with at least 4 chunks for decode, the last chunks halving in size) over
+ * three streams so the PCIe copies overlap the kernels (each chunk's host-to-device copy is
+ * enqueued before the previous chunk's kernels).  Decode moves the rows and status once per
+ * call.  Host buffers should be pinned (hipHostMalloc / hipHostRegister).
  * Synchronous: returns when the results are in host memory.  Decode writes back only the
  * slots decode can write (each stripe's recovery slots) and the rewritten rows: for k, m > 1
  * with pinned, 8-byte-aligned blocks a kernel stores exactly those blocks through the
