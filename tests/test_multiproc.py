@@ -159,3 +159,27 @@ def test_bench_aligned_decode_buffer_layout(k, m, nbytes, align):
     assert stride % align == 0 and stride - k * nbytes < align and off < align
     for s in range(5):
         assert (off + s * stride + (k - m) * nbytes) % align == 0
+
+
+def test_per_call_timing_takes_the_best_round():
+    """bench.per_call_us: `calls` calls per engine in `rounds` rounds; encode_us / decode_us
+    are the best round's mean (one preempted round must not decide the comparison with the
+    reference, which the same function times), *_mean_us the overall mean."""
+    import time
+
+    import numpy as np
+
+    import bench
+    state = {"n": 0}
+
+    def slow_first_round(*_):
+        state["n"] += 1
+        if 6 <= state["n"] <= 15:  # the first timed round (after 5 warm-up calls)
+            time.sleep(0.002)
+        return 0
+
+    out = bench.per_call_us(slow_first_round, lambda *_: 0, 4, 2, 16, 50, np.zeros(64, dtype=np.uint8),
+                            lambda i, rec: None)
+    assert out["calls"] == 50 and out["rounds"] == 5
+    assert out["encode_us"] < 100 and out["encode_mean_us"] > 300  # one round of 10 x 2 ms in 50 calls
+    assert out["decode_us"] <= out["decode_mean_us"]
