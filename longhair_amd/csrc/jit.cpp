@@ -270,7 +270,7 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
                << "], " << (k + r) % 64 << ");\n    if (s != 0xFFu) {\n"
                << "      unsigned char *rp = base + (long long)s * " << c.bytes << ";\n";
             for (int y = 0; y < 8; ++y)
-                os << "      const unsigned int r" << y << " = lh_ld(rp + " << y * c.sub << ");\n";
+                os << "      const unsigned int r" << y << " = lh_ld_r(rp + " << y * c.sub << ");\n";
             for (int y = 0; y < 8; ++y)
                 os << "      lh_st(rp + " << y * c.sub << ", a" << (r - r0) << "_" << y << " ^ r" << y << ");\n";
             os << "    }\n  }\n";
@@ -434,6 +434,11 @@ static std::string win_source_for(const JitConfig &c) {
        << "#ifndef LH_NT\n#define LH_NT 1\n#endif\n"
        << "__device__ __forceinline__ unsigned int lh_ld(const unsigned char *p) {\n"
        << "#if LH_NT\n  return __builtin_nontemporal_load((const unsigned int *)p);\n#else\n"
+       << "  unsigned int w; __builtin_memcpy(&w, p, 4); return w;\n#endif\n}\n"
+       << "// R_r, read just before V_r is stored over it (split decode): cache policy LH_NT_R\n"
+       << "#ifndef LH_NT_R\n#define LH_NT_R LH_NT\n#endif\n"
+       << "__device__ __forceinline__ unsigned int lh_ld_r(const unsigned char *p) {\n"
+       << "#if LH_NT_R\n  return __builtin_nontemporal_load((const unsigned int *)p);\n#else\n"
        << "  unsigned int w; __builtin_memcpy(&w, p, 4); return w;\n#endif\n}\n"
        << "__device__ __forceinline__ void lh_st(unsigned char *p, unsigned int v) {\n"
        << "#if LH_NT\n  __builtin_nontemporal_store(v, (unsigned int *)p);\n#else\n"
