@@ -24,6 +24,8 @@
 // all 8 sub-blocks of a block and produces the same range of all 8 output sub-blocks, so
 // every output byte depends only on input bytes at the same sub-block offset.
 #include <hip/hip_runtime.h>
+
+#include <mutex>
 #include <stdint.h>
 
 #include <cstdlib>
@@ -1019,13 +1021,29 @@ __device__ __forceinline__ void lh_mul_jump_g(uint32_t (&acc)[8][8], const uint3
 #undef LH_GT_CASE
 }
 
+// 16 outputs per wave: the same calls with all 16 body-address operands.
+template <int N>
+__device__ __forceinline__ void lh_mul_jump_gw(uint32_t (&acc)[16][8], const uint32_t (&tl)[16],
+                                               const uint32_t (&th)[16], const uint32_t (&t)[16], int r,
+                                               uint32_t hi) {
+#define LH_GTW_CASE(n)                                                                                      \
+    if constexpr (N == n)                                                                                   \
+        asm volatile(LH_INV_JUMPG##n##_ASM : LH_INV_JUMPG##n##_OUTS(acc) : LH_INV_JUMPGW_INS(tl, th, t),     \
+                     [r] "s"(r), [hi] "s"(hi) : "s92", "s93", "s94", "s95", "s97", "scc");
+    LH_GTW_CASE(1) LH_GTW_CASE(2) LH_GTW_CASE(3) LH_GTW_CASE(4) LH_GTW_CASE(5) LH_GTW_CASE(6) LH_GTW_CASE(7)
+    LH_GTW_CASE(8) LH_GTW_CASE(9) LH_GTW_CASE(10) LH_GTW_CASE(11) LH_GTW_CASE(12) LH_GTW_CASE(13)
+    LH_GTW_CASE(14) LH_GTW_CASE(15) LH_GTW_CASE(16)
+#undef LH_GTW_CASE
+}
+
 // Same staging as lh_inverse_dma_body (double-buffered LDS-DMA tiles); the multiply jumps
 // into lh_inv_gtab.  Outputs: PACK ? wave g recovers outputs 8g .. 8g + 7 (fewer waves build
 // the row tables) : g, g + nw, ... as in lh_inverse_dma_body.  The row loop is instantiated
 // per output count (1..8, wave-uniform) so no slot jumps for an unused output.
-template <int TILE>
+template <int TILE, int OPW = 8>
 __device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uint32_t *__restrict__ lvA,
                                                    uint32_t *__restrict__ lvB, uint32_t tlo, uint32_t thi) {
+    static_assert(OPW == 8 || OPW == 16, "outputs per wave");
     const int nw = (int)(blockDim.x >> 6);
     const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = (int)(threadIdx.x & 63);
@@ -1044,14 +1062,14 @@ __device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uin
     uint8_t *base = sbase + lane * 4;
     const int dof0 = (lane >> 4) * sub + (lane & 15) * 16, dof1 = dof0 + 4 * sub;
     const bool pack = a.pack != 0;
-    int nout = pack ? e - 8 * g : (g < e ? (e - g + nw - 1) / nw : 0);
-    nout = nout < 0 ? 0 : (nout > 8 ? 8 : nout);
-    auto out_of = [&](int i) { return pack ? 8 * g + i : g + i * nw; };
-    uint32_t t[8];  // lane r: body address of output slot i for recovery row r
+    int nout = pack ? e - OPW * g : (g < e ? (e - g + nw - 1) / nw : 0);
+    nout = nout < 0 ? 0 : (nout > OPW ? OPW : nout);
+    auto out_of = [&](int i) { return pack ? OPW * g + i : g + i * nw; };
+    uint32_t t[OPW];  // lane r: body address of output slot i for recovery row r
     {
         const uint8_t *cf = pv.coef_ptr();
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < OPW; ++i) {
             const uint32_t c = (rslot != 0xFFu && i < nout) ? cf[out_of(i) * m + lane] : 0u;
             t[i] = tlo + c * 68u;
         }
@@ -1080,9 +1098,9 @@ __device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uin
     };
     auto run = [&](auto no) {
         constexpr int N = decltype(no)::value;
-        uint32_t acc[8][8];
+        uint32_t acc[OPW][8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < OPW; ++i)
 #pragma unroll
             for (int y = 0; y < 8; ++y) acc[i][y] = 0;
         auto compute = [&](unsigned long long rest, const uint32_t *buf) {
@@ -1100,7 +1118,8 @@ __device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uin
                         tl[q] = pre ? (tl[pre] ^ v[low]) : v[low];
                         th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];
                     }
-                    lh_mul_jump_g<N>(acc, tl, th, t, r, thi);
+                    if constexpr (OPW == 16) lh_mul_jump_gw<N>(acc, tl, th, t, r, thi);
+                    else lh_mul_jump_g<N>(acc, tl, th, t, r, thi);
                 }
             }
         };
@@ -1136,7 +1155,23 @@ __device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uin
         case 5: run(std::integral_constant<int, 5>{}); break;
         case 6: run(std::integral_constant<int, 6>{}); break;
         case 7: run(std::integral_constant<int, 7>{}); break;
-        default: run(std::integral_constant<int, 8>{}); break;
+        case 8: run(std::integral_constant<int, 8>{}); break;
+        default:
+            if constexpr (OPW == 16) {
+                switch (nout) {
+                    case 9: run(std::integral_constant<int, 9>{}); break;
+                    case 10: run(std::integral_constant<int, 10>{}); break;
+                    case 11: run(std::integral_constant<int, 11>{}); break;
+                    case 12: run(std::integral_constant<int, 12>{}); break;
+                    case 13: run(std::integral_constant<int, 13>{}); break;
+                    case 14: run(std::integral_constant<int, 14>{}); break;
+                    case 15: run(std::integral_constant<int, 15>{}); break;
+                    default: run(std::integral_constant<int, 16>{}); break;
+                }
+            } else {
+                run(std::integral_constant<int, 8>{});
+            }
+            break;
     }
 }
 
@@ -1162,6 +1197,41 @@ __global__ void __launch_bounds__(1024) lh_inverse_gt_kernel(lh::InverseArgs a) 
         return;
     }
     lh_inverse_gt_body<TILE>(a, lvA, lvB, tlo, thi);
+}
+
+// 16 outputs per wave (LONGHAIR_AMD_INV_GTW=16, a knob): half the waves of the 8-output form,
+// so each row's nibble tables are built by half as many waves.  The host launches it only
+// after lh_inv_gtab_probe showed the table does not straddle a 4 GiB boundary (no in-asm
+// fallback exists for 16 outputs per wave).
+template <int TILE>
+__global__ void __launch_bounds__(256) lh_inverse_gtw_kernel(lh::InverseArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lvA[TILE * 8 * 64];
+    __shared__ __attribute__((aligned(16))) uint32_t lvB[TILE * 8 * 64];
+    uint32_t tlo, thi;
+    asm volatile(
+        "s_getpc_b64 s[92:93]\n"
+        "s_add_u32 s92, s92, lh_inv_gtab@rel32@lo+4\n"
+        "s_addc_u32 s93, s93, lh_inv_gtab@rel32@hi+12\n"
+        "s_mov_b32 %0, s92\n"
+        "s_mov_b32 %1, s93\n"
+        : "=s"(tlo), "=s"(thi)
+        :
+        : "s92", "s93", "scc");
+    lh_inverse_gt_body<TILE, 16>(a, lvA, lvB, tlo, thi);
+}
+
+// Low word of the table's address (one lane stores it): the host checks it once.
+__global__ void lh_inv_gtab_probe(uint32_t *out) {
+    uint32_t tlo;
+    asm volatile(
+        "s_getpc_b64 s[92:93]\n"
+        "s_add_u32 s92, s92, lh_inv_gtab@rel32@lo+4\n"
+        "s_addc_u32 s93, s93, lh_inv_gtab@rel32@hi+12\n"
+        "s_mov_b32 %0, s92\n"
+        : "=s"(tlo)
+        :
+        : "s92", "s93", "scc");
+    if (threadIdx.x == 0) out[0] = tlo;
 }
 
 // One inlined table per output (JO <= 4 copies of 17 KiB).
@@ -1279,6 +1349,27 @@ hipError_t launch_apply_generic(const ApplyArgs &a, int W, hipStream_t st) {
     return hipGetLastError();
 }
 
+// Whether lh_inv_gtab lies within one 4 GiB window (probed once per process on the current
+// device, on a private stream).
+static bool gtab_no_straddle() {
+    static int ok = -1;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> g(mu);
+    if (ok >= 0) return ok == 1;
+    ok = 0;
+    uint32_t *d = nullptr, h = 0xFFFFFFFFu;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess && hipMalloc((void **)&d, 4) == hipSuccess) {
+        hipLaunchKernelGGL(lh_inv_gtab_probe, dim3(1), dim3(64), 0, s, d);
+        if (hipMemcpyAsync(&h, d, 4, hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess)
+            ok = h <= 0xFFFFFFFFu - 256u * 68u ? 1 : 0;
+    }
+    if (d) (void)hipFree(d);
+    if (s) (void)hipStreamDestroy(s);
+    (void)hipGetLastError();
+    return ok == 1;
+}
+
 hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     // sub-blocks in 256-byte chunks (the windowed configurations: sub % 256 == 0)
     if (a.bytes % 2048 != 0 || a.e_max < 1 || a.e_max > 64 || a.m > 64) return hipErrorInvalidValue;
@@ -1347,6 +1438,13 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
         const char *fb = std::getenv("LONGHAIR_AMD_INV_FALLBACK");
         g.pack = pk ? (std::atoi(pk) ? 1 : 0) : (a.e_max <= 32 ? 1 : 0);
         g.jump_fallback = fb && std::atoi(fb) ? 1 : 0;
+        // LONGHAIR_AMD_INV_GTW=16: 16 outputs per wave (the table's address checked once).
+        const char *gw = std::getenv("LONGHAIR_AMD_INV_GTW");
+        if (gw && std::atoi(gw) == 16 && !g.jump_fallback && dma_rows == 8 && gtab_no_straddle()) {
+            hipLaunchKernelGGL((lh_inverse_gtw_kernel<8>), grid, dim3(64u * (unsigned)((a.e_max + 15) / 16)), 0, st, g);
+            note_launch("lh_inverse_gtw_kernel<8>");
+            return hipGetLastError();
+        }
         const dim3 block(64u * (unsigned)((a.e_max + 7) / 8));
         if (dma_rows == 8) {
             hipLaunchKernelGGL((lh_inverse_gt_kernel<8>), grid, block, 0, st, g);

@@ -121,4 +121,4 @@ def test_inv_jump_table_is_generated():
     assert committed.count("v_bitop3_b32") == 4 * 256 * 8  # per-output, indexed JO 4 / 8, global
     assert committed.count("s_branch 3f") == 256
     assert committed.count("s_setpc_b64 s[94:95]") == 3 * 256
-    assert committed.count("lh_inv_gtab:") == 1 and committed.count("s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)") == 8
+    assert committed.count("lh_inv_gtab:") == 1 and committed.count("s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)") == 16

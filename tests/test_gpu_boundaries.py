@@ -115,6 +115,10 @@ PHASE_B = [
     ({"LONGHAIR_AMD_INV_JUMP": "10", "LONGHAIR_AMD_INV_PACK": "1"}, 64, "lh_inverse_gt_kernel<8>"),
     ({"LONGHAIR_AMD_INV_JUMP": "10", "LONGHAIR_AMD_INV_DMA": "16"}, 33, "lh_inverse_gt_kernel<16>"),
     ({"LONGHAIR_AMD_INV_JUMP": "10", "LONGHAIR_AMD_INV_FALLBACK": "1"}, 33, "lh_inverse_gt_kernel<8>(fallback)"),
+    # 16 outputs per wave from the same table (knob)
+    ({"LONGHAIR_AMD_INV_GTW": "16"}, 32, "lh_inverse_gtw_kernel<8>"),
+    ({"LONGHAIR_AMD_INV_GTW": "16"}, 33, "lh_inverse_gtw_kernel<8>"),
+    ({"LONGHAIR_AMD_INV_GTW": "16", "LONGHAIR_AMD_INV_PACK": "0"}, 64, "lh_inverse_gtw_kernel<8>"),
 ]
 
 

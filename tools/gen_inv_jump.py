@@ -64,6 +64,8 @@ def render_indexed(jo):
 # run: 3 SALU with the body's s_setpc_b64, against 7 for LH_INV_JUMPI.
 GT_TL, GT_TH = 8, 24
 GT_MAX = 8
+# 16 outputs per wave (lh_inverse_gt_kernel<TILE, 16>): accumulators v[IDX_BASE .. IDX_BASE + 127]
+GTW_MAX = 16
 
 
 def render_global_table():
@@ -131,12 +133,16 @@ def render():
     ins = ", ".join([f'[t{q}] "v"(tl[{q}])' for q in range(1, 16)] + [f'[h{q}] "v"(th[{q}])' for q in range(1, 16)])
     lines.append(f"#define LH_INV_JUMPI_INS(tl, th) {ins}")
     lines += render_global_table()
-    for n in range(1, GT_MAX + 1):
+    for n in range(1, GTW_MAX + 1):
         lines += render_global_call(n)
     gins = ", ".join([f'"{{v{GT_TL + q}}}"(tl[{q}])' for q in range(1, 16)]
                      + [f'"{{v{GT_TH + q}}}"(th[{q}])' for q in range(1, 16)]
                      + [f'[a{i}] "v"(t[{i}])' for i in range(GT_MAX)])
     lines.append(f"#define LH_INV_JUMPG_INS(tl, th, t) {gins}")
+    wins = ", ".join([f'"{{v{GT_TL + q}}}"(tl[{q}])' for q in range(1, 16)]
+                     + [f'"{{v{GT_TH + q}}}"(th[{q}])' for q in range(1, 16)]
+                     + [f'[a{i}] "v"(t[{i}])' for i in range(GTW_MAX)])
+    lines.append(f"#define LH_INV_JUMPGW_INS(tl, th, t) {wins}")
     return "\n".join(lines) + "\n"
 
 
