@@ -1036,6 +1036,19 @@ __device__ __forceinline__ void lh_mul_jump_gw(uint32_t (&acc)[16][8], const uin
 #undef LH_GTW_CASE
 }
 
+// 4 outputs per wave: the calls for 1..4 outputs with 4 body-address operands.
+template <int N>
+__device__ __forceinline__ void lh_mul_jump_gq(uint32_t (&acc)[4][8], const uint32_t (&tl)[16],
+                                               const uint32_t (&th)[16], const uint32_t (&t)[4], int r,
+                                               uint32_t hi) {
+#define LH_GTQ_CASE(n)                                                                                      \
+    if constexpr (N == n)                                                                                   \
+        asm volatile(LH_INV_JUMPG##n##_ASM : LH_INV_JUMPG##n##_OUTS(acc) : LH_INV_JUMPGQ_INS(tl, th, t),     \
+                     [r] "s"(r), [hi] "s"(hi) : "s92", "s93", "s94", "s95", "s97", "scc");
+    LH_GTQ_CASE(1) LH_GTQ_CASE(2) LH_GTQ_CASE(3) LH_GTQ_CASE(4)
+#undef LH_GTQ_CASE
+}
+
 // Same staging as lh_inverse_dma_body (double-buffered LDS-DMA tiles); the multiply jumps
 // into lh_inv_gtab.  Outputs: PACK ? wave g recovers outputs 8g .. 8g + 7 (fewer waves build
 // the row tables) : g, g + nw, ... as in lh_inverse_dma_body.  The row loop is instantiated
@@ -1043,7 +1056,7 @@ __device__ __forceinline__ void lh_mul_jump_gw(uint32_t (&acc)[16][8], const uin
 template <int TILE, int OPW = 8>
 __device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uint32_t *__restrict__ lvA,
                                                    uint32_t *__restrict__ lvB, uint32_t tlo, uint32_t thi) {
-    static_assert(OPW == 8 || OPW == 16, "outputs per wave");
+    static_assert(OPW == 4 || OPW == 8 || OPW == 16, "outputs per wave");
     const int nw = (int)(blockDim.x >> 6);
     const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = (int)(threadIdx.x & 63);
@@ -1119,6 +1132,7 @@ __device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uin
                         th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];
                     }
                     if constexpr (OPW == 16) lh_mul_jump_gw<N>(acc, tl, th, t, r, thi);
+                    else if constexpr (OPW == 4) lh_mul_jump_gq<N>(acc, tl, th, t, r, thi);
                     else lh_mul_jump_g<N>(acc, tl, th, t, r, thi);
                 }
             }
@@ -1146,6 +1160,16 @@ __device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uin
             for (int y = 0; y < 8; ++y) __builtin_nontemporal_store(acc[i][y], (uint32_t *)(dst + (long long)y * sub));
         }
     };
+    if constexpr (OPW == 4) {
+        switch (nout) {  // wave-uniform
+            case 0: run(std::integral_constant<int, 0>{}); break;
+            case 1: run(std::integral_constant<int, 1>{}); break;
+            case 2: run(std::integral_constant<int, 2>{}); break;
+            case 3: run(std::integral_constant<int, 3>{}); break;
+            default: run(std::integral_constant<int, 4>{}); break;
+        }
+        return;
+    } else
     switch (nout) {  // wave-uniform
         case 0: run(std::integral_constant<int, 0>{}); break;
         case 1: run(std::integral_constant<int, 1>{}); break;
@@ -1218,6 +1242,30 @@ __global__ void __launch_bounds__(256) lh_inverse_gtw_kernel(lh::InverseArgs a) 
         :
         : "s92", "s93", "scc");
     lh_inverse_gt_body<TILE, 16>(a, lvA, lvB, tlo, thi);
+}
+
+// 4 outputs per wave (LONGHAIR_AMD_INV_GTW=4, a knob): twice the waves of the 8-output form
+// (fewer registers, more waves per SIMD), each row's tables built by twice as many waves.
+// The in-asm fallback covers it: with twice the waves, each gets at most 4 outputs.
+template <int TILE>
+__global__ void __launch_bounds__(1024) lh_inverse_gtq_kernel(lh::InverseArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lvA[TILE * 8 * 64];
+    __shared__ __attribute__((aligned(16))) uint32_t lvB[TILE * 8 * 64];
+    uint32_t tlo, thi;
+    asm volatile(
+        "s_getpc_b64 s[92:93]\n"
+        "s_add_u32 s92, s92, lh_inv_gtab@rel32@lo+4\n"
+        "s_addc_u32 s93, s93, lh_inv_gtab@rel32@hi+12\n"
+        "s_mov_b32 %0, s92\n"
+        "s_mov_b32 %1, s93\n"
+        : "=s"(tlo), "=s"(thi)
+        :
+        : "s92", "s93", "scc");
+    if (a.jump_fallback || tlo > 0xFFFFFFFFu - 256u * 68u) {
+        lh_inverse_dma_body<8, TILE, true>(a, lvA, lvB);
+        return;
+    }
+    lh_inverse_gt_body<TILE, 4>(a, lvA, lvB, tlo, thi);
 }
 
 // Low word of the table's address (one lane stores it): the host checks it once.
@@ -1443,6 +1491,11 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
         if (gw && std::atoi(gw) == 16 && !g.jump_fallback && dma_rows == 8 && gtab_no_straddle()) {
             hipLaunchKernelGGL((lh_inverse_gtw_kernel<8>), grid, dim3(64u * (unsigned)((a.e_max + 15) / 16)), 0, st, g);
             note_launch("lh_inverse_gtw_kernel<8>");
+            return hipGetLastError();
+        }
+        if (gw && std::atoi(gw) == 4 && dma_rows == 8) {
+            hipLaunchKernelGGL((lh_inverse_gtq_kernel<8>), grid, dim3(64u * (unsigned)((a.e_max + 3) / 4)), 0, st, g);
+            note_launch(g.jump_fallback ? "lh_inverse_gtq_kernel<8>(fallback)" : "lh_inverse_gtq_kernel<8>");
             return hipGetLastError();
         }
         const dim3 block(64u * (unsigned)((a.e_max + 7) / 8));

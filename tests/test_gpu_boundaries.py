@@ -119,6 +119,10 @@ PHASE_B = [
     ({"LONGHAIR_AMD_INV_GTW": "16"}, 32, "lh_inverse_gtw_kernel<8>"),
     ({"LONGHAIR_AMD_INV_GTW": "16"}, 33, "lh_inverse_gtw_kernel<8>"),
     ({"LONGHAIR_AMD_INV_GTW": "16", "LONGHAIR_AMD_INV_PACK": "0"}, 64, "lh_inverse_gtw_kernel<8>"),
+    # 4 outputs per wave (knob), and its in-asm fallback
+    ({"LONGHAIR_AMD_INV_GTW": "4"}, 32, "lh_inverse_gtq_kernel<8>"),
+    ({"LONGHAIR_AMD_INV_GTW": "4"}, 33, "lh_inverse_gtq_kernel<8>"),
+    ({"LONGHAIR_AMD_INV_GTW": "4", "LONGHAIR_AMD_INV_FALLBACK": "1"}, 33, "lh_inverse_gtq_kernel<8>(fallback)"),
 ]
 
 

@@ -143,6 +143,10 @@ def render():
                      + [f'"{{v{GT_TH + q}}}"(th[{q}])' for q in range(1, 16)]
                      + [f'[a{i}] "v"(t[{i}])' for i in range(GTW_MAX)])
     lines.append(f"#define LH_INV_JUMPGW_INS(tl, th, t) {wins}")
+    qins = ", ".join([f'"{{v{GT_TL + q}}}"(tl[{q}])' for q in range(1, 16)]
+                     + [f'"{{v{GT_TH + q}}}"(th[{q}])' for q in range(1, 16)]
+                     + [f'[a{i}] "v"(t[{i}])' for i in range(4)])
+    lines.append(f"#define LH_INV_JUMPGQ_INS(tl, th, t) {qins}")
     return "\n".join(lines) + "\n"
 
 
