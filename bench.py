@@ -84,6 +84,9 @@ def parse(argv=None):
                     help="decode buffer: pad the stripe stride so the recovery slots start on this byte "
                          "boundary (0 = contiguous [S, k, bytes])")
     ap.add_argument("--dry-run", action="store_true", help="no HIP work: CPU stand-in step over gloo")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="map rank r to device r %% device_count (runs the N > 1 path on fewer GPUs than ranks: "
+                         "a functional check of the control path, not a scaling measurement)")
     return ap.parse_args(argv)
 
 
@@ -105,15 +108,17 @@ def launch(args):
     return subprocess.call(cmd, env=env)
 
 
-def setup_dist(dry):
+def setup_dist(dry, share_gpu=False):
     """One process per GPU.  The group is gloo in every run: no data-path collective exists
-    (SURVEY 8e), so it carries only host-side barriers and the timing reduction."""
+    (SURVEY 8e), so it carries only host-side barriers and the timing reduction.
+    share_gpu: rank -> device local % device_count (device_count() does not initialise the
+    GPU on this image)."""
     import torch
     import torch.distributed as dist
     from longhair_amd.shard import world_info
     world, rank, local = world_info()
     if not dry:
-        torch.cuda.set_device(local)
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()) if share_gpu else local)
     if world > 1:
         dist.init_process_group(backend="gloo")
     return world, rank, local
@@ -435,7 +440,6 @@ def pcie_leg(lh, args, k, m, nbytes, X, D, rows0, rec_view, rec_index, world, ra
     memory, then cauchy_256_encode_host_batch and cauchy_256_decode_host_batch (H2D, kernels
     and D2H pipelined over three streams), every rank at the same time.  Input GB/s per rank
     and for the node (all ranks' input bytes / the slowest rank's time)."""
-    import numpy as np
     import torch
     n = args.pcie_stripes or min(X.shape[0], max(1, (640 << 20) // (k * nbytes)))
     n = min(n, X.shape[0])
@@ -450,20 +454,31 @@ def pcie_leg(lh, args, k, m, nbytes, X, D, rows0, rec_view, rec_index, world, ra
     hr0 = rows0[:n].cpu()
     hr = hr0.clone().pin_memory()
     hrec = torch.empty((n, m, nbytes), dtype=torch.uint8).pin_memory()
-    xn, bn, rn, recn = hx.numpy(), hb.numpy(), hr.numpy(), hrec.numpy()
+    return pcie_timed(lh, k, m, nbytes, hx.numpy(), hb.numpy(), hr.numpy(), hrec.numpy(), hb0.numpy(),
+                      hr0.numpy(), world, rank, reps)
+
+
+def pcie_timed(lh, k, m, nbytes, xn, bn, rn, recn, b0, r0, world, rank, reps=3, dry=False):
+    """The timed part of pcie_leg on host arrays (data xn [n, k, B], decode slots bn and rows
+    rn, recovery recn; b0 / r0 the slots and rows to restore before each decode), every rank
+    at once between barriers, and the cross-rank aggregation: every rank makes the same
+    per_rank calls in the same order (tests/test_multiproc.py drives it at world 2 on gloo
+    with a stand-in codec)."""
+    import numpy as np
+    n = xn.shape[0]
     lh.encode_host_batch(xn, m, recovery=recn)           # warm-up: buffers, streams
     lh.decode_host_batch(bn, rn, m)
     order = np.argsort(rn, axis=1)
     ok = bool(np.array_equal(np.take_along_axis(bn, order[:, :, None], axis=1), xn))
     te = td = 0.0
     for _ in range(reps):
-        barrier(world, False)
+        barrier(world, dry)
         t0 = time.perf_counter()
         lh.encode_host_batch(xn, m, recovery=recn)
         te += time.perf_counter() - t0
-        bn[:] = hb0.numpy()
-        rn[:] = hr0.numpy()
-        barrier(world, False)
+        bn[:] = b0
+        rn[:] = r0
+        barrier(world, dry)
         t0 = time.perf_counter()
         lh.decode_host_batch(bn, rn, m)
         td += time.perf_counter() - t0
@@ -496,7 +511,7 @@ def main():
         sys.exit(launch(args))
     dry = args.dry_run
     import torch
-    world, rank, local = setup_dist(dry)
+    world, rank, local = setup_dist(dry, args.share_gpu)
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     from longhair_amd.shard import shard_range
@@ -667,6 +682,9 @@ def main():
     if not dry and args.pcie == "on":
         # every rank at once: the node's host links and memory are shared
         out["pcie"] = pcie_leg(lh, args, k, m, nbytes, X, D, rows0, rec_view, rec_index, world, rank)
+    if args.share_gpu and world > 1:
+        out["share_gpu"] = (f"{world} ranks on {torch.cuda.device_count() if not dry else 0} device(s): a functional "
+                            "check of the N > 1 control path, not a scaling measurement")
     if rank == 0 and not dry:
         calls = args.dropin_calls if args.dropin_calls >= 0 else max(10, min(2000, int(4e7 / (k * nbytes))))
         if calls:

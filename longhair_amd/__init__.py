@@ -238,17 +238,7 @@ def _phase_b_kernel(k, m):
     authoritative record of a call is last_launch()."""
     if os.environ.get("LONGHAIR_AMD_WIN_SPLIT") == "0":
         return []
-    e_max = min(k, m)
-    jump_env = os.environ.get("LONGHAIR_AMD_INV_JUMP")
-    dma = os.environ.get("LONGHAIR_AMD_INV_DMA", "8") in ("8", "16")
-    if dma and jump_env in (None, "10"):
-        return ["lh_inverse_gt_kernel"]
-    if dma and jump_env in ("4", "9"):
-        return ["lh_inverse_dma_kernel"]
-    jump = jump_env or ("9" if e_max <= 32 else "4")
-    if jump == "0" or (jump == "2" and e_max > 32):
-        return ["lh_inverse_kernel"]
-    return ["lh_inverse_ji_kernel" if jump in ("5", "9") else "lh_inverse_jt_kernel"]
+    return ["lh_inverse_gt_kernel"]
 
 
 def kernel_names(k, m, block_bytes):

@@ -3,7 +3,10 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-library_path = os.path.join(_HERE, "liblonghair_amd.so")
+# LONGHAIR_AMD_LIBRARY: another in-tree build of the same sources (the phase-B checked build,
+# `make -C longhair_amd/csrc LH_DEBUG=1 OUT=$PWD/longhair_amd/liblonghair_amd_check.so
+# BUILD=$PWD/longhair_amd/build_check`); the default is the product library.
+library_path = os.path.join(_HERE, os.environ.get("LONGHAIR_AMD_LIBRARY", "liblonghair_amd.so"))
 _lib = None
 
 

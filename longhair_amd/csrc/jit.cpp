@@ -124,6 +124,11 @@ bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
     if (const char *r = std::getenv("LONGHAIR_AMD_WIN_ROWS")) cfg->rows_per_wave = std::atoi(r);
     if (!decode)  // tuning knob for the encode alone (the decode's phase A keeps its rows)
         if (const char *r = std::getenv("LONGHAIR_AMD_WIN_ROWS_ENC")) cfg->rows_per_wave = std::atoi(r);
+    cfg->rows_per_wave = std::max(1, std::min(16, cfg->rows_per_wave));
+    // The fused decode's phase B gives wave g the outputs g, g + NG, ... (NG = ceil(m / rows)),
+    // and holds at most 8 of them (lh_phase_b: acc[8][8], two packed coefficient words): at
+    // most 8 rows per wave keeps ceil(e / NG) <= 8 for every e <= m.
+    if (decode && !cfg->win_split) cfg->rows_per_wave = std::min(8, cfg->rows_per_wave);
     cfg->win_pf = 3;
     if (const char *f = std::getenv("LONGHAIR_AMD_WIN_PF")) cfg->win_pf = std::max(1, std::atoi(f));
     cfg->win_lds = 1;

@@ -13,10 +13,10 @@
 //   lh_xor_reduce_kernel    out = XOR of n inputs for any block size (m == 1 encode
 //                           :1511-1522, k <= 1 copies :1501-1509, m == 1 decode :487-535).
 //   lh_scatter_kernel       moves recovered blocks from the workspace into their slots.
-//   lh_inverse_jt_kernel    large-m decode phase B (after the windowed phase A left V_r in
+//   lh_inverse_gt_kernel    large-m decode phase B (after the windowed phase A left V_r in
 //                           the recovery slots): D_E = A^-1 V by a computed jump into 256
-//                           fixed multiply-by-c bodies (default); lh_inverse_kernel is the
-//                           Horner form (back-substitution :1083-1247, same solution).
+//                           fixed multiply-by-c bodies (back-substitution :1083-1247, same
+//                           solution).
 //   lh_writeback_kernel     pinned-host decode pipeline: recovered blocks straight into
 //                           the caller's pinned buffer.
 //
@@ -25,7 +25,7 @@
 // every output byte depends only on input bytes at the same sub-block offset.
 #include <hip/hip_runtime.h>
 
-#include <mutex>
+#include <type_traits>
 #include <stdint.h>
 
 #include <cstdlib>
@@ -626,470 +626,61 @@ __global__ void __launch_bounds__(256) lh_frame_kernel(lh::FrameArgs a) {
 // recovery block R_r by V_r = R_r + sum_{x present} B(G[r][x]) D_x in place:
 // D_{E_i} = sum_r B(coef[i][r]) V_r (the reference's back-substitution,
 // cauchy_256.cpp:1083-1247; same unique solution).  One workgroup per (stripe, 256-byte
-// chunk of every sub-block), nw = ceil(e_max / 8) waves; wave g recovers outputs g,
-// g + nw, ... (at most 8) of the stripe's e.  For each used recovery row r (ascending:
-// the plan's coefficient columns) the wave reads V_r's chunk (one dword per lane and
-// sub-block, two rows ahead, from L2 after the first wave) and adds B(coef[i][r]) V_r to
-// every output by Horner over the coefficient bits: coefficients are wave-uniform, so a
-// bit is a scalar branch and only set bits cost XORs; V is doubled in place
-// (B(2) v = (v1..v7, v0^v1^v2^v7)).  Every wave has read every V row before any output is
-// written (workgroup barrier): the outputs go to the recovery blocks' slots, where V is.
-// No LDS and ~100 VGPRs: several waves per SIMD hide the branch latency that the fused
-// kernel (an m x 2 KiB V tile per workgroup, 2 waves per SIMD) could not.
-__device__ __forceinline__ void lh_inv_load(uint32_t (&d)[8], const uint8_t *base, uint32_t rslot,
-                                            unsigned long long mk, int bytes, int sub) {
-    const int r = __builtin_ctzll(mk);
-    const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)rslot, r);
-    const uint8_t *p = base + (long long)slot * bytes;
-#pragma unroll
-    for (int y = 0; y < 8; ++y) d[y] = *(const uint32_t *)(p + (long long)y * sub);
-}
-
-template <int OPW, int NO>
-__device__ __forceinline__ void lh_inv_rows(uint32_t (&acc)[OPW][8], const uint8_t *base, uint32_t rslot,
-                                            unsigned long long used, uint32_t cpk0, uint32_t cpk1, int bytes,
-                                            int sub) {
-    uint32_t n0[8], n1[8];
-    unsigned long long pf = used;  // rows not yet loaded
-    lh_inv_load(n0, base, rslot, pf, bytes, sub);
-    pf &= pf - 1;
-    if (pf) {
-        lh_inv_load(n1, base, rslot, pf, bytes, sub);
-        pf &= pf - 1;
-    }
-    for (unsigned long long rest = used; rest; rest &= rest - 1) {
-        const int r = __builtin_ctzll(rest);
-        uint32_t v[8];
-#pragma unroll
-        for (int y = 0; y < 8; ++y) {
-            v[y] = n0[y];
-            n0[y] = n1[y];
-        }
-        if (pf) {
-            lh_inv_load(n1, base, rslot, pf, bytes, sub);
-            pf &= pf - 1;
-        }
-        const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)cpk0, r);
-        const uint32_t c1 = OPW > 4 ? (uint32_t)__builtin_amdgcn_readlane((int)cpk1, r) : 0u;
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-#pragma unroll
-            for (int i = 0; i < NO; ++i) {
-                if (__builtin_expect(((i < 4 ? c0 : c1) >> (8 * (i & 3) + t)) & 1u, 1))
-#pragma unroll
-                    for (int y = 0; y < 8; ++y) acc[i][y] ^= v[y];
-            }
-            if (t < 7) {
-                const uint32_t t7 = __builtin_amdgcn_bitop3_b32(v[0], v[1], v[2], 0x96) ^ v[7];
-#pragma unroll
-                for (int y = 0; y < 7; ++y) v[y] = v[y + 1];
-                v[7] = t7;
-            }
-        }
-    }
-}
-
-// ---- phase B by a computed jump on the coefficient value (LONGHAIR_AMD_INV_JUMP=1,
-// e_max <= 32).  The V rows of the chunk are staged in LDS once per workgroup (e x 2 KiB;
-// after that barrier the recovery slots may be overwritten).  Per used row a wave builds
-// the 16-entry XOR tables of V_r's sub-blocks 0..3 (tl) and 4..7 (th) in registers; a
-// multiply by c is then, for every output sub-row y, one XOR3 of two table entries whose
-// indices are the nibbles of c * 2^y.  Those are compile-time constants of 256 fixed-size
-// bodies (8 v_bitop3 + s_branch = 68 bytes, inv_jump.inc, tools/gen_inv_jump.py); the
-// wave jumps to body c with s_setpc_b64 (c is wave-uniform): 8 VALU per (output, row)
-// against the Horner form's 8 bit branches and ~32 XORs.  Every output of a wave inlines
-// its own copy of the 17 KiB table: JO = 4 (the default) is about 70 KiB of code, more than
-// the instruction cache (JO = 2, 35 KiB, fits but builds the tables for half as many
-// outputs and measured slower).
+// chunk of every sub-block), ceil(e_max / 8) waves, at most 8 outputs per wave.  The chunk's
+// V rows are staged in LDS by LDS-DMA in double-buffered 8-row tiles (2 KiB per row); per
+// used row a wave builds the 16-entry XOR tables of V_r's sub-blocks 0..3 (tl) and 4..7 (th)
+// in registers, and a multiply by c is, for every output sub-row y, one XOR3 of two table
+// entries whose indices are the nibbles of c * 2^y: compile-time constants of 256 fixed-size
+// bodies (8 v_bitop3_b32 + a return, 68 bytes; inv_jump.inc, tools/gen_inv_jump.py) that the
+// wave enters with c wave-uniform.  Round 3 measured seven forms of this phase (DESIGN.md
+// §5.3); two remain: the bodies once per code object (lh_inverse_gt_kernel, the default) and
+// the same bodies inside the asm statement (its fallback, lh_inverse_dma_body).
 #include "inv_jump.inc"
 
-__device__ __forceinline__ void lh_mul_jump(unsigned c, uint32_t (&a)[8], const uint32_t (&tl)[16],
-                                            const uint32_t (&th)[16]) {
-    asm volatile(LH_INV_JUMP_ASM
-                 : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7])
-                 : "s"(c), "v"(tl[0]), "v"(tl[1]), "v"(tl[2]), "v"(tl[3]), "v"(tl[4]), "v"(tl[5]), "v"(tl[6]),
-                   "v"(tl[7]), "v"(tl[8]), "v"(tl[9]), "v"(tl[10]), "v"(tl[11]), "v"(tl[12]), "v"(tl[13]),
-                   "v"(tl[14]), "v"(tl[15]), "v"(th[0]), "v"(th[1]), "v"(th[2]), "v"(th[3]), "v"(th[4]),
-                   "v"(th[5]), "v"(th[6]), "v"(th[7]), "v"(th[8]), "v"(th[9]), "v"(th[10]), "v"(th[11]),
-                   "v"(th[12]), "v"(th[13]), "v"(th[14]), "v"(th[15])
-                 : "s96", "s97", "s98", "scc");
+// The in-asm table: the 8 outputs of a wave keep their accumulators in pinned registers
+// v[40 + 8i .. 40 + 8i + 7]; one asm statement per row builds the 8 jump targets from the
+// packed coefficient bytes (masked to 8 bits in the asm), enters the table once per output
+// with GPR indexing on (SRC0 and DST relative to index 8i) and returns through s[94:95].
+__device__ __forceinline__ void lh_mul_jump_idx8(unsigned c0, unsigned c1, uint32_t (&a)[8][8],
+                                                 const uint32_t (&tl)[16], const uint32_t (&th)[16]) {
+    asm volatile(LH_INV_JUMPI8_ASM : LH_INV_JUMPI8_OUTS(a) : [c0] "s"(c0), [c1] "s"(c1), LH_INV_JUMPI_INS(tl, th)
+                 : "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "scc");
 }
 
-// ---- the computed jump with ONE copy of the table per kernel (round 3).  The wave's JO
-// outputs keep their accumulators in pinned registers v[40 + 8i .. 40 + 8i + 7]
-// (LH_INV_IDX_BASE); the table is written for output 0 and output i reaches it with GPR
-// indexing on (SRC0 and DST relative to index 8i): per row one asm statement builds the JO
-// jump targets from the coefficient bytes, enters the table JO times and returns through
-// s[94:95] (tools/gen_inv_jump.py render_indexed).  17 KiB of table code instead of JO
-// copies.
-template <int JO>
-__device__ __forceinline__ void lh_mul_jump_idx(unsigned c0, unsigned c1, uint32_t (&a)[JO][8],
-                                                const uint32_t (&tl)[16], const uint32_t (&th)[16]) {
-    if constexpr (JO == 4) {
-        asm volatile(LH_INV_JUMPI4_ASM : LH_INV_JUMPI4_OUTS(a) : [c0] "s"(c0), [c1] "s"(c1), LH_INV_JUMPI_INS(tl, th)
-                     : "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "scc");
-    } else {
-        asm volatile(LH_INV_JUMPI8_ASM : LH_INV_JUMPI8_OUTS(a) : [c0] "s"(c0), [c1] "s"(c1), LH_INV_JUMPI_INS(tl, th)
-                     : "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "scc");
+// Common to both forms: the plan view, the used recovery rows, the LDS-DMA staging of the
+// chunk's V rows (2 global_load_lds_dwordx4 per row, 16 B per lane: lane l moves bytes
+// (l % 16) * 16 of sub-block 4 h + l / 16, so each instruction fills 1 KiB of the row's
+// [sub-block][256 B] image in lane order) and the tile loop: the DMA of tile t + 1 is issued
+// right after the barrier that publishes tile t and lands while tile t is computed (one
+// counted wait + a raw barrier per tile, no __syncthreads, whose fence would drain it).
+struct lh_pb_ctx {
+    const lh::InverseArgs &a;
+    int nw, g, lane, e, m, sub;
+    lh::PlanView pv;
+    uint32_t rslot;
+    unsigned long long used;
+    uint8_t *sbase, *base;
+    int dof0, dof1;
+    __device__ __forceinline__ lh_pb_ctx(const lh::InverseArgs &a_, const uint8_t *pl)
+        : a(a_), pv(pl, a_.k, a_.m, a_.e_max) {
+        nw = (int)(blockDim.x >> 6);
+        g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+        lane = (int)(threadIdx.x & 63);
+        e = pl[0];
+        m = a.m;
+        sub = a.bytes >> 3;
+        rslot = lane < m ? (uint32_t)pv.rec_slot(lane) : 0xFFu;
+        used = __ballot(rslot != 0xFFu);
+        const int cps = a.bytes >> 11;
+        sbase = a.blocks + (blockIdx.x / cps) * a.stride + (int)(blockIdx.x % cps) * 256;  // wave-uniform
+        base = sbase + lane * 4;
+        dof0 = (lane >> 4) * sub + (lane & 15) * 16;
+        dof1 = dof0 + 4 * sub;
     }
-}
-
-// Phase B by computed jump.  One workgroup per (stripe, 256-byte chunk of every
-// sub-block), ceil(e_max / JO) waves; wave g recovers outputs g, g + nw, ... (<= JO).  The
-// chunk's V rows are staged in an LDS tile BLK rows at a time (BLK == 0: all MAXE at once),
-// wave g copying tile rows g, g + nw, ...; per used row every wave builds the 16-entry
-// tables and multiplies by its coefficients (IDX: one table copy reached by GPR indexing,
-// JO = 4 or 8; else one inlined table per output, JO <= 4).  PFR > 0: the first PFR of the
-// wave's rows of the NEXT tile are loaded into registers before the current tile is
-// computed (their HBM latency overlaps the compute) and written to LDS after the tile's
-// closing barrier.  The outputs are stored once every row has been staged (read): they
-// land in the recovery slots, where V is.
-template <int JO, int MAXE, int BLK, int PFR, bool IDX>
-__device__ __forceinline__ void lh_inverse_body(const lh::InverseArgs &a, uint32_t *lv) {
-    static_assert(IDX ? (JO == 4 || JO == 8) : (JO >= 1 && JO <= 4), "outputs per wave");
-    constexpr int TILE = BLK > 0 ? BLK : MAXE;
-    const int nw = (int)(blockDim.x >> 6);
-    const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int lane = (int)(threadIdx.x & 63);
-    const int cps = a.bytes >> 11;
-    const long long stripe = blockIdx.x / cps;
-    if (stripe >= a.stripes) return;  // workgroup-uniform
-    const uint8_t *pl = a.plan + stripe * a.plan_stride;
-    const int e = pl[0];
-    if (e == 0) return;  // workgroup-uniform
-    const int m = a.m, sub = a.bytes >> 3;
-    const lh::PlanView pv(pl, a.k, m, a.e_max);
-    const uint32_t rslot = lane < m ? (uint32_t)pv.rec_slot(lane) : 0xFFu;
-    const unsigned long long used = __ballot(rslot != 0xFFu);
-    uint8_t *base = a.blocks + stripe * a.stride + (int)(blockIdx.x % cps) * 256 + lane * 4;
-    const int nout = g < e ? (e - g + nw - 1) / nw : 0;  // outputs g, g + nw, ... (<= JO)
-    uint32_t cpk0 = 0, cpk1 = 0;  // lane r: this wave's coefficients for recovery row r
-    if (rslot != 0xFFu) {
-        const uint8_t *cf = pv.coef_ptr();
-#pragma unroll
-        for (int i = 0; i < JO; ++i)
-            if (i < nout) {
-                const uint32_t c = (uint32_t)cf[(g + i * nw) * m + lane] << (8 * (i & 3));
-                if (i < 4) cpk0 |= c;
-                else cpk1 |= c;
-            }
-    }
-    uint32_t acc[JO][8];
-#pragma unroll
-    for (int i = 0; i < JO; ++i)
-#pragma unroll
-        for (int y = 0; y < 8; ++y) acc[i][y] = 0;
-    auto row_ptr = [&](int r) {
-        const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)rslot, r);
-        return base + (long long)slot * a.bytes;
-    };
-    // This wave stages tile positions j = g, g + nw, ... of each tile.  With PFR > 0 the rows
-    // at positions g + q nw (q < PFR) of the next tile are loaded into pf[q] before the
-    // current tile is computed: unconditional loads into fixed registers (a position past the
-    // tile's rows reloads the tile's first row, unused), so nothing waits for them before the
-    // staging writes.
-    uint32_t pf[PFR > 0 ? PFR : 1][8];
-    auto tile_row = [&](unsigned long long rest, int j) {  // row at tile position j, or -1
-        for (int t = 0; t < j && rest; ++t) rest &= rest - 1;
-        return rest ? __builtin_ctzll(rest) : -1;
-    };
-    auto prefetch = [&](unsigned long long rest) {
-#pragma unroll
-        for (int q = 0; q < (PFR > 0 ? PFR : 1); ++q) {
-            const int j = g + q * nw, r = j < TILE ? tile_row(rest, j) : -1;
-            const uint8_t *p = row_ptr(r >= 0 ? r : __builtin_ctzll(rest));
-#pragma unroll
-            for (int y = 0; y < 8; ++y) pf[q][y] = *(const uint32_t *)(p + (long long)y * sub);
-        }
-    };
-    if (PFR > 0) prefetch(used);
-    unsigned long long todo = used;  // rows not yet staged
-    while (todo) {  // workgroup-uniform
-        {  // stage this tile: prefetched rows from registers, the wave's other rows loaded now
-            int nrows = 0;  // rows in this tile
-            for (unsigned long long rest = todo; rest && nrows < TILE; rest &= rest - 1) ++nrows;
-            if (PFR > 0) {
-#pragma unroll
-                for (int q = 0; q < (PFR > 0 ? PFR : 1); ++q) {
-                    const int j = g + q * nw;
-                    if (j < nrows)
-#pragma unroll
-                        for (int y = 0; y < 8; ++y) lv[(j * 8 + y) * 64 + lane] = pf[q][y];
-                }
-            }
-            for (int j = g + PFR * nw; j < nrows; j += nw) {
-                const uint8_t *p = row_ptr(tile_row(todo, j));
-                uint32_t v[8];
-#pragma unroll
-                for (int y = 0; y < 8; ++y) v[y] = *(const uint32_t *)(p + (long long)y * sub);
-#pragma unroll
-                for (int y = 0; y < 8; ++y) lv[(j * 8 + y) * 64 + lane] = v[y];
-            }
-        }
-        __syncthreads();  // this tile is in LDS
-        unsigned long long next = todo;  // rows after this tile
-        for (int j = 0; next && j < TILE; ++j) next &= next - 1;
-        if (PFR > 0 && next) prefetch(next);  // in flight while this tile is computed
-        for (int j = 0; todo && j < TILE; ++j, todo &= todo - 1) {
-            if (nout == 0) continue;
-            const int r = __builtin_ctzll(todo);
-            uint32_t v[8];
-#pragma unroll
-            for (int y = 0; y < 8; ++y) v[y] = lv[(j * 8 + y) * 64 + lane];
-            uint32_t tl[16], th[16];
-            tl[0] = th[0] = 0;
-#pragma unroll
-            for (int q = 1; q < 16; ++q) {
-                const int low = __builtin_ctz(q), pre = q & (q - 1);
-                tl[q] = pre ? (tl[pre] ^ v[low]) : v[low];
-                th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];
-            }
-            const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)cpk0, r);
-            if constexpr (IDX) {
-                // unused outputs (i >= nout) have coefficient 0: body 0 leaves them unchanged
-                const uint32_t c1 = JO > 4 ? (uint32_t)__builtin_amdgcn_readlane((int)cpk1, r) : 0u;
-                lh_mul_jump_idx<JO>(c0, c1, acc, tl, th);
-            } else {
-#pragma unroll
-                for (int i = 0; i < JO; ++i)
-                    if (i < nout) lh_mul_jump((c0 >> (8 * i)) & 0xFFu, acc[i], tl, th);
-            }
-        }
-        if (todo) __syncthreads();  // the tile is consumed before the next staging
-    }
-    // Every row was staged (read) before the last tile's barrier: the recovery slots may be
-    // overwritten.
-#pragma unroll
-    for (int i = 0; i < JO; ++i) {
-        if (i < nout) {
-            uint8_t *dst = base + (long long)pv.out_slot(g + i * nw) * a.bytes;
-#pragma unroll
-            for (int y = 0; y < 8; ++y) __builtin_nontemporal_store(acc[i][y], (uint32_t *)(dst + (long long)y * sub));
-        }
-    }
-}
-
-// Phase B with the V rows staged by LDS-DMA (round 3): double-buffered tiles of TILE rows,
-// 2 global_load_lds_dwordx4 per row (16 B per lane: lane l moves bytes (l % 16) * 16 of
-// sub-block 4 h + l / 16, so each instruction fills 1 KiB of the row's [sub-block][256 B]
-// image in lane order).  The DMA of tile t + 1 is issued right after the barrier that
-// publishes tile t and lands while tile t is computed; one counted wait + a raw barrier per
-// tile (no __syncthreads, whose fence would drain the DMA).  Same multiply and outputs as
-// lh_inverse_body.
-template <int JO, int TILE, bool IDX>
-__device__ __forceinline__ void lh_inverse_dma_body(const lh::InverseArgs &a, uint32_t *__restrict__ lvA,
-                                                    uint32_t *__restrict__ lvB) {
-    static_assert(IDX ? (JO == 4 || JO == 8) : (JO >= 1 && JO <= 4), "outputs per wave");
-    const int nw = (int)(blockDim.x >> 6);
-    const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int lane = (int)(threadIdx.x & 63);
-    const int cps = a.bytes >> 11;
-    const long long stripe = blockIdx.x / cps;
-    if (stripe >= a.stripes) return;  // workgroup-uniform
-    const uint8_t *pl = a.plan + stripe * a.plan_stride;
-    const int e = pl[0];
-    if (e == 0) return;  // workgroup-uniform
-    const int m = a.m, sub = a.bytes >> 3;
-    const lh::PlanView pv(pl, a.k, m, a.e_max);
-    const uint32_t rslot = lane < m ? (uint32_t)pv.rec_slot(lane) : 0xFFu;
-    const unsigned long long used = __ballot(rslot != 0xFFu);
-    const int chunk = (int)(blockIdx.x % cps) * 256;
-    uint8_t *sbase = a.blocks + stripe * a.stride + chunk;  // wave-uniform
-    uint8_t *base = sbase + lane * 4;
-    const int dof0 = (lane >> 4) * sub + (lane & 15) * 16, dof1 = dof0 + 4 * sub;
-    const int nout = g < e ? (e - g + nw - 1) / nw : 0;  // outputs g, g + nw, ... (<= JO)
-    uint32_t cpk0 = 0, cpk1 = 0;  // lane r: this wave's coefficients for recovery row r
-    if (rslot != 0xFFu) {
-        const uint8_t *cf = pv.coef_ptr();
-#pragma unroll
-        for (int i = 0; i < JO; ++i)
-            if (i < nout) {
-                const uint32_t c = (uint32_t)cf[(g + i * nw) * m + lane] << (8 * (i & 3));
-                if (i < 4) cpk0 |= c;
-                else cpk1 |= c;
-            }
-    }
-    uint32_t acc[JO][8];
-#pragma unroll
-    for (int i = 0; i < JO; ++i)
-#pragma unroll
-        for (int y = 0; y < 8; ++y) acc[i][y] = 0;
     // DMA of the tile starting at `rest` into `buf`: this wave moves tile positions g, g + nw, ...
-    auto issue = [&](unsigned long long rest, uint32_t *buf) {
-        for (int t = 0; t < g && rest; ++t) rest &= rest - 1;  // position g
-        for (int j = g; rest && j < TILE; j += nw) {
-            const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)rslot, __builtin_ctzll(rest));
-            const uint8_t *src = sbase + (long long)slot * a.bytes;
-            uint8_t *dst = (uint8_t *)buf + j * 2048;
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + dof0),
-                                             (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + dof1),
-                                             (__attribute__((address_space(3))) void *)(dst + 1024), 16, 0, 0);
-            for (int t = 0; t < nw && rest; ++t) rest &= rest - 1;
-        }
-    };
-    auto skip_tile = [](unsigned long long rest) {
-        for (int j = 0; rest && j < TILE; ++j) rest &= rest - 1;
-        return rest;
-    };
-    auto compute = [&](unsigned long long rest, const uint32_t *buf) {
-        for (int j = 0; rest && j < TILE; ++j, rest &= rest - 1) {
-            if (nout == 0) continue;
-            const int r = __builtin_ctzll(rest);
-            uint32_t v[8];
-#pragma unroll
-            for (int y = 0; y < 8; ++y) v[y] = buf[(j * 8 + y) * 64 + lane];
-            uint32_t tl[16], th[16];
-            tl[0] = th[0] = 0;
-#pragma unroll
-            for (int q = 1; q < 16; ++q) {
-                const int low = __builtin_ctz(q), pre = q & (q - 1);
-                tl[q] = pre ? (tl[pre] ^ v[low]) : v[low];
-                th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];
-            }
-            const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)cpk0, r);
-            if constexpr (IDX) {
-                const uint32_t c1 = JO > 4 ? (uint32_t)__builtin_amdgcn_readlane((int)cpk1, r) : 0u;
-                lh_mul_jump_idx<JO>(c0, c1, acc, tl, th);
-            } else {
-#pragma unroll
-                for (int i = 0; i < JO; ++i)
-                    if (i < nout) lh_mul_jump((c0 >> (8 * i)) & 0xFFu, acc[i], tl, th);
-            }
-        }
-    };
-    // s_waitcnt vmcnt(0) with expcnt / lgkmcnt untouched; then lgkmcnt(0) (gfx9 encodings)
-    auto publish = [] {
-        __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));   // vmcnt(0): this wave's DMAs landed
-        __builtin_amdgcn_s_waitcnt(0xF | (7 << 4) | (3 << 14));  // lgkmcnt(0): its LDS reads done
-        __builtin_amdgcn_s_barrier();
-    };
-    unsigned long long todo = used;
-    issue(todo, lvA);
-    while (true) {  // workgroup-uniform
-        publish();  // tile in A; every wave is done with B
-        unsigned long long next = skip_tile(todo);
-        if (next) issue(next, lvB);
-        compute(todo, lvA);
-        todo = next;
-        if (!todo) break;
-        publish();  // tile in B; every wave is done with A
-        next = skip_tile(todo);
-        if (next) issue(next, lvA);
-        compute(todo, lvB);
-        todo = next;
-        if (!todo) break;
-    }
-    // Every wave waited for its DMAs before the last barrier: every V row has been read, so
-    // the recovery slots may be overwritten.
-#pragma unroll
-    for (int i = 0; i < JO; ++i) {
-        if (i < nout) {
-            uint8_t *dst = base + (long long)pv.out_slot(g + i * nw) * a.bytes;
-#pragma unroll
-            for (int y = 0; y < 8; ++y) __builtin_nontemporal_store(acc[i][y], (uint32_t *)(dst + (long long)y * sub));
-        }
-    }
-}
-
-template <int JO, int TILE, bool IDX>
-__global__ void __launch_bounds__(1024) lh_inverse_dma_kernel(lh::InverseArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t lvA[TILE * 8 * 64];
-    __shared__ __attribute__((aligned(16))) uint32_t lvB[TILE * 8 * 64];
-    lh_inverse_dma_body<JO, TILE, IDX>(a, lvA, lvB);
-}
-
-// ---- phase B through ONE table per code object (round 3): the 256 bodies sit in the
-// never-launched kernel below under the hidden symbol lh_inv_gtab, every register they
-// touch fixed (tools/gen_inv_jump.py render_global_table).  A wave holds, per output slot i,
-// the absolute low address of the body for row r's coefficient in lane r of t[i] (computed
-// once), so per (output, row) only v_readlane + s_set_gpr_idx_idx + s_swappc_b64 + the
-// body's s_setpc_b64 issue on the scalar unit (3 SALU, against 7 for the in-asm table,
-// whose SALU count exceeded its VALU count: profiles/sq_k128m32.json).
-__global__ void lh_inv_gtab_holder() { asm volatile(LH_INV_GTAB_TEXT); }
-
-template <int N>
-__device__ __forceinline__ void lh_mul_jump_g(uint32_t (&acc)[8][8], const uint32_t (&tl)[16],
-                                              const uint32_t (&th)[16], const uint32_t (&t)[8], int r,
-                                              uint32_t hi) {
-#define LH_GT_CASE(n)                                                                                       \
-    if constexpr (N == n)                                                                                   \
-        asm volatile(LH_INV_JUMPG##n##_ASM : LH_INV_JUMPG##n##_OUTS(acc) : LH_INV_JUMPG_INS(tl, th, t),      \
-                     [r] "s"(r), [hi] "s"(hi) : "s92", "s93", "s94", "s95", "s97", "scc");
-    LH_GT_CASE(1) LH_GT_CASE(2) LH_GT_CASE(3) LH_GT_CASE(4) LH_GT_CASE(5) LH_GT_CASE(6) LH_GT_CASE(7)
-    LH_GT_CASE(8)
-#undef LH_GT_CASE
-}
-
-// 16 outputs per wave: the same calls with all 16 body-address operands.
-template <int N>
-__device__ __forceinline__ void lh_mul_jump_gw(uint32_t (&acc)[16][8], const uint32_t (&tl)[16],
-                                               const uint32_t (&th)[16], const uint32_t (&t)[16], int r,
-                                               uint32_t hi) {
-#define LH_GTW_CASE(n)                                                                                      \
-    if constexpr (N == n)                                                                                   \
-        asm volatile(LH_INV_JUMPG##n##_ASM : LH_INV_JUMPG##n##_OUTS(acc) : LH_INV_JUMPGW_INS(tl, th, t),     \
-                     [r] "s"(r), [hi] "s"(hi) : "s92", "s93", "s94", "s95", "s97", "scc");
-    LH_GTW_CASE(1) LH_GTW_CASE(2) LH_GTW_CASE(3) LH_GTW_CASE(4) LH_GTW_CASE(5) LH_GTW_CASE(6) LH_GTW_CASE(7)
-    LH_GTW_CASE(8) LH_GTW_CASE(9) LH_GTW_CASE(10) LH_GTW_CASE(11) LH_GTW_CASE(12) LH_GTW_CASE(13)
-    LH_GTW_CASE(14) LH_GTW_CASE(15) LH_GTW_CASE(16)
-#undef LH_GTW_CASE
-}
-
-// 4 outputs per wave: the calls for 1..4 outputs with 4 body-address operands.
-template <int N>
-__device__ __forceinline__ void lh_mul_jump_gq(uint32_t (&acc)[4][8], const uint32_t (&tl)[16],
-                                               const uint32_t (&th)[16], const uint32_t (&t)[4], int r,
-                                               uint32_t hi) {
-#define LH_GTQ_CASE(n)                                                                                      \
-    if constexpr (N == n)                                                                                   \
-        asm volatile(LH_INV_JUMPG##n##_ASM : LH_INV_JUMPG##n##_OUTS(acc) : LH_INV_JUMPGQ_INS(tl, th, t),     \
-                     [r] "s"(r), [hi] "s"(hi) : "s92", "s93", "s94", "s95", "s97", "scc");
-    LH_GTQ_CASE(1) LH_GTQ_CASE(2) LH_GTQ_CASE(3) LH_GTQ_CASE(4)
-#undef LH_GTQ_CASE
-}
-
-// Same staging as lh_inverse_dma_body (double-buffered LDS-DMA tiles); the multiply jumps
-// into lh_inv_gtab.  Outputs: PACK ? wave g recovers outputs 8g .. 8g + 7 (fewer waves build
-// the row tables) : g, g + nw, ... as in lh_inverse_dma_body.  The row loop is instantiated
-// per output count (1..8, wave-uniform) so no slot jumps for an unused output.
-template <int TILE, int OPW = 8>
-__device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uint32_t *__restrict__ lvA,
-                                                   uint32_t *__restrict__ lvB, uint32_t tlo, uint32_t thi) {
-    static_assert(OPW == 4 || OPW == 8 || OPW == 16, "outputs per wave");
-    const int nw = (int)(blockDim.x >> 6);
-    const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int lane = (int)(threadIdx.x & 63);
-    const int cps = a.bytes >> 11;
-    const long long stripe = blockIdx.x / cps;
-    if (stripe >= a.stripes) return;  // workgroup-uniform
-    const uint8_t *pl = a.plan + stripe * a.plan_stride;
-    const int e = pl[0];
-    if (e == 0) return;  // workgroup-uniform
-    const int m = a.m, sub = a.bytes >> 3;
-    const lh::PlanView pv(pl, a.k, m, a.e_max);
-    const uint32_t rslot = lane < m ? (uint32_t)pv.rec_slot(lane) : 0xFFu;
-    const unsigned long long used = __ballot(rslot != 0xFFu);
-    const int chunk = (int)(blockIdx.x % cps) * 256;
-    uint8_t *sbase = a.blocks + stripe * a.stride + chunk;  // wave-uniform
-    uint8_t *base = sbase + lane * 4;
-    const int dof0 = (lane >> 4) * sub + (lane & 15) * 16, dof1 = dof0 + 4 * sub;
-    const bool pack = a.pack != 0;
-    int nout = pack ? e - OPW * g : (g < e ? (e - g + nw - 1) / nw : 0);
-    nout = nout < 0 ? 0 : (nout > OPW ? OPW : nout);
-    auto out_of = [&](int i) { return pack ? OPW * g + i : g + i * nw; };
-    uint32_t t[OPW];  // lane r: body address of output slot i for recovery row r
-    {
-        const uint8_t *cf = pv.coef_ptr();
-#pragma unroll
-        for (int i = 0; i < OPW; ++i) {
-            const uint32_t c = (rslot != 0xFFu && i < nout) ? cf[out_of(i) * m + lane] : 0u;
-            t[i] = tlo + c * 68u;
-        }
-    }
-    auto issue = [&](unsigned long long rest, uint32_t *buf) {
-        for (int q = 0; q < g && rest; ++q) rest &= rest - 1;  // position g
-        for (int j = g; rest && j < TILE; j += nw) {
+    __device__ __forceinline__ void issue(unsigned long long rest, uint32_t *buf) const {
+        for (int q = 0; q < g && rest; ++q) rest &= rest - 1;
+        for (int j = g; rest && j < 8; j += nw) {
             const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)rslot, __builtin_ctzll(rest));
             const uint8_t *src = sbase + (long long)slot * a.bytes;
             uint8_t *dst = (uint8_t *)buf + j * 2048;
@@ -1099,77 +690,199 @@ __device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uin
                                              (__attribute__((address_space(3))) void *)(dst + 1024), 16, 0, 0);
             for (int q = 0; q < nw && rest; ++q) rest &= rest - 1;
         }
-    };
-    auto skip_tile = [](unsigned long long rest) {
-        for (int j = 0; rest && j < TILE; ++j) rest &= rest - 1;
+    }
+    __device__ __forceinline__ static unsigned long long skip_tile(unsigned long long rest) {
+        for (int j = 0; rest && j < 8; ++j) rest &= rest - 1;
         return rest;
-    };
-    auto publish = [] {
-        __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));        // vmcnt(0)
-        __builtin_amdgcn_s_waitcnt(0xF | (7 << 4) | (3 << 14));  // lgkmcnt(0)
+    }
+    // s_waitcnt vmcnt(0) (this wave's DMAs landed), then lgkmcnt(0) (its LDS reads done), then
+    // the raw barrier (gfx9 encodings; expcnt / the other counter left at their maxima).
+    __device__ __forceinline__ static void publish() {
+        __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
+        __builtin_amdgcn_s_waitcnt(0xF | (7 << 4) | (3 << 14));
         __builtin_amdgcn_s_barrier();
-    };
-    auto run = [&](auto no) {
-        constexpr int N = decltype(no)::value;
-        uint32_t acc[OPW][8];
-#pragma unroll
-        for (int i = 0; i < OPW; ++i)
-#pragma unroll
-            for (int y = 0; y < 8; ++y) acc[i][y] = 0;
-        auto compute = [&](unsigned long long rest, const uint32_t *buf) {
-            if constexpr (N > 0) {
-                for (int j = 0; rest && j < TILE; ++j, rest &= rest - 1) {
-                    const int r = __builtin_ctzll(rest);
-                    uint32_t v[8];
-#pragma unroll
-                    for (int y = 0; y < 8; ++y) v[y] = buf[(j * 8 + y) * 64 + lane];
-                    uint32_t tl[16], th[16];
-                    tl[0] = th[0] = 0;
-#pragma unroll
-                    for (int q = 1; q < 16; ++q) {
-                        const int low = __builtin_ctz(q), pre = q & (q - 1);
-                        tl[q] = pre ? (tl[pre] ^ v[low]) : v[low];
-                        th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];
-                    }
-                    if constexpr (OPW == 16) lh_mul_jump_gw<N>(acc, tl, th, t, r, thi);
-                    else if constexpr (OPW == 4) lh_mul_jump_gq<N>(acc, tl, th, t, r, thi);
-                    else lh_mul_jump_g<N>(acc, tl, th, t, r, thi);
-                }
-            }
-        };
+    }
+    // The tile loop: compute(rest, buf) multiplies the rows of the tile starting at `rest`.
+    template <class F>
+    __device__ __forceinline__ void tiles(uint32_t *lvA, uint32_t *lvB, F &&compute) const {
         unsigned long long todo = used;
         issue(todo, lvA);
         while (true) {  // workgroup-uniform
-            publish();
+            publish();  // tile in A; every wave is done with B
             unsigned long long next = skip_tile(todo);
             if (next) issue(next, lvB);
             compute(todo, lvA);
             todo = next;
             if (!todo) break;
-            publish();
+            publish();  // tile in B; every wave is done with A
             next = skip_tile(todo);
             if (next) issue(next, lvA);
             compute(todo, lvB);
             todo = next;
             if (!todo) break;
         }
+        // Every wave waited for its DMAs before the last barrier: every V row has been read,
+        // so the recovery slots may be overwritten.
+    }
+    // Row j of a tile: the 16-entry tables of V_r's sub-blocks 0..3 and 4..7.
+    __device__ __forceinline__ void tables(const uint32_t *buf, int j, uint32_t (&tl)[16], uint32_t (&th)[16]) const {
+        uint32_t v[8];
+#pragma unroll
+        for (int y = 0; y < 8; ++y) v[y] = buf[(j * 8 + y) * 64 + lane];
+        tl[0] = th[0] = 0;
+#pragma unroll
+        for (int q = 1; q < 16; ++q) {
+            const int low = __builtin_ctz(q), pre = q & (q - 1);
+            tl[q] = pre ? (tl[pre] ^ v[low]) : v[low];
+            th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];
+        }
+    }
+    __device__ __forceinline__ void store(int out, const uint32_t (&acc)[8]) const {
+        uint8_t *dst = base + (long long)pv.out_slot(out) * a.bytes;
+#pragma unroll
+        for (int y = 0; y < 8; ++y) __builtin_nontemporal_store(acc[y], (uint32_t *)(dst + (long long)y * sub));
+    }
+};
+
+// Fallback form: outputs g, g + nw, ... (at most 8) per wave, the in-asm table.
+__device__ __forceinline__ void lh_inverse_dma_body(const lh::InverseArgs &a, uint32_t *__restrict__ lvA,
+                                                    uint32_t *__restrict__ lvB) {
+    const long long stripe = blockIdx.x / (a.bytes >> 11);
+    if (stripe >= a.stripes) return;  // workgroup-uniform
+    const uint8_t *pl = a.plan + stripe * a.plan_stride;
+    if (pl[0] == 0) return;  // workgroup-uniform
+    const lh_pb_ctx C(a, pl);
+    const int nout = C.g < C.e ? (C.e - C.g + C.nw - 1) / C.nw : 0;
+    uint32_t cpk0 = 0, cpk1 = 0;  // lane r: this wave's coefficients for recovery row r
+    if (C.rslot != 0xFFu) {
+        const uint8_t *cf = C.pv.coef_ptr();
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (i < nout) {
+                const uint32_t c = (uint32_t)cf[(C.g + i * C.nw) * C.m + C.lane] << (8 * (i & 3));
+                if (i < 4) cpk0 |= c;
+                else cpk1 |= c;
+            }
+    }
+    uint32_t acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int y = 0; y < 8; ++y) acc[i][y] = 0;
+    C.tiles(lvA, lvB, [&](unsigned long long rest, const uint32_t *buf) {
+        for (int j = 0; rest && j < 8; ++j, rest &= rest - 1) {
+            if (nout == 0) continue;
+            const int r = __builtin_ctzll(rest);
+            uint32_t tl[16], th[16];
+            C.tables(buf, j, tl, th);
+            // unused outputs (i >= nout) have coefficient 0: body 0 leaves them unchanged
+            lh_mul_jump_idx8((uint32_t)__builtin_amdgcn_readlane((int)cpk0, r),
+                             (uint32_t)__builtin_amdgcn_readlane((int)cpk1, r), acc, tl, th);
+        }
+    });
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        if (i < nout) C.store(C.g + i * C.nw, acc[i]);
+}
+
+// ---- the default: the 256 bodies once per code object, in the never-launched kernel below
+// under the hidden symbol lh_inv_gtab, every register they touch fixed
+// (tools/gen_inv_jump.py render_global_table).  A wave holds, per output slot i, the absolute
+// low address of the body for row r's coefficient in lane r of t[i] (computed once), so per
+// (output, row) only v_readlane + s_set_gpr_idx_idx + s_swappc_b64 + the body's s_setpc_b64
+// issue on the scalar unit (3 SALU, against 7 for the in-asm table).
+//
+// Register and mode state: each LH_INV_JUMPG<n>_ASM statement saves M0,
+// turns GPR indexing on before the first call, moves the index between calls, and turns it
+// off and restores M0 after the last return, in straight-line code; each body is 8 VALU and
+// s_setpc_b64 s[94:95], which the s_swappc_b64 that entered it has just written and nothing
+// in the body writes.  So every call returns to the statement, and control leaves the
+// statement only through its end, with indexing off and M0 restored.  A wave with no
+// outputs (nout == 0) never executes the statement.
+__global__ void lh_inv_gtab_holder() { asm volatile(LH_INV_GTAB_TEXT); }
+
+#ifndef LH_GT_CHECK
+// Debug build (make -C longhair_amd/csrc LH_DEBUG=1): every jump target is checked to be a
+// body of the table before the call, and GPR indexing off after it; a failed check skips
+// the call and poisons the wave's outputs, so the parity tests fail loudly.
+#define LH_GT_CHECK 0
+#endif
+
+template <int N>
+__device__ __forceinline__ bool lh_mul_jump_g(uint32_t (&acc)[8][8], const uint32_t (&tl)[16],
+                                              const uint32_t (&th)[16], const uint32_t (&t)[8], int r,
+                                              uint32_t tlo, uint32_t hi) {
+#if LH_GT_CHECK
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)t[i], r) - tlo;
+        if (d >= 256u * 68u || d % 68u != 0u) return false;  // wave-uniform
+    }
+#else
+    (void)tlo;
+#endif
+#define LH_GT_CASE(n)                                                                                       \
+    if constexpr (N == n)                                                                                   \
+        asm volatile(LH_INV_JUMPG##n##_ASM : LH_INV_JUMPG##n##_OUTS(acc) : LH_INV_JUMPG_INS(tl, th, t),      \
+                     [r] "s"(r), [hi] "s"(hi) : "s92", "s93", "s94", "s95", "s97", "scc");
+    LH_GT_CASE(1) LH_GT_CASE(2) LH_GT_CASE(3) LH_GT_CASE(4) LH_GT_CASE(5) LH_GT_CASE(6) LH_GT_CASE(7)
+    LH_GT_CASE(8)
+#undef LH_GT_CASE
+#if LH_GT_CHECK
+    // MODE.GPR_IDX_EN (bit 27 of HW_REG_MODE on gfx9): must be off again after the statement.
+    if (__builtin_amdgcn_s_getreg(1 | (27 << 6) | (0 << 11)) != 0) return false;
+#endif
+    return true;
+}
+
+// Outputs: pack ? wave g recovers outputs 8g .. 8g + 7 (fewer waves build the row tables) :
+// g, g + nw, ... as the fallback.  The row loop is instantiated per output count (1..8,
+// wave-uniform) so no slot jumps for an unused output.
+__device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uint32_t *__restrict__ lvA,
+                                                   uint32_t *__restrict__ lvB, uint32_t tlo, uint32_t thi) {
+    const long long stripe = blockIdx.x / (a.bytes >> 11);
+    if (stripe >= a.stripes) return;  // workgroup-uniform
+    const uint8_t *pl = a.plan + stripe * a.plan_stride;
+    if (pl[0] == 0) return;  // workgroup-uniform
+    const lh_pb_ctx C(a, pl);
+    const bool pack = a.pack != 0;
+    int nout = pack ? C.e - 8 * C.g : (C.g < C.e ? (C.e - C.g + C.nw - 1) / C.nw : 0);
+    nout = nout < 0 ? 0 : (nout > 8 ? 8 : nout);
+    auto out_of = [&](int i) { return pack ? 8 * C.g + i : C.g + i * C.nw; };
+    uint32_t t[8];  // lane r: body address of output slot i for recovery row r
+    {
+        const uint8_t *cf = C.pv.coef_ptr();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t c = (C.rslot != 0xFFu && i < nout) ? cf[out_of(i) * C.m + C.lane] : 0u;
+            t[i] = tlo + c * 68u;
+        }
+    }
+    auto run = [&](auto no) {
+        constexpr int N = decltype(no)::value;
+        uint32_t acc[8][8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int y = 0; y < 8; ++y) acc[i][y] = 0;
+        bool ok = true;
+        C.tiles(lvA, lvB, [&](unsigned long long rest, const uint32_t *buf) {
+            if constexpr (N > 0) {
+                for (int j = 0; rest && j < 8; ++j, rest &= rest - 1) {
+                    uint32_t tl[16], th[16];
+                    C.tables(buf, j, tl, th);
+                    if (ok) ok = lh_mul_jump_g<N>(acc, tl, th, t, __builtin_ctzll(rest), tlo, thi);
+                }
+            }
+        });
 #pragma unroll
         for (int i = 0; i < N; ++i) {
-            uint8_t *dst = base + (long long)pv.out_slot(out_of(i)) * a.bytes;
+            if (!ok)
 #pragma unroll
-            for (int y = 0; y < 8; ++y) __builtin_nontemporal_store(acc[i][y], (uint32_t *)(dst + (long long)y * sub));
+                for (int y = 0; y < 8; ++y) acc[i][y] = 0xDEADBEEFu;
+            C.store(out_of(i), acc[i]);
         }
     };
-    if constexpr (OPW == 4) {
-        switch (nout) {  // wave-uniform
-            case 0: run(std::integral_constant<int, 0>{}); break;
-            case 1: run(std::integral_constant<int, 1>{}); break;
-            case 2: run(std::integral_constant<int, 2>{}); break;
-            case 3: run(std::integral_constant<int, 3>{}); break;
-            default: run(std::integral_constant<int, 4>{}); break;
-        }
-        return;
-    } else
     switch (nout) {  // wave-uniform
         case 0: run(std::integral_constant<int, 0>{}); break;
         case 1: run(std::integral_constant<int, 1>{}); break;
@@ -1179,33 +892,16 @@ __device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uin
         case 5: run(std::integral_constant<int, 5>{}); break;
         case 6: run(std::integral_constant<int, 6>{}); break;
         case 7: run(std::integral_constant<int, 7>{}); break;
-        case 8: run(std::integral_constant<int, 8>{}); break;
-        default:
-            if constexpr (OPW == 16) {
-                switch (nout) {
-                    case 9: run(std::integral_constant<int, 9>{}); break;
-                    case 10: run(std::integral_constant<int, 10>{}); break;
-                    case 11: run(std::integral_constant<int, 11>{}); break;
-                    case 12: run(std::integral_constant<int, 12>{}); break;
-                    case 13: run(std::integral_constant<int, 13>{}); break;
-                    case 14: run(std::integral_constant<int, 14>{}); break;
-                    case 15: run(std::integral_constant<int, 15>{}); break;
-                    default: run(std::integral_constant<int, 16>{}); break;
-                }
-            } else {
-                run(std::integral_constant<int, 8>{});
-            }
-            break;
+        default: run(std::integral_constant<int, 8>{}); break;
     }
 }
 
 // The table's address comes from a PC-relative relocation.  A table that would straddle a
 // 4 GiB boundary (the body addresses' high word differs; never seen) or a.jump_fallback
 // (tests) takes the in-asm table instead.
-template <int TILE>
 __global__ void __launch_bounds__(1024) lh_inverse_gt_kernel(lh::InverseArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t lvA[TILE * 8 * 64];
-    __shared__ __attribute__((aligned(16))) uint32_t lvB[TILE * 8 * 64];
+    __shared__ __attribute__((aligned(16))) uint32_t lvA[8 * 8 * 64];
+    __shared__ __attribute__((aligned(16))) uint32_t lvB[8 * 8 * 64];
     uint32_t tlo, thi;
     asm volatile(
         "s_getpc_b64 s[92:93]\n"
@@ -1217,137 +913,10 @@ __global__ void __launch_bounds__(1024) lh_inverse_gt_kernel(lh::InverseArgs a) 
         :
         : "s92", "s93", "scc");
     if (a.jump_fallback || tlo > 0xFFFFFFFFu - 256u * 68u) {
-        lh_inverse_dma_body<8, TILE, true>(a, lvA, lvB);
+        lh_inverse_dma_body(a, lvA, lvB);
         return;
     }
-    lh_inverse_gt_body<TILE>(a, lvA, lvB, tlo, thi);
-}
-
-// 16 outputs per wave (LONGHAIR_AMD_INV_GTW=16, a knob): half the waves of the 8-output form,
-// so each row's nibble tables are built by half as many waves.  The host launches it only
-// after lh_inv_gtab_probe showed the table does not straddle a 4 GiB boundary (no in-asm
-// fallback exists for 16 outputs per wave).
-template <int TILE>
-__global__ void __launch_bounds__(256) lh_inverse_gtw_kernel(lh::InverseArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t lvA[TILE * 8 * 64];
-    __shared__ __attribute__((aligned(16))) uint32_t lvB[TILE * 8 * 64];
-    uint32_t tlo, thi;
-    asm volatile(
-        "s_getpc_b64 s[92:93]\n"
-        "s_add_u32 s92, s92, lh_inv_gtab@rel32@lo+4\n"
-        "s_addc_u32 s93, s93, lh_inv_gtab@rel32@hi+12\n"
-        "s_mov_b32 %0, s92\n"
-        "s_mov_b32 %1, s93\n"
-        : "=s"(tlo), "=s"(thi)
-        :
-        : "s92", "s93", "scc");
-    lh_inverse_gt_body<TILE, 16>(a, lvA, lvB, tlo, thi);
-}
-
-// 4 outputs per wave (LONGHAIR_AMD_INV_GTW=4, a knob): twice the waves of the 8-output form
-// (fewer registers, more waves per SIMD), each row's tables built by twice as many waves.
-// The in-asm fallback covers it: with twice the waves, each gets at most 4 outputs.
-template <int TILE>
-__global__ void __launch_bounds__(1024) lh_inverse_gtq_kernel(lh::InverseArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t lvA[TILE * 8 * 64];
-    __shared__ __attribute__((aligned(16))) uint32_t lvB[TILE * 8 * 64];
-    uint32_t tlo, thi;
-    asm volatile(
-        "s_getpc_b64 s[92:93]\n"
-        "s_add_u32 s92, s92, lh_inv_gtab@rel32@lo+4\n"
-        "s_addc_u32 s93, s93, lh_inv_gtab@rel32@hi+12\n"
-        "s_mov_b32 %0, s92\n"
-        "s_mov_b32 %1, s93\n"
-        : "=s"(tlo), "=s"(thi)
-        :
-        : "s92", "s93", "scc");
-    if (a.jump_fallback || tlo > 0xFFFFFFFFu - 256u * 68u) {
-        lh_inverse_dma_body<8, TILE, true>(a, lvA, lvB);
-        return;
-    }
-    lh_inverse_gt_body<TILE, 4>(a, lvA, lvB, tlo, thi);
-}
-
-// Low word of the table's address (one lane stores it): the host checks it once.
-__global__ void lh_inv_gtab_probe(uint32_t *out) {
-    uint32_t tlo;
-    asm volatile(
-        "s_getpc_b64 s[92:93]\n"
-        "s_add_u32 s92, s92, lh_inv_gtab@rel32@lo+4\n"
-        "s_addc_u32 s93, s93, lh_inv_gtab@rel32@hi+12\n"
-        "s_mov_b32 %0, s92\n"
-        : "=s"(tlo)
-        :
-        : "s92", "s93", "scc");
-    if (threadIdx.x == 0) out[0] = tlo;
-}
-
-// One inlined table per output (JO <= 4 copies of 17 KiB).
-template <int JO, int MAXE, int BLK, int PFR>
-__global__ void __launch_bounds__(1024) lh_inverse_jt_kernel(lh::InverseArgs a) {
-    __shared__ uint32_t lv[(BLK > 0 ? BLK : MAXE) * 8 * 64];  // V rows, [row in tile][sub-block][lane]
-    lh_inverse_body<JO, MAXE, BLK, PFR, false>(a, lv);
-}
-
-// One table copy reached by GPR indexing (JO = 4 or 8).
-template <int JO, int MAXE, int BLK, int PFR>
-__global__ void __launch_bounds__(1024) lh_inverse_ji_kernel(lh::InverseArgs a) {
-    __shared__ uint32_t lv[(BLK > 0 ? BLK : MAXE) * 8 * 64];
-    lh_inverse_body<JO, MAXE, BLK, PFR, true>(a, lv);
-}
-
-// OPW: outputs per wave (8, or 4: twice the waves, half the accumulators).
-template <int OPW>
-__global__ void __launch_bounds__(1024) lh_inverse_kernel(lh::InverseArgs a) {
-    const int nw = (int)(blockDim.x >> 6);
-    const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int lane = (int)(threadIdx.x & 63);
-    const int cps = a.bytes >> 11;  // 256-byte chunks per sub-block
-    const long long stripe = blockIdx.x / cps;
-    if (stripe >= a.stripes) return;  // workgroup-uniform
-    const uint8_t *pl = a.plan + stripe * a.plan_stride;
-    const int e = pl[0];
-    if (e == 0) return;  // workgroup-uniform: nothing to recover, or invalid rows
-    const int m = a.m, sub = a.bytes >> 3;
-    const lh::PlanView pv(pl, a.k, m, a.e_max);
-    const uint32_t rslot = lane < m ? (uint32_t)pv.rec_slot(lane) : 0xFFu;
-    const unsigned long long used = __ballot(rslot != 0xFFu);
-    const int nout = g < e ? (e - g + nw - 1) / nw : 0;  // outputs g, g + nw, ... < e
-    uint32_t cpk0 = 0, cpk1 = 0;  // lane r: coefficients of this wave's outputs for row r
-    if (rslot != 0xFFu) {
-        const uint8_t *cf = pv.coef_ptr();
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (i < nout) cpk0 |= (uint32_t)cf[(g + i * nw) * m + lane] << (8 * i);
-            if (OPW > 4 && i + 4 < nout) cpk1 |= (uint32_t)cf[(g + (i + 4) * nw) * m + lane] << (8 * i);
-        }
-    }
-    uint8_t *base = a.blocks + stripe * a.stride + (int)(blockIdx.x % cps) * 256 + lane * 4;
-    uint32_t acc[OPW][8];
-#pragma unroll
-    for (int i = 0; i < OPW; ++i)
-#pragma unroll
-        for (int y = 0; y < 8; ++y) acc[i][y] = 0;
-    switch (nout) {  // wave-uniform
-        case 0: break;
-        case 1: lh_inv_rows<OPW, 1>(acc, base, rslot, used, cpk0, cpk1, a.bytes, sub); break;
-        case 2: lh_inv_rows<OPW, 2>(acc, base, rslot, used, cpk0, cpk1, a.bytes, sub); break;
-        case 3: lh_inv_rows<OPW, 3>(acc, base, rslot, used, cpk0, cpk1, a.bytes, sub); break;
-        case 4: lh_inv_rows<OPW, 4>(acc, base, rslot, used, cpk0, cpk1, a.bytes, sub); break;
-        case 5: lh_inv_rows<OPW, (OPW > 4 ? 5 : 4)>(acc, base, rslot, used, cpk0, cpk1, a.bytes, sub); break;
-        case 6: lh_inv_rows<OPW, (OPW > 4 ? 6 : 4)>(acc, base, rslot, used, cpk0, cpk1, a.bytes, sub); break;
-        case 7: lh_inv_rows<OPW, (OPW > 4 ? 7 : 4)>(acc, base, rslot, used, cpk0, cpk1, a.bytes, sub); break;
-        default: lh_inv_rows<OPW, OPW>(acc, base, rslot, used, cpk0, cpk1, a.bytes, sub); break;
-    }
-    __syncthreads();  // every V row read by every wave before the outputs overwrite them
-#pragma unroll
-    for (int i = 0; i < OPW; ++i) {
-        if (i < nout) {
-            uint8_t *dst = base + (long long)pv.out_slot(g + i * nw) * a.bytes;
-#pragma unroll
-            for (int y = 0; y < 8; ++y) __builtin_nontemporal_store(acc[i][y], (uint32_t *)(dst + (long long)y * sub));
-        }
-    }
+    lh_inverse_gt_body(a, lvA, lvB, tlo, thi);
 }
 
 // ------------------------------------------------------------------ pinned-host write-back
@@ -1397,162 +966,24 @@ hipError_t launch_apply_generic(const ApplyArgs &a, int W, hipStream_t st) {
     return hipGetLastError();
 }
 
-// Whether lh_inv_gtab lies within one 4 GiB window (probed once per process on the current
-// device, on a private stream).
-static bool gtab_no_straddle() {
-    static int ok = -1;
-    static std::mutex mu;
-    std::lock_guard<std::mutex> g(mu);
-    if (ok >= 0) return ok == 1;
-    ok = 0;
-    uint32_t *d = nullptr, h = 0xFFFFFFFFu;
-    hipStream_t s = nullptr;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess && hipMalloc((void **)&d, 4) == hipSuccess) {
-        hipLaunchKernelGGL(lh_inv_gtab_probe, dim3(1), dim3(64), 0, s, d);
-        if (hipMemcpyAsync(&h, d, 4, hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess)
-            ok = h <= 0xFFFFFFFFu - 256u * 68u ? 1 : 0;
-    }
-    if (d) (void)hipFree(d);
-    if (s) (void)hipStreamDestroy(s);
-    (void)hipGetLastError();
-    return ok == 1;
-}
-
 hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     // sub-blocks in 256-byte chunks (the windowed configurations: sub % 256 == 0)
     if (a.bytes % 2048 != 0 || a.e_max < 1 || a.e_max > 64 || a.m > 64) return hipErrorInvalidValue;
     const long long blocks = (long long)a.stripes * (a.bytes / 2048);
     if (blocks <= 0) return hipSuccess;
     if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-    // Phase-B kernel (profiles/r2_tune_split_decode.txt, r3 sessions):
-    // Register-staged phase B (LONGHAIR_AMD_INV_DMA=0, or the variants below):
-    //   LONGHAIR_AMD_INV_JUMP  default: e_max <= 32 as 9, above as 4
-    //                          4 computed jump, one inlined table per output, 4 outputs per
-    //                            wave
-    //                         40 as 4, e_max <= 32 staged all at once
-    //                          5 / 9  one table copy reached by GPR indexing, 4 / 8 outputs
-    //                            per wave
-    //                          2 two outputs per wave (e_max <= 32; larger: Horner)
-    //                          0 the Horner kernel lh_inverse_kernel, LONGHAIR_AMD_INV_OPW =
-    //                            4 (default) or 8 outputs per wave
-    //   LONGHAIR_AMD_INV_PF    rows of the next tile prefetched per wave (0, default, or 2)
-    //   LONGHAIR_AMD_INV_BLK   e_max > 32: rows per tile, 0 (all at once, default) or 16
-    // e_max <= 32 stages 16 rows per tile (32 KiB: k128/m32 decode 4.10 -> 3.84 ms against
-    // all 32 at once).  Measured on one box (profiles/r3d_phase_b.txt, decode incl. planner
-    // and phase A): k128/m32 jt<4> 3.97-3.99 ms, indexed JO 8 3.78-3.80, JO 4 with
-    // prefetch 4.80; prefetch costs 0.8 ms on jt<4> (registers); k200/m56 jt<4,64,0> 0.606,
-    // indexed JO 8 0.634-0.672, 16-row tiles 0.64-0.72.
-    const char *jpe = std::getenv("LONGHAIR_AMD_INV_JUMP");
-    const int jp = jpe ? std::atoi(jpe) : (a.e_max <= 32 ? 9 : 4);
-    const char *pfe = std::getenv("LONGHAIR_AMD_INV_PF");
-    const int pf = pfe && std::atoi(pfe) ? 2 : 0;
-    const char *ble = std::getenv("LONGHAIR_AMD_INV_BLK");
-    const int blk = ble && std::atoi(ble) == 16 ? 16 : 0;
-    const dim3 grid((unsigned)blocks);
-    const bool small = a.e_max <= 32;
-#define LH_LAUNCH_INV(KERNEL, JO, MAXE, BLK, PF)                                                        \
-    do {                                                                                                \
-        hipLaunchKernelGGL((KERNEL<JO, MAXE, BLK, PF>), grid, dim3(64u * (unsigned)((a.e_max + JO - 1) / JO)), 0, \
-                           st, a);                                                                      \
-        note_launch(#KERNEL "<" #JO "," #MAXE "," #BLK "," #PF ">");                                     \
-        return hipGetLastError();                                                                       \
-    } while (0)
-#define LH_LAUNCH_INV_PF(KERNEL, JO, MAXE, BLK)                 \
-    do {                                                        \
-        if (pf) LH_LAUNCH_INV(KERNEL, JO, MAXE, BLK, 2);         \
-        LH_LAUNCH_INV(KERNEL, JO, MAXE, BLK, 0);                 \
-    } while (0)
-    // Default (round 3): V staged by LDS-DMA into double-buffered 8-row tiles, the indexed
-    // single-table jump with 8 outputs per wave, at every e_max (profiles/r3i_phase_b_dma.txt:
-    // k128/m32 decode 3.87-3.88 -> 3.71 ms, k200/m56 0.615-0.622 -> 0.604-0.605; 16-row tiles
-    // 4.59 ms: 64 KiB of LDS per workgroup).  LONGHAIR_AMD_INV_DMA = 0 selects the register-
-    // staged kernels below (LONGHAIR_AMD_INV_JUMP etc.), 8 / 16 the tile rows; with
-    // LONGHAIR_AMD_INV_JUMP = 4 the DMA kernel uses one inlined table per output.
-    const char *dm = std::getenv("LONGHAIR_AMD_INV_DMA");
-    const int dma_rows = dm ? std::atoi(dm) : 8;
-    // LONGHAIR_AMD_INV_JUMP = 10: the DMA staging with the per-code-object table
-    // (lh_inverse_gt_kernel).  (A chained form, each body jumping straight to the next
-    // output's body, was measured in round 3 and removed: a GPU test process running it did
-    // not exit after its tests passed.)
-    // LONGHAIR_AMD_INV_PACK = 1 packs 8 consecutive outputs per wave,
-    // LONGHAIR_AMD_INV_FALLBACK = 1 forces the in-asm-table path inside that kernel (tests).
-    // Default since the end of round 3 (no LONGHAIR_AMD_INV_JUMP): this kernel, outputs
-    // packed 8 per wave for e_max <= 32 and spread above (profiles/r3m_phase_b_gtab.txt, one
-    // box, two rounds: k128/m32 decode 3.56 -> 3.51-3.52 ms packed, k200/m56 0.583-0.584 ->
-    // 0.567-0.568 spread, against lh_inverse_dma_kernel<8,8,true>).
-    if ((jp == 10 || jpe == nullptr) && (dma_rows == 8 || dma_rows == 16)) {
-        InverseArgs g = a;
-        const char *pk = std::getenv("LONGHAIR_AMD_INV_PACK");
-        const char *fb = std::getenv("LONGHAIR_AMD_INV_FALLBACK");
-        g.pack = pk ? (std::atoi(pk) ? 1 : 0) : (a.e_max <= 32 ? 1 : 0);
-        g.jump_fallback = fb && std::atoi(fb) ? 1 : 0;
-        // LONGHAIR_AMD_INV_GTW=16: 16 outputs per wave (the table's address checked once).
-        const char *gw = std::getenv("LONGHAIR_AMD_INV_GTW");
-        if (gw && std::atoi(gw) == 16 && !g.jump_fallback && dma_rows == 8 && gtab_no_straddle()) {
-            hipLaunchKernelGGL((lh_inverse_gtw_kernel<8>), grid, dim3(64u * (unsigned)((a.e_max + 15) / 16)), 0, st, g);
-            note_launch("lh_inverse_gtw_kernel<8>");
-            return hipGetLastError();
-        }
-        if (gw && std::atoi(gw) == 4 && dma_rows == 8) {
-            hipLaunchKernelGGL((lh_inverse_gtq_kernel<8>), grid, dim3(64u * (unsigned)((a.e_max + 3) / 4)), 0, st, g);
-            note_launch(g.jump_fallback ? "lh_inverse_gtq_kernel<8>(fallback)" : "lh_inverse_gtq_kernel<8>");
-            return hipGetLastError();
-        }
-        const dim3 block(64u * (unsigned)((a.e_max + 7) / 8));
-        if (dma_rows == 8) {
-            hipLaunchKernelGGL((lh_inverse_gt_kernel<8>), grid, block, 0, st, g);
-            note_launch(g.jump_fallback ? "lh_inverse_gt_kernel<8>(fallback)" : "lh_inverse_gt_kernel<8>");
-        } else {
-            hipLaunchKernelGGL((lh_inverse_gt_kernel<16>), grid, block, 0, st, g);
-            note_launch(g.jump_fallback ? "lh_inverse_gt_kernel<16>(fallback)" : "lh_inverse_gt_kernel<16>");
-        }
-        return hipGetLastError();
-    }
-    if ((dma_rows == 8 || dma_rows == 16) && (jpe == nullptr || jp == 4 || jp == 9)) {
-        const int t = dma_rows;
-        const bool idx = jpe == nullptr || jp == 9;
-        const int jo = idx ? 8 : 4;
-        const dim3 block(64u * (unsigned)((a.e_max + jo - 1) / jo));
-#define LH_LAUNCH_DMA(JO, T, IDX)                                                              \
-        do {                                                                                   \
-            hipLaunchKernelGGL((lh_inverse_dma_kernel<JO, T, IDX>), grid, block, 0, st, a);   \
-            note_launch("lh_inverse_dma_kernel<" #JO "," #T "," #IDX ">");                       \
-            return hipGetLastError();                                                          \
-        } while (0)
-        if (t == 8 || t == 16) {
-            if (idx && t == 8) LH_LAUNCH_DMA(8, 8, true);
-            if (idx) LH_LAUNCH_DMA(8, 16, true);
-            if (t == 8) LH_LAUNCH_DMA(4, 8, false);
-            LH_LAUNCH_DMA(4, 16, false);
-        }
-#undef LH_LAUNCH_DMA
-    }
-    if (jp == 2 && small) LH_LAUNCH_INV(lh_inverse_jt_kernel, 2, 32, 0, 0);
-    if (jp == 40 && small) LH_LAUNCH_INV(lh_inverse_jt_kernel, 4, 32, 0, 0);
-    if (jp == 5) {
-        if (small) LH_LAUNCH_INV_PF(lh_inverse_ji_kernel, 4, 32, 16);
-        if (blk) LH_LAUNCH_INV_PF(lh_inverse_ji_kernel, 4, 64, 16);
-        LH_LAUNCH_INV(lh_inverse_ji_kernel, 4, 64, 0, 0);
-    }
-    if (jp == 9) {
-        if (small) LH_LAUNCH_INV_PF(lh_inverse_ji_kernel, 8, 32, 16);
-        if (blk) LH_LAUNCH_INV_PF(lh_inverse_ji_kernel, 8, 64, 16);
-        LH_LAUNCH_INV(lh_inverse_ji_kernel, 8, 64, 0, 0);
-    }
-    if (jp != 0 && jp != 2) {
-        if (small) LH_LAUNCH_INV_PF(lh_inverse_jt_kernel, 4, 32, 16);
-        if (blk) LH_LAUNCH_INV_PF(lh_inverse_jt_kernel, 4, 64, 16);
-        LH_LAUNCH_INV(lh_inverse_jt_kernel, 4, 64, 0, 0);
-    }
-#undef LH_LAUNCH_INV_PF
-#undef LH_LAUNCH_INV
-    const char *o = std::getenv("LONGHAIR_AMD_INV_OPW");
-    const int opw = (o && std::atoi(o) == 8) ? 8 : 4;
-    const unsigned threads = 64u * (unsigned)((a.e_max + opw - 1) / opw);
-    if (threads > 1024) return hipErrorInvalidValue;
-    if (opw == 4) hipLaunchKernelGGL(lh_inverse_kernel<4>, grid, dim3(threads), 0, st, a);
-    else hipLaunchKernelGGL(lh_inverse_kernel<8>, grid, dim3(threads), 0, st, a);
-    note_launch(opw == 4 ? "lh_inverse_kernel<4>" : "lh_inverse_kernel<8>");
+    // lh_inverse_gt_kernel: 8 outputs per wave, packed (wave g: outputs 8g .. 8g + 7) for
+    // e_max <= 32 and spread (g, g + nw, ...) above (profiles/r3m_phase_b_gtab.txt: k128/m32
+    // decode 3.56 -> 3.51 ms packed, k200/m56 0.583 -> 0.567 spread).  Knobs:
+    //   LONGHAIR_AMD_INV_PACK=0|1      override the output distribution
+    //   LONGHAIR_AMD_INV_FALLBACK=1    the in-asm table inside the same kernel (tests)
+    InverseArgs g = a;
+    const char *pk = std::getenv("LONGHAIR_AMD_INV_PACK");
+    const char *fb = std::getenv("LONGHAIR_AMD_INV_FALLBACK");
+    g.pack = pk ? (std::atoi(pk) ? 1 : 0) : (a.e_max <= 32 ? 1 : 0);
+    g.jump_fallback = fb && std::atoi(fb) ? 1 : 0;
+    hipLaunchKernelGGL(lh_inverse_gt_kernel, dim3((unsigned)blocks), dim3(64u * (unsigned)((a.e_max + 7) / 8)), 0, st, g);
+    note_launch(g.jump_fallback ? "lh_inverse_gt_kernel(fallback)" : "lh_inverse_gt_kernel");
     return hipGetLastError();
 }
 

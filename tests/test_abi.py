@@ -108,7 +108,7 @@ def test_launch_trace_empty_without_gpu():
 
 
 def test_inv_jump_table_is_generated():
-    """inv_jump.inc (the computed-jump bodies of lh_inverse_jt_kernel) is exactly what
+    """inv_jump.inc (the computed-jump bodies of lh_inverse_gt_kernel) is exactly what
     tools/gen_inv_jump.py renders: no hand edits, no stale generator."""
     import importlib.util
     spec = importlib.util.spec_from_file_location("gen_inv_jump", os.path.join(REPO, "tools", "gen_inv_jump.py"))
@@ -116,9 +116,11 @@ def test_inv_jump_table_is_generated():
     spec.loader.exec_module(gen)
     committed = open(os.path.join(REPO, "longhair_amd", "csrc", "inv_jump.inc")).read()
     assert committed == gen.render()
-    # four tables (per-output copies; indexed for 4 and for 8 outputs; global) of 256 bodies of
-    # 8 v_bitop3_b32 + a branch or return: the fixed 68-byte stride the jump assumes
-    assert committed.count("v_bitop3_b32") == 4 * 256 * 8  # per-output, indexed JO 4 / 8, global
-    assert committed.count("s_branch 3f") == 256
-    assert committed.count("s_setpc_b64 s[94:95]") == 3 * 256
-    assert committed.count("lh_inv_gtab:") == 1 and committed.count("s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)") == 16
+    # two tables (in-asm indexed for 8 outputs; once per code object) of 256 bodies of
+    # 8 v_bitop3_b32 + a return: the fixed 68-byte stride the jump assumes
+    assert committed.count("v_bitop3_b32") == 2 * 256 * 8
+    assert committed.count("s_setpc_b64 s[94:95]") == 2 * 256
+    # every call statement (1..8 outputs) turns GPR indexing on once and off once, and
+    # restores M0 (no path leaves the statement with indexing on)
+    assert committed.count("lh_inv_gtab:") == 1 and committed.count("s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)") == 8
+    assert committed.count("s_set_gpr_idx_off") == 8 + 1 and committed.count("s_mov_b32 m0, s97") == 8 + 1

@@ -25,7 +25,7 @@ SMALL4 = ["lh_plan_small_kernel<4>", "lh_jit_decode"]
 SMALL8 = ["lh_plan_small_kernel<8>", "lh_jit_decode"]
 GENERIC_CF = ["lh_plan_kernel(closed form)", "lh_apply_generic_kernel", "lh_scatter_kernel"]
 GENERIC_S8 = ["lh_plan_small_kernel<8>", "lh_apply_generic_kernel", "lh_scatter_kernel"]
-WIDE16 = ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_gt_kernel<8>"]
+WIDE16 = ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_gt_kernel"]
 WIDE64 = WIDE16  # (one phase-B kernel for every e_max since round 3)
 
 # (id, k, m, bytes, stripes, env, encode kernels, decode kernels)
@@ -66,63 +66,18 @@ BOUNDARIES = [
     ("jump-emax33", 40, 33, 2048, 8, {}, ["lh_jit_encode_win"], WIDE64),
 ]
 
-# Phase-B kernel variants (kernels.hip launch_inverse, LONGHAIR_AMD_INV_JUMP / _INV_OPW).
+# Phase-B kernel (kernels.hip launch_inverse): one kernel, lh_inverse_gt_kernel, with its
+# outputs packed 8 per wave (default for e_max <= 32) or spread (default above), and its
+# in-asm-table fallback.  (Round 3's other six forms were removed in round 4.)
 PHASE_B = [
-    # register-staged V tiles (LONGHAIR_AMD_INV_DMA=0): Horner, per-output tables, indexed
-    ({"LONGHAIR_AMD_INV_JUMP": "0"}, 32, "lh_inverse_kernel<4>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "0", "LONGHAIR_AMD_INV_OPW": "8"}, 32, "lh_inverse_kernel<8>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "0"}, 33, "lh_inverse_kernel<4>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "0", "LONGHAIR_AMD_INV_OPW": "8"}, 33, "lh_inverse_kernel<8>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "2"}, 32, "lh_inverse_jt_kernel<2,32,0,0>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "2"}, 33, "lh_inverse_kernel<4>"),      # e_max > 32: Horner
-    ({"LONGHAIR_AMD_INV_JUMP": "40"}, 32, "lh_inverse_jt_kernel<4,32,0,0>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "40"}, 33, "lh_inverse_jt_kernel<4,64,0,0>"),
-    ({"LONGHAIR_AMD_INV_DMA": "0", "LONGHAIR_AMD_INV_JUMP": "4"}, 32, "lh_inverse_jt_kernel<4,32,16,0>"),
-    ({"LONGHAIR_AMD_INV_DMA": "0", "LONGHAIR_AMD_INV_JUMP": "4", "LONGHAIR_AMD_INV_PF": "1"}, 32,
-     "lh_inverse_jt_kernel<4,32,16,2>"),
-    ({"LONGHAIR_AMD_INV_DMA": "0"}, 33, "lh_inverse_jt_kernel<4,64,0,0>"),
-    ({"LONGHAIR_AMD_INV_DMA": "0", "LONGHAIR_AMD_INV_BLK": "16"}, 33, "lh_inverse_jt_kernel<4,64,16,0>"),
-    ({"LONGHAIR_AMD_INV_DMA": "0", "LONGHAIR_AMD_INV_BLK": "16", "LONGHAIR_AMD_INV_PF": "1"}, 33,
-     "lh_inverse_jt_kernel<4,64,16,2>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "5"}, 32, "lh_inverse_ji_kernel<4,32,16,0>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "5", "LONGHAIR_AMD_INV_PF": "1"}, 32, "lh_inverse_ji_kernel<4,32,16,2>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "5"}, 33, "lh_inverse_ji_kernel<4,64,0,0>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "5", "LONGHAIR_AMD_INV_BLK": "16"}, 33, "lh_inverse_ji_kernel<4,64,16,0>"),
-    ({"LONGHAIR_AMD_INV_DMA": "0"}, 32, "lh_inverse_ji_kernel<8,32,16,0>"),
-    ({"LONGHAIR_AMD_INV_DMA": "0", "LONGHAIR_AMD_INV_PF": "1"}, 32, "lh_inverse_ji_kernel<8,32,16,2>"),
-    ({"LONGHAIR_AMD_INV_DMA": "0", "LONGHAIR_AMD_INV_JUMP": "9"}, 33, "lh_inverse_ji_kernel<8,64,0,0>"),
-    ({"LONGHAIR_AMD_INV_DMA": "0", "LONGHAIR_AMD_INV_JUMP": "9", "LONGHAIR_AMD_INV_BLK": "16"}, 33,
-     "lh_inverse_ji_kernel<8,64,16,0>"),
-    ({"LONGHAIR_AMD_INV_DMA": "0", "LONGHAIR_AMD_INV_JUMP": "9", "LONGHAIR_AMD_INV_BLK": "16",
-      "LONGHAIR_AMD_INV_PF": "1"}, 33, "lh_inverse_ji_kernel<8,64,16,2>"),
-    # V staged by LDS-DMA into double-buffered tiles, in-asm tables: indexed 8 outputs per
-    # wave (the default until the end of round 3) or one inlined table per output
-    ({"LONGHAIR_AMD_INV_JUMP": "9"}, 32, "lh_inverse_dma_kernel<8,8,true>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "9"}, 33, "lh_inverse_dma_kernel<8,8,true>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "9", "LONGHAIR_AMD_INV_DMA": "16"}, 32, "lh_inverse_dma_kernel<8,16,true>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "9", "LONGHAIR_AMD_INV_DMA": "16"}, 33, "lh_inverse_dma_kernel<8,16,true>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "4"}, 32, "lh_inverse_dma_kernel<4,8,false>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "4"}, 33, "lh_inverse_dma_kernel<4,8,false>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "4", "LONGHAIR_AMD_INV_DMA": "16"}, 33, "lh_inverse_dma_kernel<4,16,false>"),
-    # one table per code object (lh_inv_gtab), outputs spread or packed 8 per wave (the
-    # default: packed for e_max <= 32, spread above; 16-row tiles by LONGHAIR_AMD_INV_DMA)
-    ({"LONGHAIR_AMD_INV_DMA": "16"}, 32, "lh_inverse_gt_kernel<16>"),
-    ({"LONGHAIR_AMD_INV_PACK": "0"}, 32, "lh_inverse_gt_kernel<8>"),
-    ({"LONGHAIR_AMD_INV_PACK": "1"}, 33, "lh_inverse_gt_kernel<8>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "10"}, 32, "lh_inverse_gt_kernel<8>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "10"}, 33, "lh_inverse_gt_kernel<8>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "10", "LONGHAIR_AMD_INV_PACK": "1"}, 32, "lh_inverse_gt_kernel<8>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "10", "LONGHAIR_AMD_INV_PACK": "1"}, 64, "lh_inverse_gt_kernel<8>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "10", "LONGHAIR_AMD_INV_DMA": "16"}, 33, "lh_inverse_gt_kernel<16>"),
-    ({"LONGHAIR_AMD_INV_JUMP": "10", "LONGHAIR_AMD_INV_FALLBACK": "1"}, 33, "lh_inverse_gt_kernel<8>(fallback)"),
-    # 16 outputs per wave from the same table (knob)
-    ({"LONGHAIR_AMD_INV_GTW": "16"}, 32, "lh_inverse_gtw_kernel<8>"),
-    ({"LONGHAIR_AMD_INV_GTW": "16"}, 33, "lh_inverse_gtw_kernel<8>"),
-    ({"LONGHAIR_AMD_INV_GTW": "16", "LONGHAIR_AMD_INV_PACK": "0"}, 64, "lh_inverse_gtw_kernel<8>"),
-    # 4 outputs per wave (knob), and its in-asm fallback
-    ({"LONGHAIR_AMD_INV_GTW": "4"}, 32, "lh_inverse_gtq_kernel<8>"),
-    ({"LONGHAIR_AMD_INV_GTW": "4"}, 33, "lh_inverse_gtq_kernel<8>"),
-    ({"LONGHAIR_AMD_INV_GTW": "4", "LONGHAIR_AMD_INV_FALLBACK": "1"}, 33, "lh_inverse_gtq_kernel<8>(fallback)"),
+    ({}, 32, "lh_inverse_gt_kernel"),
+    ({}, 33, "lh_inverse_gt_kernel"),
+    ({"LONGHAIR_AMD_INV_PACK": "0"}, 32, "lh_inverse_gt_kernel"),
+    ({"LONGHAIR_AMD_INV_PACK": "1"}, 33, "lh_inverse_gt_kernel"),
+    ({"LONGHAIR_AMD_INV_PACK": "1"}, 64, "lh_inverse_gt_kernel"),
+    ({"LONGHAIR_AMD_INV_FALLBACK": "1"}, 32, "lh_inverse_gt_kernel(fallback)"),
+    ({"LONGHAIR_AMD_INV_FALLBACK": "1"}, 33, "lh_inverse_gt_kernel(fallback)"),
+    ({"LONGHAIR_AMD_INV_FALLBACK": "1"}, 64, "lh_inverse_gt_kernel(fallback)"),
 ]
 
 
@@ -200,7 +155,7 @@ def test_selection_boundary(lh, oracle, monkeypatch, case):
 
 
 @pytest.mark.parametrize("env,m,kernel", PHASE_B,
-                         ids=[f"{'-'.join(k[17:] + v for k, v in e.items())}-m{m}" for e, m, _ in PHASE_B])
+                         ids=[f"{'-'.join(k[17:] + v for k, v in e.items()) or 'default'}-m{m}" for e, m, _ in PHASE_B])
 def test_phase_b_variant(lh, oracle, monkeypatch, env, m, kernel):
     """Every phase-B kernel of the split large-m decode against the oracle (k = 40, 2048-byte
     blocks, e_max = m), on both sides of e_max = 32."""

@@ -183,3 +183,76 @@ def test_per_call_timing_takes_the_best_round():
     assert out["calls"] == 50 and out["rounds"] == 5
     assert out["encode_us"] < 100 and out["encode_mean_us"] > 300  # one round of 10 x 2 ms in 50 calls
     assert out["decode_us"] <= out["decode_mean_us"]
+
+
+class _StandInCodec:
+    """Host-batch entry points of longhair_amd with the same argument shapes: encode is a
+    no-op, decode puts each stripe's missing originals into its recovery slots (it is handed
+    the originals -- the control path under test does not look at how they were recovered).
+    Rank r sleeps r * 10 ms per call, so the slowest rank is known."""
+
+    def __init__(self, X, k, delay):
+        self.X, self.k, self.delay = X, k, delay
+
+    def encode_host_batch(self, xn, m, recovery=None):
+        import time
+        time.sleep(self.delay)
+
+    def decode_host_batch(self, bn, rn, m):
+        import time
+        time.sleep(self.delay)
+        k = self.k
+        for s in range(bn.shape[0]):
+            missing = sorted(set(range(k)) - set(int(r) for r in rn[s] if r < k))
+            for j in [j for j in range(k) if rn[s, j] >= k]:
+                x = missing.pop(0)
+                bn[s, j] = self.X[s, x]
+                rn[s, j] = x
+
+
+def _pcie_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    k, m, nbytes, n = 6, 3, 65536, 40   # 15.7 MB per rank: rates of a few GB/s at 10-20 ms
+    X = lhutil.fill(40 + rank, n * k * nbytes).reshape(n, k, nbytes)
+    rows = np.array([[3, 4, 5, 6, 7, 8]] * n, dtype=np.uint8)   # originals 0..2 erased
+    slots = X.copy()
+    slots[:, :3] = X[:, 3:]
+    slots[:, 3:] = 0
+    rows[:, :3] = [3, 4, 5]
+    rows[:, 3:] = [k, k + 1, k + 2]
+    b0, r0 = slots.copy(), rows.copy()
+    out = bench.pcie_timed(_StandInCodec(X, k, 0.01 + 0.02 * rank), k, m, nbytes, X, slots, rows,
+                           np.zeros((n, m, nbytes), dtype=np.uint8), b0, r0, world, rank, reps=2, dry=True)
+    dist.destroy_process_group()
+    q.put((rank, out))
+
+
+def test_pcie_leg_aggregation_world2():
+    """bench.pcie_timed (the timed half of the PCIe-inclusive leg) at world 2 on gloo: both
+    ranks make the same cross-rank calls, every rank gets both ranks' rates, the node rate is
+    all input bytes over the slowest rank's time, and `ok` is the AND over ranks."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pcie_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    a, b = results[0], results[1]
+    for out in (a, b):
+        assert out["ok"] is True
+        assert len(out["encode_GBps_per_rank"]) == 2 and len(out["decode_GBps_per_rank"]) == 2
+        # rank 1 sleeps 30 ms per call against rank 0's 10: it is the slower one, and the node
+        # rate is both ranks' bytes over its time
+        assert out["encode_GBps_per_rank"][1] < out["encode_GBps_per_rank"][0]
+        assert out["decode_GBps_per_rank"][1] < out["decode_GBps_per_rank"][0]
+        assert abs(out["node_encode_GBps"] - 2 * out["encode_GBps_per_rank"][1]) <= 0.02
+        assert abs(out["node_decode_GBps"] - 2 * out["decode_GBps_per_rank"][1]) <= 0.02
+    assert a["encode_GBps_per_rank"] == b["encode_GBps_per_rank"]
+    assert a["node_decode_GBps"] == b["node_decode_GBps"]

@@ -1,10 +1,16 @@
 #!/usr/bin/env python3
-"""Generate longhair_amd/csrc/inv_jump.inc: the asm text of lh_inverse_jt_kernel's
-computed jump (kernels.hip).  Body c (68 bytes: 8 VOP3 v_bitop3_b32 + s_branch) adds
-B(c) V to the 8 accumulator words: output sub-row y is acc ^= tl[lo] ^ th[hi] with
-(lo, hi) the nibbles of c * 2^y in GF(2^8)/0x187, tl / th the 16-entry XOR tables of V's
-sub-rows 0..3 / 4..7 (entry 0 = a zero register).  Operands: %0..%7 accumulators,
-%8 the coefficient (SGPR), %9..%24 tl[0..15], %25..%40 th[0..15]."""
+"""Generate longhair_amd/csrc/inv_jump.inc: the asm text of the large-m decode's phase-B
+multiply (kernels.hip lh_inverse_gt_kernel and its fallback; jit.cpp's fused windowed
+decode).  Body c (68 bytes: 8 VOP3 v_bitop3_b32 + the return) adds B(c) V to the 8
+accumulator words of one output: output sub-row y is acc ^= tl[lo] ^ th[hi] with (lo, hi)
+the nibbles of c * 2^y in GF(2^8)/0x187, tl / th the 16-entry XOR tables of V's sub-rows
+0..3 / 4..7 (entry 0 = the inline constant 0).
+
+Two renderings of the same 256 bodies:
+  LH_INV_JUMPI8_*   the table inside the asm statement (one copy per call site), 8 outputs
+  LH_INV_GTAB_TEXT  the table once per code object, entered by LH_INV_JUMPG<n>_ASM
+Run `make -C longhair_amd/csrc regen-inv-jump` after editing; tests/test_abi.py checks that
+the committed file equals this script's output."""
 import os
 
 
@@ -64,8 +70,6 @@ def render_indexed(jo):
 # run: 3 SALU with the body's s_setpc_b64, against 7 for LH_INV_JUMPI.
 GT_TL, GT_TH = 8, 24
 GT_MAX = 8
-# 16 outputs per wave (lh_inverse_gt_kernel<TILE, 16>): accumulators v[IDX_BASE .. IDX_BASE + 127]
-GTW_MAX = 16
 
 
 def render_global_table():
@@ -108,45 +112,19 @@ def render_global_call(n):
 def render():
     """The text of inv_jump.inc."""
     lines = ["// generated by tools/gen_inv_jump.py -- do not edit",
-             "#define LH_INV_JUMP_ASM \\"]
-    # c is masked to 8 bits again here: the jump stays inside the table whatever the
-    # caller passes.
-    body = ["s_getpc_b64 s[96:97]", "0:", "s_and_b32 s98, %8, 0xff", "s_mul_i32 s98, s98, 68",
-            "s_add_u32 s96, s96, s98",
-            "s_addc_u32 s97, s97, 0", "s_add_u32 s96, s96, (2f-0b)", "s_addc_u32 s97, s97, 0",
-            "s_nop 0", "s_setpc_b64 s[96:97]", "2:"]
-    for c in range(256):
-        s = c
-        for y in range(8):
-            lo, hi = s & 15, s >> 4
-            body.append(f"v_bitop3_b32 %{y}, %{y}, %{9 + lo}, %{25 + hi} bitop3:0x96")
-            s = xt(s)
-        body.append("s_branch 3f")
-    body.append("3:")
-    for i, b in enumerate(body):
-        lines.append(f'    "{b}\\n"' + (" \\" if i + 1 < len(body) else ""))
-    lines.append(f"#define LH_INV_IDX_BASE {IDX_BASE}")
-    for jo in (4, 8):
-        lines += render_indexed(jo)
-        outs = ", ".join(f'"+{{v{IDX_BASE + 8 * i + y}}}"(a[{i}][{y}])' for i in range(jo) for y in range(8))
-        lines.append(f"#define LH_INV_JUMPI{jo}_OUTS(a) {outs}")
+             f"#define LH_INV_IDX_BASE {IDX_BASE}"]
+    lines += render_indexed(8)
+    outs = ", ".join(f'"+{{v{IDX_BASE + 8 * i + y}}}"(a[{i}][{y}])' for i in range(8) for y in range(8))
+    lines.append(f"#define LH_INV_JUMPI8_OUTS(a) {outs}")
     ins = ", ".join([f'[t{q}] "v"(tl[{q}])' for q in range(1, 16)] + [f'[h{q}] "v"(th[{q}])' for q in range(1, 16)])
     lines.append(f"#define LH_INV_JUMPI_INS(tl, th) {ins}")
     lines += render_global_table()
-    for n in range(1, GTW_MAX + 1):
+    for n in range(1, GT_MAX + 1):
         lines += render_global_call(n)
     gins = ", ".join([f'"{{v{GT_TL + q}}}"(tl[{q}])' for q in range(1, 16)]
                      + [f'"{{v{GT_TH + q}}}"(th[{q}])' for q in range(1, 16)]
                      + [f'[a{i}] "v"(t[{i}])' for i in range(GT_MAX)])
     lines.append(f"#define LH_INV_JUMPG_INS(tl, th, t) {gins}")
-    wins = ", ".join([f'"{{v{GT_TL + q}}}"(tl[{q}])' for q in range(1, 16)]
-                     + [f'"{{v{GT_TH + q}}}"(th[{q}])' for q in range(1, 16)]
-                     + [f'[a{i}] "v"(t[{i}])' for i in range(GTW_MAX)])
-    lines.append(f"#define LH_INV_JUMPGW_INS(tl, th, t) {wins}")
-    qins = ", ".join([f'"{{v{GT_TL + q}}}"(tl[{q}])' for q in range(1, 16)]
-                     + [f'"{{v{GT_TH + q}}}"(th[{q}])' for q in range(1, 16)]
-                     + [f'[a{i}] "v"(t[{i}])' for i in range(4)])
-    lines.append(f"#define LH_INV_JUMPGQ_INS(tl, th, t) {qins}")
     return "\n".join(lines) + "\n"
 
 
@@ -155,7 +133,7 @@ OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 
 
 
 def main():
-    """Writes inv_jump.inc (run by longhair_amd/csrc/Makefile when this script changes)."""
+    """Writes inv_jump.inc (`make -C longhair_amd/csrc regen-inv-jump`)."""
     with open(OUT, "w") as f:
         f.write(render())
 

@@ -2,7 +2,7 @@
 """Summarise a rocprofv3 SQ counter pass (tools/gpu_pmc_sq.sh) per lh_* kernel into
 profiles/sq_<config>.json, which bench.py reads for the VALU roofline of the large-m
 configs: SQ_INSTS_VALU (wave-level VALU instructions per launch, median over dispatches)
-and the wait / busy ratios.  Usage: sq_summary.py COUNTER_CSV CONFIG"""
+and the wait / busy ratios.  Usage: sq_summary.py COUNTER_CSV CONFIG [OUT_JSON]"""
 import csv
 import json
 import os
@@ -37,7 +37,7 @@ def main():
             agg["wait_any_frac"] = round(agg.get("SQ_WAIT_ANY", 0) / agg["SQ_WAVE_CYCLES"], 4)
         agg["dispatches"] = len(disp)
         out["kernels"][short(name)] = agg
-    dst = os.path.join(REPO, "profiles", f"sq_{cfg}.json")
+    dst = sys.argv[3] if len(sys.argv) > 3 else os.path.join(REPO, "profiles", f"sq_{cfg}.json")
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
