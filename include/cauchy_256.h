@@ -21,11 +21,16 @@
  *   - decode recovers erased originals in place: the i-th recovery Block (array order)
  *     receives the i-th missing original row (ascending) and its row field is
  *     rewritten.  -1 when erasures are present and k + m > 256 or block_bytes % 8 != 0.
- *   - any HIP failure returns -3; rows that index outside the code (row >= k + m or
- *     duplicated rows) return -1 instead of the reference's undefined behaviour.
+ *   - any HIP failure returns -3.  For m > 1, rows that index outside the code
+ *     (row >= k + m) or duplicated rows return -1 instead of the reference's undefined
+ *     behaviour; for m = 1 any rows are accepted, as by the reference's cauchy_decode_m1
+ *     (cauchy_256.cpp:487-535: every row >= k is a recovery block, the last one in array
+ *     order is the output).
  *
- * Buffers may be host memory (pageable or pinned) or HIP device memory; the work always
- * runs on the GPU.  For batches of stripes resident in device memory use
+ * Buffers may be host memory (pageable or pinned) or HIP device memory.  Where a call runs
+ * is the dispatch policy of cauchy_256_dispatch.h: by default (AUTO) a small all-host call
+ * runs on the host SIMD engine and every other call on the GPU; the library needs a GPU
+ * under every policy.  For batches of stripes resident in device memory use
  * cauchy_256_batch.h, which avoids the per-call PCIe round trip.
  */
 #ifndef LONGHAIR_AMD_CAUCHY_256_H

@@ -272,16 +272,19 @@ static int generic_word(int sub) {
     return 1;
 }
 
-// Specialised kernels of a configuration.  Batch calls (allow_compile) compile a missing
-// module with hiprtc unless LONGHAIR_AMD_JIT_COMPILE=0; drop-in calls never compile.
-// Without compiling, a module is still used when it is loaded or in the on-disk cache
-// (jit_cache/, tools/precompile.py); otherwise the caller takes the generic kernels.
-// Returns nullptr with *hard set when a compilation was attempted and failed.
+// Specialised kernels of a configuration.  A module loaded or in the on-disk cache
+// (jit_cache/, tools/precompile.py) is used at once.  Otherwise batch calls (allow_compile)
+// start hiprtc on a background thread and take the generic kernels until the module is
+// ready (batch_jit_mode: LONGHAIR_AMD_JIT_SYNC=1 compiles in the call instead,
+// LONGHAIR_AMD_JIT_COMPILE=0 never compiles); drop-in calls never compile.  Returns nullptr
+// with *hard set when a compilation made for this call (LONGHAIR_AMD_JIT_SYNC=1) failed;
+// a failed background compilation leaves the shape on the generic kernels.
 static const JitKernels *jit_lookup(Device *d, const JitConfig &cfg, bool allow_compile, std::string *err,
                                     bool *hard) {
-    const bool compile = allow_compile && jit_compile_allowed();
-    const JitKernels *jk = d->jit.get(cfg, err, compile);
-    *hard = !jk && compile;
+    const JitMode mode = allow_compile ? batch_jit_mode() : JitMode::kCached;
+    bool failed = false;
+    const JitKernels *jk = d->jit.get(cfg, err, mode, &failed);
+    *hard = !jk && failed && mode == JitMode::kBlocking;
     return jk;
 }
 

@@ -3,8 +3,9 @@
 // (cauchy_256.h:78, :103; README.md:111-182).  A single small stripe is latency-bound:
 // staging it over PCIe to the GPU costs ~30-66 us per call where the bit-sliced XOR work
 // itself is ~2 us of AVX-512 (profiles/r2_bench_k29m4.json, dropin_per_call).  The
-// policy (codec.cpp) sends such calls here only when the caller selects it
-// (cauchy_256_set_dispatch / LONGHAIR_AMD_DISPATCH); the library still requires a GPU.
+// dispatch policy (codec.cpp, cauchy_256_dispatch.h) sends such calls here by default
+// (AUTO: all-host calls with at most LONGHAIR_AMD_HOST_MAX_WORK bytes of XOR work) or when
+// the caller selects HOST; the library still requires a GPU.
 //
 // Both operations are one bit-sliced coefficient apply (same algebra as the GPU kernels):
 //   out[i] sub-row y  ^=  in[j] sub-block b   for every bit b of C[i][j] * 2^y,

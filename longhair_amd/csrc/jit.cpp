@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <sstream>
+#include <thread>
 
 #include "field.hpp"
 
@@ -555,9 +556,14 @@ std::string jit_source_for(const JitConfig &c) {
     return os.str();
 }
 
+JitCache::Key JitCache::key_of(const JitConfig &cfg) {
+    return Key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines,
+               cfg.win_split * 1000000 + cfg.win * 100000 + cfg.win_lds * 10000 + cfg.rows_per_wave * 100 + cfg.win_pf);
+}
+
 const JitKernels *JitCache::peek(const JitConfig &cfg) {
     std::lock_guard<std::mutex> g(mu_);
-    auto it = cache_.find(Key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines, cfg.win_split * 1000000 + cfg.win * 100000 + cfg.win_lds * 10000 + cfg.rows_per_wave * 100 + cfg.win_pf));
+    auto it = cache_.find(key_of(cfg));
     return it == cache_.end() ? nullptr : &it->second;
 }
 
@@ -615,6 +621,38 @@ bool jit_compile_allowed() {
     const char *e = std::getenv("LONGHAIR_AMD_JIT_COMPILE");
     return !(e && std::string(e) == "0");
 }
+
+JitMode batch_jit_mode() {
+    if (!jit_compile_allowed()) return JitMode::kCached;
+    const char *s = std::getenv("LONGHAIR_AMD_JIT_SYNC");
+    return (s && std::string(s) == "1") ? JitMode::kBlocking : JitMode::kAsync;
+}
+
+// Background compilations: joined by jit_join_background(), and at process exit by the
+// registry's destructor (a function-local static, constructed after hiprtc's own state and
+// so destroyed before it: no compile thread outlives the library it calls).
+namespace {
+struct CompileThreads {
+    std::mutex mu;
+    std::vector<std::thread> threads;
+    ~CompileThreads() { join(); }
+    void join() {
+        std::vector<std::thread> t;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            t.swap(threads);
+        }
+        for (auto &th : t)
+            if (th.joinable()) th.join();
+    }
+};
+CompileThreads &compile_threads() {
+    static CompileThreads r;
+    return r;
+}
+}  // namespace
+
+void jit_join_background() { compile_threads().join(); }
 
 bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::string *err, bool fresh, bool compile) {
     const std::string src = jit_source_for(cfg);
@@ -678,28 +716,15 @@ bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::str
     return true;
 }
 
-const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err, bool compile) {
-    std::lock_guard<std::mutex> g(mu_);
-    const Key key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines, cfg.win_split * 1000000 + cfg.win * 100000 + cfg.win_lds * 10000 + cfg.rows_per_wave * 100 + cfg.win_pf);
-    auto it = cache_.find(key);
-    if (it != cache_.end()) return &it->second;
-    if (!compile && not_cached_.count(key)) {  // (generating the source to hash it costs ms)
-        *err = "not cached";
-        return nullptr;
-    }
-
-    std::vector<char> code;
-    if (!compile_code_object(cfg, &code, err, false, compile)) {
-        if (!compile) not_cached_[key] = true;
-        return nullptr;
-    }
-
+// Loads a code object into the current device's context and records its kernels (mu_ held).
+const JitKernels *JitCache::load_locked(const Key &key, const JitConfig &cfg, std::vector<char> &code,
+                                        std::string *err) {
     JitKernels kern;
     kern.cfg = cfg;
     if (hipModuleLoadData(&kern.module, code.data()) != hipSuccess) {
-        // A damaged or foreign cached object: drop it and compile once more.
+        // A damaged or foreign cached object: drop it and compile once more (synchronously).
         (void)hipGetLastError();
-        if (!compile_code_object(cfg, &code, err, true, compile)) return nullptr;
+        if (!compile_code_object(cfg, &code, err, true, true)) return nullptr;
         if (hipModuleLoadData(&kern.module, code.data()) != hipSuccess) {
             *err = "hipModuleLoadData failed for the specialised kernels";
             return nullptr;
@@ -722,8 +747,116 @@ const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err, bool com
         *err = "specialised module has no encode kernel";
         return nullptr;
     }
+    not_cached_.erase(key);
     auto res = cache_.emplace(key, kern);
     return &res.first->second;
+}
+
+const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err, JitMode mode, bool *failed) {
+    const Key key = key_of(cfg);
+    std::shared_ptr<Pending> p;
+    bool compile_here = false;  // kBlocking and no compilation in flight: run hiprtc on this thread
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = cache_.find(key);
+        if (it != cache_.end()) return &it->second;
+        auto f = failed_.find(key);
+        if (f != failed_.end()) {
+            *err = f->second;
+            if (failed) *failed = true;
+            return nullptr;
+        }
+        auto pi = pending_.find(key);
+        if (pi != pending_.end()) {
+            p = pi->second;
+            bool done;
+            {
+                std::lock_guard<std::mutex> pg(p->mu);
+                done = p->done;
+            }
+            if (done) {  // compiled in the background: load it here (this thread's device)
+                pending_.erase(pi);
+                if (!p->ok) {
+                    failed_[key] = *err = p->err;
+                    if (failed) *failed = true;
+                    return nullptr;
+                }
+                return load_locked(key, cfg, p->code, err);
+            }
+            if (mode != JitMode::kBlocking) {
+                *err = "specialised module compiling in the background";
+                return nullptr;
+            }
+        } else {
+            // Not compiled in this process: the on-disk cache (fast: a file read), unless an
+            // earlier cached-only lookup already found nothing there.
+            if (!(mode == JitMode::kCached && not_cached_.count(key))) {
+                std::vector<char> code;
+                std::string e2;
+                if (compile_code_object(cfg, &code, &e2, false, false)) return load_locked(key, cfg, code, err);
+            }
+            if (mode == JitMode::kCached) {
+                not_cached_[key] = true;
+                *err = "not cached";
+                return nullptr;
+            }
+            p = std::make_shared<Pending>();
+            pending_[key] = p;
+            if (mode == JitMode::kAsync) {
+                // hiprtc only (no device calls) on the worker; the module is loaded by the
+                // first lookup after it finishes.
+                std::lock_guard<std::mutex> tg(compile_threads().mu);
+                compile_threads().threads.emplace_back([p, cfg] {
+                    std::vector<char> code;
+                    std::string e;
+                    const bool ok = compile_code_object(cfg, &code, &e, false, true);
+                    std::lock_guard<std::mutex> pg(p->mu);
+                    p->ok = ok;
+                    p->code.swap(code);
+                    p->err = e;
+                    p->done = true;
+                    p->cv.notify_all();
+                });
+                *err = "specialised module compiling in the background";
+                return nullptr;
+            }
+            compile_here = true;
+        }
+    }
+    // kBlocking: compile here without mu_ (other shapes' lookups proceed), or wait for the
+    // compilation in flight.
+    if (compile_here) {
+        std::vector<char> code;
+        std::string e;
+        const bool ok = compile_code_object(cfg, &code, &e, false, true);
+        std::lock_guard<std::mutex> pg(p->mu);
+        p->ok = ok;
+        p->code.swap(code);
+        p->err = e;
+        p->done = true;
+        p->cv.notify_all();
+    } else {
+        std::unique_lock<std::mutex> pg(p->mu);
+        p->cv.wait(pg, [&] { return p->done; });
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = cache_.find(key);
+    if (it != cache_.end()) return &it->second;  // another waiter loaded it
+    auto fi = failed_.find(key);
+    if (fi != failed_.end()) {
+        *err = fi->second;
+        if (failed) *failed = true;
+        return nullptr;
+    }
+    auto pi = pending_.find(key);
+    if (pi != pending_.end() && pi->second == p) pending_.erase(pi);
+    if (!p->ok) {
+        failed_[key] = *err = p->err;
+        if (failed) *failed = true;
+        return nullptr;
+    }
+    std::vector<char> code = p->code;  // other waiters hold p too
+    return load_locked(key, cfg, code, err);
 }
 
 }  // namespace lh

@@ -3,8 +3,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
 #include <cstdint>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <tuple>
@@ -49,20 +51,45 @@ bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode = f
 // Number of ones in the expanded generator (= XORs of the straight-line network).
 long long generator_ones(int k, int m);
 
+// How a lookup may obtain a module that is neither loaded nor in the on-disk cache.
+enum class JitMode {
+    kCached,    // not at all: nullptr, *err = "not cached" (drop-in calls)
+    kAsync,     // start hiprtc on a background thread and return nullptr at once; the
+                // caller serves the call with the generic kernels, a later lookup loads
+                // the module once it is compiled (batch calls, the default)
+    kBlocking,  // compile now (or wait for the compile in flight) and load it
+                // (cauchy_256_batch_prepare*, LONGHAIR_AMD_JIT_SYNC=1)
+};
+
 class JitCache {
 public:
-    // Returns compiled kernels for the configuration (compiling on first use).  On
-    // failure returns nullptr and fills *err.  compile = false: only a module already in
-    // memory or in the on-disk cache (nullptr, *err = "not cached", when there is none).
-    const JitKernels *get(const JitConfig &cfg, std::string *err, bool compile = true);
-    // Only returns an already compiled entry (no compilation).
+    // Kernels of the configuration, obtained as `mode` allows.  nullptr with *err filled
+    // when there is no module (yet); *failed (optional) is set when a compilation of this
+    // configuration failed.  No lock is held while hiprtc runs: lookups of other shapes
+    // (and of this one, in kAsync / kCached mode) proceed meanwhile.
+    const JitKernels *get(const JitConfig &cfg, std::string *err, JitMode mode, bool *failed = nullptr);
+    const JitKernels *get(const JitConfig &cfg, std::string *err) { return get(cfg, err, JitMode::kBlocking); }
+    // Only returns an already loaded entry.
     const JitKernels *peek(const JitConfig &cfg);
 
 private:
     using Key = std::tuple<int, int, int, int, std::string, int>;
+    // A compilation in flight (or finished, not yet loaded); shared with its worker thread,
+    // which touches nothing else of the cache.
+    struct Pending {
+        std::mutex mu;
+        std::condition_variable cv;
+        bool done = false, ok = false;
+        std::vector<char> code;
+        std::string err;
+    };
+    static Key key_of(const JitConfig &cfg);
+    const JitKernels *load_locked(const Key &key, const JitConfig &cfg, std::vector<char> &code, std::string *err);
     std::mutex mu_;
     std::map<Key, JitKernels> cache_;
-    std::map<Key, bool> not_cached_;  // lookups without compilation that found no module
+    std::map<Key, bool> not_cached_;                  // kCached lookups that found no module
+    std::map<Key, std::shared_ptr<Pending>> pending_;  // compilations in flight / not yet loaded
+    std::map<Key, std::string> failed_;               // compilations that failed (not retried)
 };
 
 std::string jit_source_for(const JitConfig &cfg);
@@ -77,5 +104,12 @@ bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::str
 // True unless LONGHAIR_AMD_JIT_COMPILE=0: batch calls may run hiprtc for a shape whose
 // specialised module is not cached (drop-in calls never do).
 bool jit_compile_allowed();
+
+// How batch calls obtain a missing module: kAsync by default, kBlocking with
+// LONGHAIR_AMD_JIT_SYNC=1, kCached with LONGHAIR_AMD_JIT_COMPILE=0.
+JitMode batch_jit_mode();
+
+// Waits for every background compilation to finish (also run at process exit).
+void jit_join_background();
 
 }  // namespace lh

@@ -313,3 +313,48 @@ def test_aligned_decode_buffer(lh, oracle, align):
     for s in range(stripes):
         pad[off + s * stride: off + s * stride + k * nbytes] = False
     assert (raw[pad] == 0x5A).all()
+
+
+def test_jit_compiles_in_background(lh, oracle, monkeypatch, tmp_path):
+    """A batch call on a shape with no specialised module returns at once on the generic
+    kernels while hiprtc compiles the module on a background thread (no lock held: other
+    shapes' lookups proceed); a later call of the same shape launches the specialised
+    kernels.  Bytes against the oracle on both paths (jit.cpp JitCache::get, kAsync)."""
+    import os
+    import time
+
+    import torch
+    monkeypatch.setenv("LONGHAIR_AMD_JIT_SYNC", "0")
+    monkeypatch.setenv("LONGHAIR_AMD_CACHE_DIR", str(tmp_path))  # nothing cached on disk
+    k, m, nbytes, stripes = 13, 3, 88, 40                     # a shape no other test uses
+    data = lhutil.fill(77, stripes * k * nbytes).reshape(stripes, k, nbytes)
+    expect = np.stack([oracle.encode(k, m, data[s], nbytes)[1].reshape(m, nbytes) for s in range(stripes)])
+    x = _gpu(data)
+    t0 = time.perf_counter()
+    rec = lh.encode_batch(x, m)
+    torch.cuda.synchronize()
+    first = time.perf_counter() - t0
+    assert lh.last_launch() == ["lh_apply_generic_kernel"], lh.last_launch()
+    assert first < 1.0, f"first call took {first:.2f} s"
+    assert np.array_equal(rec.cpu().numpy(), expect)
+    # another shape meanwhile: its (cached) module is not held up by the compilation
+    t1 = time.perf_counter()
+    lh.encode_batch(_gpu(lhutil.fill(1, 9 * 29 * 1296).reshape(9, 29, 1296)), 4)
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t1 < 1.0
+    deadline = time.time() + 100
+    while True:
+        rec = lh.encode_batch(x, m)
+        torch.cuda.synchronize()
+        trace = lh.last_launch()
+        if trace == ["lh_jit_encode"]:
+            break
+        assert trace == ["lh_apply_generic_kernel"], trace
+        assert time.time() < deadline, "the background compilation did not finish in 100 s"
+        time.sleep(0.25)
+    assert np.array_equal(rec.cpu().numpy(), expect)
+    assert any(f.endswith(".co") for f in os.listdir(tmp_path)), "the module was not written to the cache"
+    # the same module serves the decode (fused plan: e_max = 3)
+    scen = _scenarios(k, m, stripes, 5)
+    _, dec = roundtrip(lh, oracle, k, m, nbytes, stripes, seed=9, scen=scen)
+    assert dec == FUSED, dec
