@@ -88,6 +88,17 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     cfg->nch = nch2;
     cfg->spw = spw;
     cfg->wps = wps;
+    // Aligned column loads (jit_codec.hip LH_AL): 8-byte lanes over whole stripes whose
+    // sub-blocks start off an 8-byte boundary, when the last lane's valid bytes come from its
+    // own aligned word for every sub-block (LONGHAIR_AMD_JIT_AL=0 turns it off).
+    cfg->al = 0;
+    if (W == 8 && nch2 <= 64 && sub % 8 != 0) {
+        const int vlast = sub - 8 * (nch2 - 1);
+        int smax = 0;
+        for (int b = 0; b < 8; ++b) smax = std::max(smax, (b * sub) % 8);
+        const char *al = std::getenv("LONGHAIR_AMD_JIT_AL");
+        cfg->al = (vlast + smax <= 8 && !(al && std::string(al) == "0")) ? 1 : 0;
+    }
     cfg->defines.clear();
     if (const char *d = std::getenv("LONGHAIR_AMD_JIT_DEFINES")) cfg->defines = d;
     return true;
@@ -111,25 +122,21 @@ bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
     cfg->win = decode ? 2 : 1;
     // Rows per wave: 16 (half the redundant column loads and nibble tables of 8: k128/m32
     // encode 4.21 -> 3.00 ms; split decode phase A: k128/m32 decode 4.24 -> 4.14 ms,
-    // k200/m56 0.87 -> 0.79); 8 for the fused decode, whose V tile in LDS (m x 2 KiB per
-    // workgroup) caps the workgroups per CU, so it needs more waves each.
+    // k200/m56 0.87 -> 0.79), for the fused decode too (its V rows stay in the registers of
+    // the wave that computed them).
     cfg->win_split = decode ? 1 : 0;
     if (const char *sp = std::getenv("LONGHAIR_AMD_WIN_SPLIT")) cfg->win_split = decode && std::atoi(sp) ? 1 : 0;
     // At most 16 rows per wave, spread evenly over the ceil(m / 16) waves: the waves meet
     // at a barrier every column, so the fullest one sets the pace (k200/m56: 14-row groups
     // instead of 16 + 16 + 16 + 8, encode 0.414 -> 0.396 ms, decode 0.810 -> 0.788 ms).
     {
-        const int cap = (decode && !cfg->win_split) ? 8 : 16, ng = (m + cap - 1) / cap;
+        const int cap = 16, ng = (m + cap - 1) / cap;
         cfg->rows_per_wave = (m + ng - 1) / ng;
     }
     if (const char *r = std::getenv("LONGHAIR_AMD_WIN_ROWS")) cfg->rows_per_wave = std::atoi(r);
     if (!decode)  // tuning knob for the encode alone (the decode's phase A keeps its rows)
         if (const char *r = std::getenv("LONGHAIR_AMD_WIN_ROWS_ENC")) cfg->rows_per_wave = std::atoi(r);
     cfg->rows_per_wave = std::max(1, std::min(16, cfg->rows_per_wave));
-    // The fused decode's phase B gives wave g the outputs g, g + NG, ... (NG = ceil(m / rows)),
-    // and holds at most 8 of them (lh_phase_b: acc[8][8], two packed coefficient words): at
-    // most 8 rows per wave keeps ceil(e / NG) <= 8 for every e <= m.
-    if (decode && !cfg->win_split) cfg->rows_per_wave = std::min(8, cfg->rows_per_wave);
     cfg->win_pf = 3;
     if (const char *f = std::getenv("LONGHAIR_AMD_WIN_PF")) cfg->win_pf = std::max(1, std::atoi(f));
     cfg->win_lds = 1;
@@ -173,8 +180,9 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
     const int ndma = (NG == 1 || priv) ? 2 : (g < 2 ? 1 : 0);  // DMA instructions per column, this wave
     const std::string toff = priv ? " + " + std::to_string(g * 2048) : "";  // this wave's ring slot
     const bool split = elim && c.win_split;  // V_r goes back in place of R_r (lh_inverse_kernel follows)
-    os << "__device__ __forceinline__ void lh_wg" << g << "(" << (split ? "" : "const ") << "unsigned char *__restrict__ base, "
-       << (elim ? "const unsigned char *__restrict__ zero, const unsigned int (&slv)[LH_NQ], unsigned int *__restrict__ lv"
+    os << "__device__ __forceinline__ void lh_wg" << g << "(" << (elim ? "" : "const ") << "unsigned char *__restrict__ base, "
+       << (elim ? "const unsigned char *__restrict__ zero, const unsigned int (&slv)[LH_NQ], unsigned int *__restrict__ lv, "
+                  "const unsigned char *__restrict__ pl"
                 : "unsigned char *__restrict__ o")
        << (lds ? ", const unsigned char *__restrict__ sb, const unsigned char *__restrict__ zb" : "")
        << ") {\n";
@@ -281,16 +289,59 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
                 os << "      lh_st(rp + " << y * c.sub << ", a" << (r - r0) << "_" << y << " ^ r" << y << ");\n";
             os << "    }\n  }\n";
         }
-    } else if (elim) {  // V_r = R_r + sum_x ...: XOR the recovery row r (zero page if absent)
+    } else if (elim) {  // fused: V_r = R_r + sum_x ... stays in this wave's registers
         for (int r = r0; r < r1; ++r) {
             os << "  {\n    const unsigned char *rp = lh_slot(slv, " << k + r << ", base, zero);\n";
             for (int y = 0; y < 8; ++y)
                 os << "    a" << (r - r0) << "_" << y << " ^= lh_ld(rp + " << y * c.sub << ");\n";
             os << "  }\n";
         }
-        for (int r = r0; r < r1; ++r)
-            for (int y = 0; y < 8; ++y)
-                os << "  lv[" << (r * 8 + y) * 64 << " + (threadIdx.x & 63)] = a" << (r - r0) << "_" << y << ";\n";
+        // Phase B, 8 outputs at a time: this wave's share sum_{r in its rows} B(coef[i][r]) V_r
+        // of outputs i = ob .. ob + 7 (the computed-jump multiply of inv_jump.inc, one table
+        // build per row), XORed into the workgroup's LDS tile lv[8 outputs][8 sub-rows][64
+        // lanes]; after a barrier each wave stores and clears outputs ob + g, ob + g + NG, ...
+        const int NGt = (m + R - 1) / R, coef_off = 16 + std::min(k, m) + k + m;
+        os << "  const int lnb = threadIdx.x & 63;\n"
+           << "  const int e = pl[0];\n"
+           << "  for (int ob = 0; ob < e; ob += 8) {  // workgroup-uniform\n"
+           << "    unsigned cpk0 = 0, cpk1 = 0;  // lane r: coefficients of outputs ob .. ob + 7 for row r\n"
+           << "    if (lnb < " << m << ") {\n"
+           << "#pragma unroll\n      for (int i = 0; i < 8; ++i)\n"
+           << "        if (ob + i < e) {\n"
+           << "          const unsigned cb = (unsigned)pl[" << coef_off << " + (ob + i) * " << m << " + lnb] << (8 * (i & 3));\n"
+           << "          if (i < 4) cpk0 |= cb; else cpk1 |= cb;\n"
+           << "        }\n    }\n"
+           << "    unsigned acc[8][8];\n"
+           << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n#pragma unroll\n      for (int y = 0; y < 8; ++y) acc[i][y] = 0;\n";
+        for (int r = r0; r < r1; ++r) {
+            const std::string a = "a" + std::to_string(r - r0) + "_";
+            // the pin orders this row's table build after the previous row's multiply (both
+            // volatile): otherwise the scheduler hoists every row's tables and they all live at once
+            os << "    if (__builtin_amdgcn_readlane((int)slv[" << (k + r) / 64 << "], " << (k + r) % 64 << ") != 0xFF) {\n"
+               << "      asm volatile(\"\" :";
+            for (int y = 0; y < 8; ++y) os << (y ? ", " : " ") << "\"+v\"(" << a << y << ")";
+            os << ");\n"
+               << "      unsigned tl[16], th[16];\n      tl[0] = th[0] = 0;\n";
+            for (int q = 1; q < 16; ++q) {
+                const int low = __builtin_ctz(q), pre = q & (q - 1);
+                os << "      tl[" << q << "] = " << (pre ? "tl[" + std::to_string(pre) + "] ^ " : "") << a << low << ";\n"
+                   << "      th[" << q << "] = " << (pre ? "th[" + std::to_string(pre) + "] ^ " : "") << a << 4 + low << ";\n";
+            }
+            os << "      lh_mul8((unsigned)__builtin_amdgcn_readlane((int)cpk0, " << r << "), "
+               << "(unsigned)__builtin_amdgcn_readlane((int)cpk1, " << r << "), acc, tl, th);\n    }\n";
+        }
+        os << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n"
+           << "      if (ob + i < e)\n"
+           << "#pragma unroll\n        for (int y = 0; y < 8; ++y) __hip_atomic_fetch_xor(&lv[(i * 8 + y) * 64 + lnb], acc[i][y],\n"
+           << "                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
+           << "    __syncthreads();  // every wave's share of this batch is in the tile\n"
+           << "    for (int i = " << g << "; i < 8 && ob + i < e; i += " << NGt << ") {\n"
+           << "      unsigned char *dst = base + (long long)pl[16 + ob + i] * " << c.bytes << ";\n"
+           << "#pragma unroll\n      for (int y = 0; y < 8; ++y) {\n"
+           << "        lh_st(dst + " << "y * " << c.sub << ", lv[(i * 8 + y) * 64 + lnb]);\n"
+           << "        lv[(i * 8 + y) * 64 + lnb] = 0u;\n      }\n    }\n"
+           << "    __syncthreads();  // the tile is clear for the next batch\n"
+           << "  }\n";
     } else {
         for (int r = r0; r < r1; ++r)
             for (int y = 0; y < 8; ++y)
@@ -299,136 +350,64 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
     os << "}\n";
 }
 
-// Fused large-m decode (m <= 64, one workgroup per (stripe, 64 * W-byte column chunk)):
+// Large-m decode modules (m <= 64, one workgroup per (stripe, 64 * W-byte column chunk)):
 // phase A (V_r = R_r + sum_{x present} B(G[r][x]) D_x, windowed network above, slot maps
-// from the stripe's plan held in VGPR lanes and read with v_readlane) into an LDS tile,
-// then phase B: wave g recovers D_{E_i} = sum_r B(coef[i][r]) V_r for i in [8g, 8g + 8)
-// from LDS.  Coefficients are workgroup-uniform, so each coefficient bit is a scalar
-// branch; V_r is doubled in place (B(2) in bit-sliced form: (v1..v7, v0^v1^v2^v7)).
+// from the stripe's plan held in VGPR lanes and read with v_readlane).
+//  split (default): V_r written back in place of R_r; phase B is lh_inverse_gt_kernel.
+//  fused (LONGHAIR_AMD_WIN_SPLIT=0, round 4): V stays in the registers of the wave that
+//   computed it and every wave adds its rows' share of each output into an LDS tile of 8
+//   outputs (emit_win_group): no V round trip through HBM and a 16 KiB tile instead of
+//   round 3's m x 2 KiB V tile.
 static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::vector<uint8_t> &G) {
     const int R = c.rows_per_wave, NG = (c.m + R - 1) / R, CPS = c.sub / (64 * c.W);
     const int e_max = std::min(c.k, c.m), km = c.k + c.m;
-    const int coef_off = 16 + e_max + c.k + c.m;  // kernels.hpp PlanView
     os << "#define LH_NQ " << (km + 63) / 64 << "\n"
        << "__device__ __forceinline__ const unsigned char *lh_slot(const unsigned int (&slv)[LH_NQ], const int i,\n"
        << "    const unsigned char *base, const unsigned char *zero) {\n"
        << "  const unsigned int s = (unsigned int)__builtin_amdgcn_readlane((int)slv[i / 64], i % 64);\n"
        << "  return s == 0xFFu ? zero : base + (long long)s * " << c.bytes << ";\n}\n";
-    for (int g = 0; g < NG; ++g) emit_win_group(os, c, G, g);
-    if (c.win_split) {
-        // Phase A only: every present recovery block R_r becomes V_r in place; phase B is
-        // lh_inverse_kernel (kernels.hip), launched after this kernel on the same stream.
-        // No V tile in LDS: the workgroup holds only the column-tile ring, so occupancy is
-        // set by registers, not by m x 2 KiB of LDS.
-        os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
-           << "lh_jit_decode_wide(unsigned char *__restrict__ blocks, long long stride,\n"
-           << "                   const unsigned char *__restrict__ plan, long long plan_stride,\n"
-           << "                   const unsigned char *__restrict__ zero_page, int stripes) {\n"
-           << "  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
-           << "  const int lane = threadIdx.x & 63;\n"
-           << "  const long long stripe = blockIdx.x / " << CPS << ";\n"
-           << "  if (stripe >= stripes) return;\n"
-           << "  const unsigned char *pl = plan + stripe * plan_stride;\n"
-           << "  if (pl[0] == 0) return;\n"
-           << "  unsigned int slv[LH_NQ];\n"
-           << "#pragma unroll\n  for (int q = 0; q < LH_NQ; ++q) {\n"
-           << "    const int i = q * 64 + lane;\n"
-           << "    slv[q] = i < " << km << " ? (unsigned int)pl[" << 16 + e_max << " + i] : 0xFFu;\n"
-           << "  }\n"
-           << "  const int chunk = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << ";\n"
-           << "  unsigned char *b = blocks + stripe * stride + chunk + lane * " << c.W << ";\n"
-           << "  const unsigned char *z = zero_page + chunk + lane * " << c.W << ";\n";
-        const char *dargs = "(b, z, slv, nullptr)";
-        if (c.win_lds) {
-            os << "  const unsigned char *sb = blocks + stripe * stride + chunk;\n"
-               << "  const unsigned char *zb = zero_page + chunk;\n";
-            dargs = "(b, z, slv, nullptr, sb, zb)";
-        }
-        for (int g = 0; g < NG; ++g) os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << dargs << ";\n";
-        os << "}\n";
-        return;
+    if (!c.win_split) {
+        // The computed-jump multiply (inv_jump.inc, the in-asm table reached by GPR indexing,
+        // the 8 accumulators of each output pinned to v[40 + 8i ..]).
+        os << lh_inv_jump_source;
+        os << "__device__ __forceinline__ void lh_mul8(unsigned c0, unsigned c1, unsigned (&a)[8][8],\n"
+           << "    const unsigned (&tl)[16], const unsigned (&th)[16]) {\n"
+           << "  asm volatile(LH_INV_JUMPI8_ASM : LH_INV_JUMPI8_OUTS(a) : [c0] \"s\"(c0), [c1] \"s\"(c1),\n"
+           << "               LH_INV_JUMPI_INS(tl, th) : \"s88\", \"s89\", \"s90\", \"s91\", \"s92\", \"s93\", \"s94\",\n"
+           << "               \"s95\", \"s96\", \"s97\", \"scc\");\n}\n";
     }
-    // Phase B from the LDS tile of V (round 3): wave g recovers outputs g, g + NG, ... (at
-    // most 8: e <= m <= 8 NG) as D_{E_i} = sum_r B(coef[i][r]) V_r with the computed-jump
-    // multiply of kernels.hip (inv_jump.inc, one table copy reached by GPR indexing, the 8
-    // accumulators of each output pinned to v[40 + 8i ..]): per used row the wave reads V_r
-    // from LDS, builds the 16-entry XOR tables of its sub-blocks 0..3 / 4..7 and enters the
-    // table once per output.  (Round 2 did this by Horner over the coefficient bits, one
-    // scalar branch per bit: k128/m32 decode 5.88 ms against 4.77 for the split kernels.)
-    os << lh_inv_jump_source;
-    os << "__device__ __forceinline__ void lh_mul8(unsigned c0, unsigned c1, unsigned (&a)[8][8],\n"
-       << "    const unsigned (&tl)[16], const unsigned (&th)[16]) {\n"
-       << "  asm volatile(LH_INV_JUMPI8_ASM : LH_INV_JUMPI8_OUTS(a) : [c0] \"s\"(c0), [c1] \"s\"(c1),\n"
-       << "               LH_INV_JUMPI_INS(tl, th) : \"s88\", \"s89\", \"s90\", \"s91\", \"s92\", \"s93\", \"s94\",\n"
-       << "               \"s95\", \"s96\", \"s97\", \"scc\");\n}\n";
-    os << "__device__ __forceinline__ void lh_phase_b(const int g, const int e, const int lane,\n"
-       << "    const unsigned *__restrict__ lv, const unsigned char *__restrict__ pl, unsigned char *__restrict__ base) {\n"
-       << "  const int nout = g < e ? (e - g + " << NG - 1 << ") / " << NG << " : 0;  // outputs g, g + " << NG << ", ...\n"
-       << "  if (nout == 0) return;  // wave-uniform\n"
-       << "  const unsigned rs = lane < " << c.m << " ? (unsigned)pl[" << 16 + e_max + c.k << " + lane] : 0xFFu;\n"
-       << "  unsigned long long used = __ballot(rs != 0xFFu);  // recovery rows present, ascending\n"
-       << "  unsigned cpk0 = 0, cpk1 = 0;  // lane r: the wave's coefficients for row r\n"
-       << "  if (rs != 0xFFu) {\n"
-       << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n"
-       << "      if (i < nout) {\n"
-       << "        const unsigned cb = (unsigned)pl[" << coef_off << " + (g + i * " << NG << ") * " << c.m
-       << " + lane] << (8 * (i & 3));\n"
-       << "        if (i < 4) cpk0 |= cb; else cpk1 |= cb;\n"
-       << "      }\n  }\n"
-       << "  unsigned acc[8][8];\n"
-       << "#pragma unroll\n  for (int i = 0; i < 8; ++i)\n#pragma unroll\n    for (int y = 0; y < 8; ++y) acc[i][y] = 0;\n"
-       << "  for (; used; used &= used - 1) {\n"
-       << "    const int r = __builtin_ctzll(used);\n"
-       << "    unsigned v[8];\n"
-       << "#pragma unroll\n    for (int y = 0; y < 8; ++y) v[y] = lv[(r * 8 + y) * 64 + lane];\n"
-       << "    unsigned tl[16], th[16];\n"
-       << "    tl[0] = th[0] = 0;\n"
-       << "#pragma unroll\n    for (int q = 1; q < 16; ++q) {\n"
-       << "      const int low = __builtin_ctz(q), pre = q & (q - 1);\n"
-       << "      tl[q] = pre ? (tl[pre] ^ v[low]) : v[low];\n"
-       << "      th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];\n"
-       << "    }\n"
-       << "    lh_mul8((unsigned)__builtin_amdgcn_readlane((int)cpk0, r), (unsigned)__builtin_amdgcn_readlane((int)cpk1, r),\n"
-       << "            acc, tl, th);\n"
-       << "  }\n"
-       << "#pragma unroll\n  for (int i = 0; i < 8; ++i)\n"
-       << "    if (i < nout) {\n"
-       << "      unsigned char *dst = base + (long long)pl[16 + g + i * " << NG << "] * " << c.bytes << ";\n"
-       << "#pragma unroll\n      for (int y = 0; y < 8; ++y) lh_st(dst + y * " << c.sub << ", acc[i][y]);\n"
-       << "    }\n}\n";
+    for (int g = 0; g < NG; ++g) emit_win_group(os, c, G, g);
     os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
        << "lh_jit_decode_wide(unsigned char *__restrict__ blocks, long long stride,\n"
        << "                   const unsigned char *__restrict__ plan, long long plan_stride,\n"
-       << "                   const unsigned char *__restrict__ zero_page, int stripes) {\n"
-       << "  __shared__ unsigned int lv[" << c.m * 8 * 64 << "];\n"
-       << "  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
+       << "                   const unsigned char *__restrict__ zero_page, int stripes) {\n";
+    if (!c.win_split) os << "  __shared__ unsigned int lv[8 * 8 * 64];  // phase B: 8 outputs x 8 sub-rows x 64 lanes\n";
+    os << "  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
        << "  const int lane = threadIdx.x & 63;\n"
        << "  const long long stripe = blockIdx.x / " << CPS << ";\n"
        << "  if (stripe >= stripes) return;\n"
        << "  const unsigned char *pl = plan + stripe * plan_stride;\n"
-       << "  const int e = pl[0];\n"
-       << "  if (e == 0) return;\n"
+       << "  if (pl[0] == 0) return;  // workgroup-uniform\n"
        << "  unsigned int slv[LH_NQ];\n"
        << "#pragma unroll\n  for (int q = 0; q < LH_NQ; ++q) {\n"
        << "    const int i = q * 64 + lane;\n"
        << "    slv[q] = i < " << km << " ? (unsigned int)pl[" << 16 + e_max << " + i] : 0xFFu;\n"
        << "  }\n"
-       << "  const int p = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << " + lane * " << c.W << ";\n"
-       << "  unsigned char *b = blocks + stripe * stride + p;\n"
-       << "  const unsigned char *z = zero_page + p;\n";
-    const char *dargs = "(b, z, slv, lv)";
+       << "  const int chunk = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << ";\n"
+       << "  unsigned char *b = blocks + stripe * stride + chunk + lane * " << c.W << ";\n"
+       << "  const unsigned char *z = zero_page + chunk + lane * " << c.W << ";\n";
+    if (!c.win_split)
+        os << "  for (int i = threadIdx.x; i < 8 * 8 * 64; i += blockDim.x) lv[i] = 0u;\n"
+           << "  __syncthreads();\n";
+    const std::string lvarg = c.win_split ? "nullptr" : "lv";
+    std::string dargs = "(b, z, slv, " + lvarg + ", pl)";
     if (c.win_lds) {
-        os << "  const int chunk = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << ";\n"
-           << "  const unsigned char *sb = blocks + stripe * stride + chunk;\n"
+        os << "  const unsigned char *sb = blocks + stripe * stride + chunk;\n"
            << "  const unsigned char *zb = zero_page + chunk;\n";
-        dargs = "(b, z, slv, lv, sb, zb)";
+        dargs = "(b, z, slv, " + lvarg + ", pl, sb, zb)";
     }
     for (int g = 0; g < NG; ++g) os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << dargs << ";\n";
-    os << "  __syncthreads();  // V of every row in LDS; every slot read\n"
-       << "#ifndef LH_PB_SKIP  // timing probe only (tools/time_probe.py): phase A alone\n"
-       << "  lh_phase_b(g, e, lane, lv, pl, b);\n"
-       << "#endif\n"
-       << "}\n";
+    os << "}\n";
 }
 
 static std::string win_source_for(const JitConfig &c) {
@@ -532,6 +511,7 @@ std::string jit_source_for(const JitConfig &c) {
     os << "#define LH_K " << c.k << "\n#define LH_M " << c.m << "\n#define LH_BYTES " << c.bytes
        << "\n#define LH_SUB " << c.sub << "\n#define LH_W " << c.W << "\n#define LH_NCH " << c.nch
        << "\n#define LH_SPW " << (c.spw ? c.spw : 1) << "\n#define LH_WPS " << (c.wps ? c.wps : 1) << "\n";
+    if (c.al) os << "#define LH_AL 1\n";
     const std::vector<uint8_t> g = generator_matrix(c.k, c.m);
     os << "static constexpr unsigned char LH_BM[" << c.m << "][" << c.k << "][8] = {";
     for (int r = 0; r < c.m; ++r) {
@@ -558,7 +538,8 @@ std::string jit_source_for(const JitConfig &c) {
 
 JitCache::Key JitCache::key_of(const JitConfig &cfg) {
     return Key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines,
-               cfg.win_split * 1000000 + cfg.win * 100000 + cfg.win_lds * 10000 + cfg.rows_per_wave * 100 + cfg.win_pf);
+               cfg.al * 10000000 + cfg.win_split * 1000000 + cfg.win * 100000 + cfg.win_lds * 10000 +
+                   cfg.rows_per_wave * 100 + cfg.win_pf);
 }
 
 const JitKernels *JitCache::peek(const JitConfig &cfg) {

@@ -212,9 +212,75 @@ __device__ __forceinline__ void lh_column(lh_word (&acc)[LH_M][8], const lh_word
 #endif
 }
 
+// LH_AL = 1 (chosen by the host, jit.cpp: W = 8, whole stripes per wave, sub % 8 != 0):
+// aligned column loads.  Sub-block b of a block starts (b * sub) % 8 = S_b bytes past an
+// 8-byte boundary, so a lane's 8 bytes [p, p + 8) of it straddle two aligned words: every
+// lane loads the aligned word at p - S_b and takes the bytes it lacks from the next lane's
+// word (DPP wave_shl:1, one v_mov per dword, then v_alignbyte; S_b is a compile-time
+// constant per b).  Lanes own p = 8c; the last lane of a stripe (c = nch - 1) holds only
+// LH_VLAST valid bytes, which its own word supplies (the host checks LH_VLAST + S_b <= 8), and
+// stores [sub - 8, sub) assembled with the previous lane's word (DPP wave_shr:1).  The same
+// bytes as 2-byte-aligned 8-byte loads (LH_AL = 0), with 8-byte-aligned load addresses:
+// tools/ubench_floor.hip measures the two access patterns.
+#ifndef LH_AL
+#define LH_AL 0
+#endif
+#if LH_AL
+#if LH_W != 8 || LH_NCH > 64
+#error "LH_AL needs 8-byte lanes and whole stripes per wave"
+#endif
+#define LH_VLAST (LH_SUB - 8 * (LH_NCH - 1))  // valid bytes of the last lane of a stripe
+__device__ __forceinline__ unsigned int lh_dpp_next(unsigned int v) {  // lane i <- lane i + 1
+    return (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
+}
+__device__ __forceinline__ unsigned int lh_dpp_prev(unsigned int v) {  // lane i <- lane i - 1
+    return (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+}
+// Bytes [S, S + 8) of the 16 bytes d[0..3] (little endian), S a compile-time constant.
+template <int S>
+__device__ __forceinline__ lh_word lh_funnel(unsigned int d0, unsigned int d1, unsigned int d2, unsigned int d3) {
+    const unsigned int d[4] = {d0, d1, d2, d3};
+    constexpr int a = S / 4, r = S % 4;
+    lh_word w;
+    if constexpr (r == 0) {
+        w.v[0] = d[a];
+        w.v[1] = d[a + 1];
+    } else {
+        w.v[0] = __builtin_amdgcn_alignbyte(d[a + 1], d[a], r);
+        w.v[1] = __builtin_amdgcn_alignbyte(d[a + 2], d[a + 1], r);
+    }
+    return w;
+}
+// Sub-block B's word loaded from its aligned floor -> the lane's bytes [p, p + 8).
+template <int B>
+__device__ __forceinline__ lh_word lh_realign(const lh_word &w) {
+    constexpr int S = (B * LH_SUB) % 8;
+    if constexpr (S == 0) {
+        return w;
+    } else {
+        // only the next lane's dwords the funnel reads are moved
+        const unsigned int n0 = lh_dpp_next(w.v[0]);
+        const unsigned int n1 = (S > 4) ? lh_dpp_next(w.v[1]) : 0u;
+        return lh_funnel<S>(w.v[0], w.v[1], n0, n1);
+    }
+}
+// The word a lane stores: its own, or for the last lane of a stripe the 8 bytes ending at
+// the sub-block's end (the previous lane's bytes LH_VLAST..7, then its own 0..LH_VLAST-1).
+__device__ __forceinline__ lh_word lh_store_word(const lh_word &w, bool last) {
+    const unsigned int p0 = lh_dpp_prev(w.v[0]), p1 = lh_dpp_prev(w.v[1]);
+    const lh_word f = lh_funnel<LH_VLAST>(p0, p1, w.v[0], w.v[1]);
+    lh_word o;
+    o.v[0] = last ? f.v[0] : w.v[0];
+    o.v[1] = last ? f.v[1] : w.v[1];
+    return o;
+}
+#endif
+
 struct lh_lane {
     long long stripe;
-    int p;
+    int p;       // first byte of the lane's chunk in every sub-block (loads)
+    int ps;      // first byte the lane stores (LH_AL: the last lane stores [sub - 8, sub))
+    bool last;   // last chunk of its stripe
     bool active;
 };
 
@@ -245,7 +311,14 @@ __device__ __forceinline__ lh_lane lh_map_lane(int stripes, long long wave) {
     l.stripe = wave / LH_WPS;
     l.active = (c0 < LH_NCH) && (l.stripe < stripes);
 #endif
-    l.p = (c == LH_NCH - 1) ? (LH_SUB - LH_W) : c * LH_W;
+    l.last = c == LH_NCH - 1;
+#if LH_AL
+    l.p = c * LH_W;
+    l.ps = l.last ? LH_SUB - LH_W : l.p;
+#else
+    l.p = l.last ? (LH_SUB - LH_W) : c * LH_W;
+    l.ps = l.p;
+#endif
     return l;
 }
 
@@ -339,13 +412,36 @@ struct lh_esrc {
     __device__ __forceinline__ lh_word load(int x, int b) const {
         return lh_load_buf<LH_NT ? 2 : 0>(rs, lbase + b * LH_SUB, x * LH_BYTES);
     }
+#if LH_AL
+    template <int B>
+    __device__ __forceinline__ lh_word load_al(int x) const {
+        return lh_realign<B>(lh_load_buf<LH_NT ? 2 : 0>(rs, lbase + B * LH_SUB - (B * LH_SUB) % 8, x * LH_BYTES));
+    }
+#endif
+    // The 8 sub-block words of column x.
+    __device__ __forceinline__ void load8(lh_word (&d)[8], int x) const {
+#if LH_AL
+        d[0] = load_al<0>(x); d[1] = load_al<1>(x); d[2] = load_al<2>(x); d[3] = load_al<3>(x);
+        d[4] = load_al<4>(x); d[5] = load_al<5>(x); d[6] = load_al<6>(x); d[7] = load_al<7>(x);
+#else
+#pragma unroll
+        for (int b = 0; b < 8; ++b) d[b] = load(x, b);
+#endif
+    }
 #else
     const unsigned char *base;
     __device__ __forceinline__ lh_word load(int x, int b) const {
         return lh_load(base + (long long)x * LH_BYTES + b * LH_SUB);
     }
+    __device__ __forceinline__ void load8(lh_word (&d)[8], int x) const {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) d[b] = load(x, b);
+    }
 #endif
 };
+#if LH_AL && !LH_BUF
+#error "LH_AL loads through buffer resources"
+#endif
 
 // Column loop, unrolled at compile time, with the next LH_PF columns' loads in flight
 // while column X is combined.
@@ -357,8 +453,7 @@ struct lh_unroll_encode {
     __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], lh_word (&ring)[LH_PF][8], const lh_esrc &S) {
         if (X + LH_PF < LH_K) {
             lh_word nxt[8];
-#pragma unroll
-            for (int b = 0; b < 8; ++b) nxt[b] = S.load(X + LH_PF, b);
+            S.load8(nxt, X + LH_PF);
             lh_column<X>(acc, ring[X % LH_PF]);
             lh_opaque(acc);
 #pragma unroll
@@ -404,15 +499,18 @@ __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned ch
     lh_word ring[LH_PF][8];
 #pragma unroll
     for (int q = 0; q < LH_PF; ++q)
-        if (q < LH_K)
-#pragma unroll
-            for (int b = 0; b < 8; ++b) ring[q][b] = S.load(q, b);
+        if (q < LH_K) S.load8(ring[q], q);
     lh_unroll_encode<0>::run(acc, ring, S);
-    unsigned char *o = out + l.stripe * out_stride + l.p;
+    unsigned char *o = out + l.stripe * out_stride + l.ps;
 #pragma unroll
     for (int r = 0; r < LH_M; ++r)
 #pragma unroll
-        for (int y = 0; y < 8; ++y) lh_store(o + (long long)r * LH_BYTES + y * LH_SUB, acc[r][y]);
+        for (int y = 0; y < 8; ++y)
+#if LH_AL
+            lh_store(o + (long long)r * LH_BYTES + y * LH_SUB, lh_store_word(acc[r][y], l.last));
+#else
+            lh_store(o + (long long)r * LH_BYTES + y * LH_SUB, acc[r][y]);
+#endif
 }
 
 #if 1
@@ -485,8 +583,15 @@ struct lh_dsrc {
 template <bool NT = (LH_NT_DEC == 1)>
 __device__ __forceinline__ void lh_load_col(lh_word (&d)[8], const lh_dsrc &S, unsigned int slot) {
     const int off = S.col(slot);
+#if LH_AL
+    // an absent column's offset is out of range: zeros, and so are its neighbours' words
+#define LH_ALD(B) d[B] = lh_realign<B>(lh_load_buf<NT ? 2 : 0>(S.rs, off + (B * LH_SUB - (B * LH_SUB) % 8)))
+    LH_ALD(0); LH_ALD(1); LH_ALD(2); LH_ALD(3); LH_ALD(4); LH_ALD(5); LH_ALD(6); LH_ALD(7);
+#undef LH_ALD
+#else
 #pragma unroll
     for (int b = 0; b < 8; ++b) d[b] = lh_load_buf<NT ? 2 : 0>(S.rs, off + b * LH_SUB);
+#endif
 }
 #else
 // Column source of a lane: its stripe's chunk pointer and the zero page.
@@ -634,7 +739,8 @@ __device__ __forceinline__ void lh_dec_phase_a(lh_word (&v)[LH_M][8], lh_word (&
 #define LH_PB_PROBE 0  // timing probe only (tools/tune.py): V_i stored as output i, no phase-B XORs
 #endif
 __device__ __forceinline__ void lh_dec_phase_b(const lh_word (&v)[LH_M][8], const lh_plan_regs &pr,
-                                               unsigned char *base) {
+                                               unsigned char *base, bool last) {
+    (void)last;
     const int e = pr.e;
 #if LH_PB_PROBE
 #pragma unroll
@@ -683,7 +789,12 @@ __device__ __forceinline__ void lh_dec_phase_b(const lh_word (&v)[LH_M][8], cons
             }
             unsigned char *dst = base + (long long)LH_BYTE(outw, i) * LH_BYTES;
 #pragma unroll
-            for (int y = 0; y < 8; ++y) lh_store(dst + y * LH_SUB, o[y]);
+            for (int y = 0; y < 8; ++y)
+#if LH_AL
+                lh_store(dst + y * LH_SUB, lh_store_word(o[y], last));
+#else
+                lh_store(dst + y * LH_SUB, o[y]);
+#endif
         }
     }
 }
@@ -730,7 +841,7 @@ __device__ __forceinline__ void lh_decode_body(const lh_lane &l, long long wave,
 #endif
         lh_dec_phase_a<PF>(v, ring, pr, S);
     }
-    lh_dec_phase_b(v, pr, blocks + l.stripe * stripe_stride + l.p);
+    lh_dec_phase_b(v, pr, blocks + l.stripe * stripe_stride + l.ps, l.last);
 }
 
 __device__ __forceinline__ void lh_decode_wave(long long wave, unsigned char *__restrict__ blocks,

@@ -195,6 +195,38 @@ def test_reference_main_sweep(lh, oracle, monkeypatch):
             "lh_xor_reduce_kernel"} <= seen, sorted(seen)
 
 
+def _jit_sample(n=24, seed=2024):
+    """A seeded sample of register-network shapes outside the boundary pairs and the sweep's
+    precompiled set: k in [17, 128], m in [2, 12], blocks of 16..4096 bytes (k * m <= 700
+    keeps the network within jit.cpp's kMaxNetworkOnes).  tools/precompile.py compiles every
+    one at build time (the test itself never waits on hiprtc)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = []
+    while len(out) < n:
+        k, m = int(rng.integers(17, 129)), int(rng.integers(2, 13))
+        nbytes = 8 * int(rng.integers(2, 513))
+        if k * m <= 700 and (k, m, nbytes) not in out:
+            out.append((k, m, nbytes))
+    return out
+
+
+JIT_SAMPLE = _jit_sample()
+
+
+@pytest.mark.parametrize("k,m,nbytes", JIT_SAMPLE, ids=[f"k{k}m{m}b{b}" for k, m, b in JIT_SAMPLE])
+def test_specialised_sample(lh, oracle, k, m, nbytes):
+    """The hiprtc-specialised kernels (one module per (k, m, bytes), the generator bits as
+    constants) on a seeded sample of shapes: encode through lh_jit_encode, decode through the
+    specialised kernel its e_max selects (fused plan, or the small planner + lh_jit_decode;
+    the generic apply above e_max * m = 64), bytes and rewritten rows against the oracle,
+    random e per stripe (the first at e_max), random recovery rows, shuffled slots."""
+    assert lh.batch_path(k, m, nbytes) == "jit", (k, m, nbytes)
+    enc_k, dec_k = lh.kernel_names(k, m, nbytes)
+    enc, dec = roundtrip(lh, oracle, k, m, nbytes, 24, seed=k * 131 + m * 17 + nbytes)
+    assert enc == ["lh_jit_encode"], enc
+    assert [d.split("<")[0].split("(")[0] for d in dec] == dec_k, (dec, dec_k)
+
+
 @pytest.mark.parametrize("k,nbytes", [(29, 1296), (5, 24), (2, 8)])
 def test_m1_accepts_any_rows_like_the_reference(lh, oracle, k, nbytes):
     """m == 1 decode (cauchy_decode_m1, cauchy_256.cpp:487-535) accepts any rows: rows >= k

@@ -18,7 +18,7 @@ TESTS = [(29, 2, 1296), (29, 3, 1296), (29, 8, 1296), (4, 2, 16), (10, 6, 8), (1
          (128, 32, 1024), (5, 3, 8), (100, 16, 2048), (40, 20, 4096), (250, 6, 2048), (10, 6, 24), (3, 2, 8),
          (64, 4, 4096), (64, 3, 4096), (64, 2, 8192)]
 # Shapes whose fused large-m decode (LONGHAIR_AMD_WIN_SPLIT=0) the GPU tests run.
-VARIANT_SHAPES = [(40, 20, 4096), (100, 16, 2048)]
+VARIANT_SHAPES = [(40, 20, 4096), (100, 16, 2048), (128, 32, 8192), (200, 56, 65536), (250, 6, 2048)]
 
 
 def boundary_jobs():
@@ -70,6 +70,9 @@ def main():
                     jobs_list.append((sh, (None, env)))
                     have.add(sh)
             jobs_list += [(sh, None) for sh in dict.fromkeys(sweep_shapes(tb)) if sh not in have]
+            have |= set(sweep_shapes(tb))
+            # the specialised-kernel parity sample (test_specialised_sample), slowest first
+            jobs_list += [(sh, None) for sh in sorted(tb.JIT_SAMPLE, key=lambda s: -s[0] * s[1]) if sh not in have]
 
             def run(job):
                 shape, part = job
