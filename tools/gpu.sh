@@ -14,7 +14,7 @@
 #   sq[:CFG]         one SQ counter pass (waves, cycles, waits, VALU/VMEM issue)
 #   pcie             tools/pcie_bench.py k29m4 k200m56
 #   ubench:NAME[:G]  tools/NAME (built here beforehand) with optional group list G (commas)
-#   tune:VARIANTS    tools/tune.py with TUNE_VARIANTS=VARIANTS (env TUNE_ROUNDS; TUNE_ARGS='k m bytes stripes')
+#   tune:VARIANTS[@k m bytes stripes]  tools/tune.py with TUNE_VARIANTS=VARIANTS (env TUNE_ROUNDS)
 #   bench2           bench.py --gpus 2 --share-gpu (the N>1 control path on one GPU)
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -77,7 +77,9 @@ for step in "$@"; do
       cat "$OUT/$name.txt" ;;
     tune)
       n=$((${n:-0} + 1))
-      TUNE_VARIANTS="$arg" timeout -k 10 600 python -u tools/tune.py ${TUNE_ARGS:-} > "$OUT/tune$n.txt" 2> "$OUT/tune$n.err" || fail "$step" "$OUT/tune$n.err"
+      targs=""
+      if [ "${arg#*@}" != "$arg" ]; then targs=${arg#*@}; arg=${arg%%@*}; fi
+      TUNE_VARIANTS="$arg" timeout -k 10 600 python -u tools/tune.py $targs > "$OUT/tune$n.txt" 2> "$OUT/tune$n.err" || fail "$step" "$OUT/tune$n.err"
       cat "$OUT/tune$n.txt" ;;
     *)
       echo "unknown step $step"; exit 2 ;;

@@ -227,7 +227,7 @@ __device__ __forceinline__ u32x2 realign(u32x2 w) {
 template <int B, int MODE>
 __device__ __forceinline__ u32x2 aload(__amdgpu_buffer_rsrc_t rs, int lbase, int soff) {
   constexpr int SB = MODE == 1 ? 168 : SUB;
-  constexpr int S = MODE == 1 ? 0 : (2 * B) % 8;
+  constexpr int S = MODE == 1 ? 0 : (2 * B) % 8;  // MODE 3: loads as MODE 2
   const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(rs, lbase + B * SB - S, soff, 2);
   if constexpr (MODE == 1) return w;
   else return realign<B>(w);
@@ -274,7 +274,8 @@ __global__ void __launch_bounds__(256) enc_al(const uint8_t *__restrict__ in, ui
       for (int b = 0; b < 8; ++b) ring[x % PF][b] = nxt[b];
   }
   if (lane >= SPW * NCH || s0 + sl >= stripes) return;
-  uint8_t *o = out + (s0 + sl) * (long long)(M * BY);
+  constexpr int OSB = MODE == 3 ? 168 : SB;  // MODE 3: outputs in 168-byte (aligned) sub-blocks
+  uint8_t *o = out + (s0 + sl) * (long long)(M * 8 * OSB);
 #pragma unroll
   for (int r = 0; r < M; ++r)
 #pragma unroll
@@ -287,7 +288,7 @@ __global__ void __launch_bounds__(256) enc_al(const uint8_t *__restrict__ in, ui
         v = c == NCH - 1 ? w : v;
         p = c == NCH - 1 ? SUB - 8 : p;
       }
-      __builtin_nontemporal_store(v, (u32x2 *)(o + r * BY + y * SB + p));
+      __builtin_nontemporal_store(v, (u32x2 *)(o + r * 8 * OSB + y * OSB + p));
     }
 }
 
@@ -493,6 +494,7 @@ int main(int argc, char **argv) {
     }
     rep("enc dpp-realign PF=3", timeit([&] { enc_al<2, 3><<<ga, 256>>>(din, dout, (int)STRIPES); }));
     rep("enc dpp-realign PF=2", timeit([&] { enc_al<2, 2><<<ga, 256>>>(din, dout, (int)STRIPES); }));
+    rep("enc dpp-realign, aligned stores", timeit([&] { enc_al<3, 3><<<ga, 256>>>(din, dout, (int)STRIPES); }));
     {  // the realigned loads must give the misaligned kernel's bytes
       const size_t ob = (size_t)OUT_BYTES;
       std::vector<uint8_t> h1(ob), h2(ob);
