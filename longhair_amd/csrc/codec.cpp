@@ -13,6 +13,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -140,11 +141,17 @@ struct Device {
     std::vector<uint8_t *> retired;      // outgrown zero pages (never freed: see zero_page)
     std::map<hipStream_t, Workspace> ws;
     JitCache jit;
-    // drop-in (single stripe, host pointers) staging
-    std::mutex dropin_mu;
-    hipStream_t stream = nullptr;
-    DevBuf stage;
-    HostPinned host_stage;
+    // Drop-in (single stripe) calls on the GPU: kDropinSlots independent staging slots, each
+    // with its own stream and buffers, so concurrent callers (the reference's calls are
+    // re-entrant) run side by side instead of one at a time per device.
+    struct DropinSlot {
+        std::mutex mu;
+        hipStream_t stream = nullptr;  // created on first use
+        DevBuf stage;
+        HostPinned host_stage;
+    };
+    static constexpr int kDropinSlots = 4;  // GPU_MAX_HW_QUEUES is 4 by default
+    DropinSlot dropin[kDropinSlots];
     // host-batch pipeline: per ring slot a stream, device buffers and an event
     std::mutex pipe_mu;
     hipStream_t pipe_stream[3] = {nullptr, nullptr, nullptr};
@@ -173,7 +180,6 @@ static int current_device(Device **out) {
         LH_HIP(hipMalloc(&d->gf_log, 256 * sizeof(int16_t)));
         LH_HIP(hipMemcpy(d->gf_exp, F.exp, 512, hipMemcpyHostToDevice));
         LH_HIP(hipMemcpy(d->gf_log, F.log, 256 * sizeof(int16_t), hipMemcpyHostToDevice));
-        LH_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
         LH_HIP(hipDeviceGetAttribute(&d->cus, hipDeviceAttributeMultiprocessorCount, id));
         slot = std::move(d);
     }
@@ -872,6 +878,26 @@ static int classify(const void *const *ptrs, int n, const void *extra) {
     return dev == 0 ? 1 : dev == tot ? 0 : -1;
 }
 
+// A free drop-in slot (the first whose lock is free), else the slot this thread hashes to,
+// waited for.  Its stream is created on first use.
+static int dropin_slot(Device *d, std::unique_lock<std::mutex> *lk, Device::DropinSlot **out) {
+    Device::DropinSlot *s = nullptr;
+    for (int i = 0; i < Device::kDropinSlots && !s; ++i) {
+        std::unique_lock<std::mutex> l(d->dropin[i].mu, std::try_to_lock);
+        if (l.owns_lock()) {
+            *lk = std::move(l);
+            s = &d->dropin[i];
+        }
+    }
+    if (!s) {
+        s = &d->dropin[std::hash<std::thread::id>{}(std::this_thread::get_id()) % Device::kDropinSlots];
+        *lk = std::unique_lock<std::mutex>(s->mu);
+    }
+    if (!s->stream) LH_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    *out = s;
+    return kOk;
+}
+
 static int dropin_encode(int k, int m, const unsigned char *data_ptrs[], void *recovery, int bytes) {
     if (k < 1 || m < 1 || bytes <= 0 || k > 256 || m > 256) return fail(kInvalid, "invalid k, m or block_bytes");
     Device *d = nullptr;
@@ -881,15 +907,17 @@ static int dropin_encode(int k, int m, const unsigned char *data_ptrs[], void *r
         const int rc = host::encode(k, m, (const uint8_t *const *)data_ptrs, (uint8_t *)recovery, bytes);
         return rc == 0 ? kOk : fail(kInvalid, "k + m > 256 or block_bytes % 8 != 0");
     }
-    std::lock_guard<std::mutex> g(d->dropin_mu);
+    std::unique_lock<std::mutex> g;
+    Device::DropinSlot *sl = nullptr;
+    if (int rc = dropin_slot(d, &g, &sl)) return rc;
     const size_t in_n = (size_t)k * bytes, out_n = (size_t)m * bytes;
-    LH_HIP(d->stage.reserve(in_n + out_n));
-    LH_HIP(d->host_stage.reserve(in_n + out_n));
-    hipStream_t st = d->stream;
-    uint8_t *din = d->stage.ptr, *dout = d->stage.ptr + in_n;
+    LH_HIP(sl->stage.reserve(in_n + out_n));
+    LH_HIP(sl->host_stage.reserve(in_n + out_n));
+    hipStream_t st = sl->stream;
+    uint8_t *din = sl->stage.ptr, *dout = sl->stage.ptr + in_n;
     if (where == 1) {  // gather into pinned staging, one host-to-device copy
-        for (int x = 0; x < k; ++x) std::memcpy(d->host_stage.ptr + (size_t)x * bytes, data_ptrs[x], bytes);
-        LH_HIP(hipMemcpyAsync(din, d->host_stage.ptr, in_n, hipMemcpyHostToDevice, st));
+        for (int x = 0; x < k; ++x) std::memcpy(sl->host_stage.ptr + (size_t)x * bytes, data_ptrs[x], bytes);
+        LH_HIP(hipMemcpyAsync(din, sl->host_stage.ptr, in_n, hipMemcpyHostToDevice, st));
     } else {  // device or mixed pointers: the runtime resolves each copy's direction
         for (int x = 0; x < k; ++x) LH_HIP(hipMemcpyAsync(din + (size_t)x * bytes, data_ptrs[x], bytes, hipMemcpyDefault, st));
     }
@@ -901,9 +929,9 @@ static int dropin_encode(int k, int m, const unsigned char *data_ptrs[], void *r
     // On kInvalid only recovery block 0 was produced (reference behaviour).
     const size_t n = (rc == kOk) ? out_n : (size_t)bytes;
     if (where == 1) {
-        LH_HIP(hipMemcpyAsync(d->host_stage.ptr + in_n, dout, n, hipMemcpyDeviceToHost, st));
+        LH_HIP(hipMemcpyAsync(sl->host_stage.ptr + in_n, dout, n, hipMemcpyDeviceToHost, st));
         LH_HIP(hipStreamSynchronize(st));
-        std::memcpy(recovery, d->host_stage.ptr + in_n, n);
+        std::memcpy(recovery, sl->host_stage.ptr + in_n, n);
     } else {
         LH_HIP(hipMemcpyAsync(recovery, dout, n, hipMemcpyDefault, st));
         LH_HIP(hipStreamSynchronize(st));
@@ -935,14 +963,16 @@ static int dropin_decode(int k, int m, Block *blocks, int bytes) {
         }
         return host::decode(k, m, blocks, bytes) == 0 ? kOk : fail(kInvalid, "invalid or duplicated block rows");
     }
-    std::lock_guard<std::mutex> g(d->dropin_mu);
+    std::unique_lock<std::mutex> g;
+    Device::DropinSlot *sl = nullptr;
+    if (int rc = dropin_slot(d, &g, &sl)) return rc;
     // Device and host staging share one layout: [k blocks][256 rows][16 status], so each
     // direction is a single copy for host pointers.
     const size_t in_n = (size_t)k * bytes, tot = in_n + 256 + 16;
-    LH_HIP(d->stage.reserve(tot));
-    LH_HIP(d->host_stage.reserve(tot));
-    hipStream_t st = d->stream;
-    uint8_t *hs = d->host_stage.ptr, *ds = d->stage.ptr;
+    LH_HIP(sl->stage.reserve(tot));
+    LH_HIP(sl->host_stage.reserve(tot));
+    hipStream_t st = sl->stream;
+    uint8_t *hs = sl->host_stage.ptr, *ds = sl->stage.ptr;
     uint8_t *hrows = hs + in_n, *drows = ds + in_n;
     for (int i = 0; i < k; ++i) hrows[i] = blocks[i].row;
     if (where == 1) {

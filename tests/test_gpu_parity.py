@@ -130,6 +130,52 @@ def test_dropin_random_vs_oracle(lh, oracle, policy, k, m, nbytes, cases):
         assert all(a.tobytes() == b.tobytes() for a, b in zip(bufs, exp)), (k, m, c, e)
 
 
+@pytest.mark.parametrize("k,m,nbytes", [(29, 4, 1296), (128, 32, 8192)])
+def test_dropin_concurrent_callers(lh, oracle, k, m, nbytes):
+    """Drop-in calls from several threads at once on the GPU (policy GPU): each call takes one
+    of the device's independent staging slots (own stream and buffers), so concurrent callers
+    are not serialised; every result against the oracle (computed beforehand)."""
+    import threading
+    codec = DropIn(lh)
+    cases = []
+    rng = np.random.Generator(np.random.PCG64(k + 7 * m))
+    for c in range(24):
+        data = lhutil.fill(int(rng.integers(0, 2**31)), k * nbytes).reshape(k, nbytes)
+        rc_o, rec_o = oracle.encode(k, m, data, nbytes)
+        e = int(rng.integers(1, min(k, m) + 1))
+        slots, rows = lhutil.erasure_case(int(rng.integers(0, 2**31)), k, m, e)
+        rec = rec_o.reshape(m, nbytes)
+        bufs = [(data[x] if kind == "d" else rec[x]).copy() for kind, x in slots]
+        exp = [b.copy() for b in bufs]
+        rc_d, exp_rows = oracle.decode(k, m, exp, rows, nbytes)
+        assert rc_o == rc_d == 0
+        cases.append((data, rec_o, bufs, rows, exp, exp_rows))
+    errors = []
+
+    def worker(t):
+        try:
+            for c in range(t, len(cases), 4):
+                data, rec_o, bufs, rows, exp, exp_rows = cases[c]
+                rc, rec = codec.encode(k, m, data, nbytes)
+                assert rc == 0 and rec.tobytes() == rec_o.tobytes(), ("encode", c)
+                rc, got_rows = codec.decode(k, m, bufs, rows, nbytes)
+                assert rc == 0 and got_rows == exp_rows, ("rows", c)
+                assert all(a.tobytes() == b.tobytes() for a, b in zip(bufs, exp)), ("decode", c)
+        except Exception as ex:  # noqa: BLE001 -- reported below
+            errors.append(ex)
+
+    prev = lh.set_dispatch("gpu")
+    try:
+        threads = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=120)
+    finally:
+        lh.set_dispatch(prev)
+    assert not errors, errors
+
+
 def test_dropin_invalid_rows_untouched(lh, policy):
     """Duplicate or out-of-range rows: -1 and the blocks untouched (documented deviation:
     undefined behaviour in the reference, cauchy_256.cpp:612-614, :733)."""
