@@ -16,6 +16,7 @@
 #   ubench:NAME[:G]  tools/NAME (built here beforehand) with optional group list G (commas)
 #   tune:VARIANTS[@k m bytes stripes]  tools/tune.py with TUNE_VARIANTS=VARIANTS (env TUNE_ROUNDS)
 #   bench2           bench.py --gpus 2 --share-gpu (the N>1 control path on one GPU)
+#   benchg[:CFG]     bench.py on the generic kernels only (LONGHAIR_AMD_PATH=generic), 5 steps
 set -o pipefail
 cd "$(dirname "$0")/.."
 OUT=gpurun_out/${1:?usage: tools/gpu.sh OUT STEP...}
@@ -44,6 +45,10 @@ for step in "$@"; do
       [ "$cfg" != k29m4 ] && extra=(--steps 5 --warmup 2)
       timeout -k 10 400 python bench.py --config "$cfg" "${extra[@]}" > "$OUT/bench_$cfg.json" 2> "$OUT/bench_$cfg.err" || fail "$step" "$OUT/bench_$cfg.err"
       cat "$OUT/bench_$cfg.json" ;;
+    benchg)
+      cfg=${arg:-k29m4}
+      LONGHAIR_AMD_PATH=generic timeout -k 10 400 python bench.py --config "$cfg" --steps 5 --warmup 2 --cpu-baseline off --pcie off --dropin-calls 0 > "$OUT/benchg_$cfg.json" 2> "$OUT/benchg_$cfg.err" || fail "$step" "$OUT/benchg_$cfg.err"
+      cat "$OUT/benchg_$cfg.json" ;;
     bench2)
       timeout -k 10 600 python bench.py --gpus 2 --share-gpu --steps 10 --warmup 2 > "$OUT/bench_gpus2.json" 2> "$OUT/bench_gpus2.err" || fail "$step" "$OUT/bench_gpus2.err"
       cat "$OUT/bench_gpus2.json" ;;
