@@ -276,6 +276,45 @@ __device__ __forceinline__ lh_word lh_store_word(const lh_word &w, bool last) {
 }
 #endif
 
+// LH_ALS = 1 (with LH_AL; a tuning knob): the outputs are stored as 8-byte-aligned words too.
+// In store instruction y, lane c stores the aligned word at y * sub - S_y + 8c of the block
+// (S_y = (y * sub) % 8): bytes 8 - S_y.. of the previous lane's chunk then its own, gathered
+// with ds_bpermute; lane 0 takes the previous sub-block's last bytes from its stripe's last
+// lane, which shares the 8 bytes ending at that sub-block's end instead of its own chunk.
+// The last lane's word extends into the next sub-block unless S_y >= 8 - LH_VLAST: then
+// the next instruction's lane 0 stores it and this lane's store gets an out-of-range
+// buffer offset (dropped).  Stores go through a buffer resource over the wave's stripes.
+#ifndef LH_ALS
+#define LH_ALS 0
+#endif
+#if LH_AL && LH_ALS
+template <int AUX>
+__device__ __forceinline__ void lh_store_buf(const lh_word &w, const __amdgpu_buffer_rsrc_t &rs, int off) {
+    const lh_u32x2 v = {w.v[0], w.v[1]};
+    __builtin_amdgcn_raw_buffer_store_b64(v, rs, off, 0, AUX);
+}
+// One block row (8 sub-row words, the lane's chunk of each sub-block) at byte offset `blk`
+// of the resource.  c: the lane's chunk; src: lane c - 1, or for c = 0 its stripe's last lane.
+template <int Y = 0>
+__device__ __forceinline__ void lh_store_block_al(const __amdgpu_buffer_rsrc_t &rs, int blk, int c, int src,
+                                                  const lh_word (&w)[8], lh_word lprev) {
+    if constexpr (Y < 8) {
+        constexpr int S = (Y * LH_SUB) % 8;
+        const bool last = c == LH_NCH - 1;
+        lh_word word = w[Y];
+        if constexpr (S != 0) {
+            const unsigned int s0 = last ? lprev.v[0] : w[Y].v[0], s1 = last ? lprev.v[1] : w[Y].v[1];
+            const unsigned int p0 = (unsigned int)__builtin_amdgcn_ds_bpermute(src * 4, (int)s0);
+            const unsigned int p1 = (unsigned int)__builtin_amdgcn_ds_bpermute(src * 4, (int)s1);
+            word = lh_funnel<8 - S>(p0, p1, w[Y].v[0], w[Y].v[1]);
+        }
+        const bool skip = last && S < 8 - LH_VLAST;
+        lh_store_buf<LH_NT_ST ? 2 : 0>(word, rs, skip ? (int)0x80000000 : blk + Y * LH_SUB - S + 8 * c);
+        if constexpr (Y < 7) lh_store_block_al<Y + 1>(rs, blk, c, src, w, lh_store_word(w[Y], true));
+    }
+}
+#endif
+
 struct lh_lane {
     long long stripe;
     int p;       // first byte of the lane's chunk in every sub-block (loads)
@@ -501,6 +540,22 @@ __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned ch
     for (int q = 0; q < LH_PF; ++q)
         if (q < LH_K) S.load8(ring[q], q);
     lh_unroll_encode<0>::run(acc, ring, S);
+#if LH_AL && LH_ALS
+    {
+        const long long s0o = (long long)__builtin_amdgcn_readfirstlane((int)wave) * LH_SPW;
+        const long long nso = (stripes - s0o) < LH_SPW ? (stripes - s0o) : LH_SPW;
+        if (nso * out_stride < (1ll << 31)) {  // wave-uniform: the outputs in one 32-bit range
+            const __amdgpu_buffer_rsrc_t ro =
+                __builtin_amdgcn_make_buffer_rsrc(out + s0o * out_stride, 0, (int)(nso * out_stride), 0x00020000);
+            const int lane = threadIdx.x & 63, c = lane % LH_NCH;
+            const int src = c == 0 ? lane + LH_NCH - 1 : lane - 1;
+            const int so = (int)((l.stripe - s0o) * out_stride);
+#pragma unroll
+            for (int r = 0; r < LH_M; ++r) lh_store_block_al(ro, so + r * LH_BYTES, c, src, acc[r], acc[r][0]);
+            return;
+        }
+    }
+#endif
     unsigned char *o = out + l.stripe * out_stride + l.ps;
 #pragma unroll
     for (int r = 0; r < LH_M; ++r)
