@@ -7,6 +7,7 @@
 # OUT names gpurun_out/OUT/.  Steps:
 #   tests            pytest -m gpu (every GPU parity test), one process
 #   tests:EXPR       pytest -m gpu -k EXPR
+#   testscheck[:EXPR] pytest -m gpu -k EXPR (default phase_b) on the phase-B checked build
 #   smoke            __graft_entry__.smoke()
 #   bench[:CFG]      bench.py (default k29m4; k128m32 / k200m56 with 5 steps)
 #   prof[:CFG]       rocprofv3 --kernel-trace --stats of a short bench run
@@ -35,6 +36,11 @@ for step in "$@"; do
       sel=()
       [ -n "$arg" ] && sel=(-k "$arg")
       timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${sel[@]}" > "$log" 2>&1 || fail "$step" "$log"
+      tail -3 "$log" ;;
+    testscheck)
+      # the phase-B checked build (make -C longhair_amd/csrc LH_DEBUG=1 OUT=... BUILD=...)
+      log="$OUT/pytest_gpu_check.txt"
+      LONGHAIR_AMD_LIBRARY=liblonghair_amd_check.so timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${arg:-phase_b}" > "$log" 2>&1 || fail "$step" "$log"
       tail -3 "$log" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.txt" 2>&1 || fail smoke "$OUT/smoke.txt"
