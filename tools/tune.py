@@ -98,6 +98,8 @@ def main():
                 torch.cuda.synchronize()
                 tot += d0.elapsed_time(d1)
             results[name][1].append(tot / reps)
+            print(f"round {rnd} {name}: encode {results[name][0][-1]:.4f} decode {results[name][1][-1]:.4f} ms",
+                  file=sys.stderr, flush=True)  # progress (a long sweep must not look hung)
     inb = k * nbytes * stripes
     print(f"k={k} m={m} bytes={nbytes} stripes={stripes} path enc={lh.batch_path(k, m, nbytes)} "
           f"dec={lh.batch_path(k, m, nbytes, True)}")
