@@ -88,16 +88,25 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     cfg->nch = nch2;
     cfg->spw = spw;
     cfg->wps = wps;
-    // Aligned column loads (jit_codec.hip LH_AL): 8-byte lanes over whole stripes whose
-    // sub-blocks start off an 8-byte boundary, when the last lane's valid bytes come from its
-    // own aligned word for every sub-block (LONGHAIR_AMD_JIT_AL=0 turns it off).
+    // 8-byte lanes over whole stripes whose sub-blocks start off an 8-byte boundary (sub % 8
+    // != 0), when the last chunk's valid bytes plus any sub-block's offset fit one word
+    // (jit_codec.hip LH_VLAST + S_b <= 8: sub % 8 in {1, 2, 4}, e.g. 1296-byte blocks):
+    //  al = 2 (default): the outputs are stored as aligned words (LH_ALS; LONGHAIR_AMD_JIT_ALS=0
+    //         keeps the 2-byte-aligned stores);
+    //  al = 1 (LONGHAIR_AMD_JIT_AL=1): aligned column loads realigned across lanes by DPP
+    //         (LH_AL) -- slower: the realignment costs more than the misaligned loads
+    //         (profiles/r4c_ubench_floor_enc.txt: k29/m4 access pattern 0.554 vs 0.530 ms).
     cfg->al = 0;
     if (W == 8 && nch2 <= 64 && sub % 8 != 0) {
         const int vlast = sub - 8 * (nch2 - 1);
         int smax = 0;
         for (int b = 0; b < 8; ++b) smax = std::max(smax, (b * sub) % 8);
-        const char *al = std::getenv("LONGHAIR_AMD_JIT_AL");
-        cfg->al = (vlast + smax <= 8 && !(al && std::string(al) == "0")) ? 1 : 0;
+        if (vlast + smax <= 8) {
+            const char *al = std::getenv("LONGHAIR_AMD_JIT_AL");
+            const char *als = std::getenv("LONGHAIR_AMD_JIT_ALS");
+            if (al && std::string(al) == "1") cfg->al = 1;
+            else if (!(als && std::string(als) == "0")) cfg->al = 2;
+        }
     }
     cfg->defines.clear();
     if (const char *d = std::getenv("LONGHAIR_AMD_JIT_DEFINES")) cfg->defines = d;
@@ -511,7 +520,8 @@ std::string jit_source_for(const JitConfig &c) {
     os << "#define LH_K " << c.k << "\n#define LH_M " << c.m << "\n#define LH_BYTES " << c.bytes
        << "\n#define LH_SUB " << c.sub << "\n#define LH_W " << c.W << "\n#define LH_NCH " << c.nch
        << "\n#define LH_SPW " << (c.spw ? c.spw : 1) << "\n#define LH_WPS " << (c.wps ? c.wps : 1) << "\n";
-    if (c.al) os << "#define LH_AL 1\n";
+    if (c.al == 1) os << "#define LH_AL 1\n";
+    if (c.al == 2) os << "#define LH_ALS 1\n";
     const std::vector<uint8_t> g = generator_matrix(c.k, c.m);
     os << "static constexpr unsigned char LH_BM[" << c.m << "][" << c.k << "][8] = {";
     for (int r = 0; r < c.m; ++r) {
@@ -589,9 +599,14 @@ static std::string cache_path(const std::string &src) {
     for (const char *o : kOpts) key += std::string("\n") + o;
     // (HIP_VERSION is the build's headers; hipRuntimeGetVersion would need a device, and
     // the cache is filled on a machine without one.)
-    int major = 0, minor = 0;
-    (void)hiprtcVersion(&major, &minor);
-    key += "\nhiprtc " + std::to_string(major) + "." + std::to_string(minor) + " hip " + std::to_string(HIP_VERSION);
+    // hiprtcVersion once per process: hiprtc serialises its API calls, so asking while a
+    // background compilation runs would wait for it (a cached-module lookup blocked ~1.4 s).
+    static const std::string ver = [] {
+        int major = 0, minor = 0;
+        (void)hiprtcVersion(&major, &minor);
+        return std::to_string(major) + "." + std::to_string(minor);
+    }();
+    key += "\nhiprtc " + ver + " hip " + std::to_string(HIP_VERSION);
     char name[64];
     snprintf(name, sizeof(name), "/lh_%016llx.co", (unsigned long long)fnv1a(key));
     const std::string d = cache_dir();

@@ -27,7 +27,7 @@ struct JitConfig {
     int win_lds = 1;      // windowed modules: stage column tiles in LDS by LDS-DMA (0: per-wave loads)
     int win_split = 1;    // windowed decode: phase A writes V in place, lh_inverse_gt_kernel does phase B
                           // (0: the fused kernel, phase B from an LDS tile of V)
-    int al = 0;           // register networks: aligned column loads realigned across lanes (LH_AL)
+    int al = 0;           // register networks: 2 aligned output stores (LH_ALS), 1 aligned column loads (LH_AL)
     int lanes_per_launch_unit() const { return 64; }
 };
 

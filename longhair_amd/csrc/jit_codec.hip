@@ -225,17 +225,26 @@ __device__ __forceinline__ void lh_column(lh_word (&acc)[LH_M][8], const lh_word
 #ifndef LH_AL
 #define LH_AL 0
 #endif
-#if LH_AL
-#if LH_W != 8 || LH_NCH > 64
-#error "LH_AL needs 8-byte lanes and whole stripes per wave"
+// LH_ALS = 1 (host-chosen with LH_AL = 0, jit.cpp; a knob): the outputs are stored as
+// 8-byte-aligned words.  Lanes own p = 8c, the last lane of a stripe p = sub - 8 (its chunk
+// overlaps the previous one).  In store instruction y, lane c stores the aligned word at
+// y * sub - S_y + 8c of the block (S_y = (y * sub) % 8): bytes 8 - S_y .. 7 of lane c - 1's
+// chunk, then bytes 0 .. 7 - S_y of its own, gathered with ds_bpermute; lane 0 takes the
+// previous sub-block's last S_y bytes from its stripe's last lane, which shares its chunk of
+// that sub-block (exactly its last 8 bytes).  The last lane stores its own chunk when it is
+// the aligned word (S_y = 8 - LH_VLAST) and otherwise nothing: the next instruction's lane 0
+// covers that word (an out-of-range buffer offset drops the store).  Every aligned word of
+// the block is stored once when LH_VLAST + max S_y <= 8, which the host checks.
+// profiles/r4c_ubench_floor_enc.txt: the k29/m4 access pattern with aligned stores 0.519 vs
+// 0.554 ms with the same loads and 2-byte-aligned stores.
+#ifndef LH_ALS
+#define LH_ALS 0
 #endif
-#define LH_VLAST (LH_SUB - 8 * (LH_NCH - 1))  // valid bytes of the last lane of a stripe
-__device__ __forceinline__ unsigned int lh_dpp_next(unsigned int v) {  // lane i <- lane i + 1
-    return (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
-}
-__device__ __forceinline__ unsigned int lh_dpp_prev(unsigned int v) {  // lane i <- lane i - 1
-    return (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
-}
+#if LH_AL || LH_ALS
+#if LH_W != 8 || LH_NCH > 64
+#error "LH_AL / LH_ALS need 8-byte lanes and whole stripes per wave"
+#endif
+#define LH_VLAST (LH_SUB - 8 * (LH_NCH - 1))  // valid bytes of the last chunk of a stripe
 // Bytes [S, S + 8) of the 16 bytes d[0..3] (little endian), S a compile-time constant.
 template <int S>
 __device__ __forceinline__ lh_word lh_funnel(unsigned int d0, unsigned int d1, unsigned int d2, unsigned int d3) {
@@ -250,6 +259,17 @@ __device__ __forceinline__ lh_word lh_funnel(unsigned int d0, unsigned int d1, u
         w.v[1] = __builtin_amdgcn_alignbyte(d[a + 2], d[a + 1], r);
     }
     return w;
+}
+#endif
+#if LH_AL && LH_ALS
+#error "LH_ALS assumes the 2-byte-aligned load mapping (LH_AL = 0)"
+#endif
+#if LH_AL
+__device__ __forceinline__ unsigned int lh_dpp_next(unsigned int v) {  // lane i <- lane i + 1
+    return (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
+}
+__device__ __forceinline__ unsigned int lh_dpp_prev(unsigned int v) {  // lane i <- lane i - 1
+    return (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
 }
 // Sub-block B's word loaded from its aligned floor -> the lane's bytes [p, p + 8).
 template <int B>
@@ -275,42 +295,35 @@ __device__ __forceinline__ lh_word lh_store_word(const lh_word &w, bool last) {
     return o;
 }
 #endif
-
-// LH_ALS = 1 (with LH_AL; a tuning knob): the outputs are stored as 8-byte-aligned words too.
-// In store instruction y, lane c stores the aligned word at y * sub - S_y + 8c of the block
-// (S_y = (y * sub) % 8): bytes 8 - S_y.. of the previous lane's chunk then its own, gathered
-// with ds_bpermute; lane 0 takes the previous sub-block's last bytes from its stripe's last
-// lane, which shares the 8 bytes ending at that sub-block's end instead of its own chunk.
-// The last lane's word extends into the next sub-block unless S_y >= 8 - LH_VLAST: then
-// the next instruction's lane 0 stores it and this lane's store gets an out-of-range
-// buffer offset (dropped).  Stores go through a buffer resource over the wave's stripes.
-#ifndef LH_ALS
-#define LH_ALS 0
+#if LH_ALS
+#if !LH_BUF
+#error "LH_ALS stores through buffer resources"
 #endif
-#if LH_AL && LH_ALS
 template <int AUX>
 __device__ __forceinline__ void lh_store_buf(const lh_word &w, const __amdgpu_buffer_rsrc_t &rs, int off) {
     const lh_u32x2 v = {w.v[0], w.v[1]};
     __builtin_amdgcn_raw_buffer_store_b64(v, rs, off, 0, AUX);
 }
-// One block row (8 sub-row words, the lane's chunk of each sub-block) at byte offset `blk`
-// of the resource.  c: the lane's chunk; src: lane c - 1, or for c = 0 its stripe's last lane.
-template <int Y = 0>
+// One block (8 sub-row words: the lane's chunk of each sub-block) at byte offset `blk` of
+// the resource.  c: the lane's chunk; src: lane c - 1, or for c = 0 its stripe's last lane.
+template <int AUX, int Y = 0>
 __device__ __forceinline__ void lh_store_block_al(const __amdgpu_buffer_rsrc_t &rs, int blk, int c, int src,
-                                                  const lh_word (&w)[8], lh_word lprev) {
+                                                  const lh_word (&w)[8]) {
     if constexpr (Y < 8) {
         constexpr int S = (Y * LH_SUB) % 8;
         const bool last = c == LH_NCH - 1;
         lh_word word = w[Y];
         if constexpr (S != 0) {
-            const unsigned int s0 = last ? lprev.v[0] : w[Y].v[0], s1 = last ? lprev.v[1] : w[Y].v[1];
-            const unsigned int p0 = (unsigned int)__builtin_amdgcn_ds_bpermute(src * 4, (int)s0);
-            const unsigned int p1 = (unsigned int)__builtin_amdgcn_ds_bpermute(src * 4, (int)s1);
-            word = lh_funnel<8 - S>(p0, p1, w[Y].v[0], w[Y].v[1]);
+            const lh_word &sh = last ? w[Y - 1] : w[Y];
+            const unsigned int p0 = (unsigned int)__builtin_amdgcn_ds_bpermute(src * 4, (int)sh.v[0]);
+            const unsigned int p1 = (unsigned int)__builtin_amdgcn_ds_bpermute(src * 4, (int)sh.v[1]);
+            const lh_word f = lh_funnel<8 - S>(p0, p1, w[Y].v[0], w[Y].v[1]);
+            word.v[0] = last ? w[Y].v[0] : f.v[0];
+            word.v[1] = last ? w[Y].v[1] : f.v[1];
         }
-        const bool skip = last && S < 8 - LH_VLAST;
-        lh_store_buf<LH_NT_ST ? 2 : 0>(word, rs, skip ? (int)0x80000000 : blk + Y * LH_SUB - S + 8 * c);
-        if constexpr (Y < 7) lh_store_block_al<Y + 1>(rs, blk, c, src, w, lh_store_word(w[Y], true));
+        const bool skip = last && S != 8 - LH_VLAST;
+        lh_store_buf<AUX>(word, rs, skip ? (int)0x80000000 : blk + Y * LH_SUB - S + 8 * c);
+        lh_store_block_al<AUX, Y + 1>(rs, blk, c, src, w);
     }
 }
 #endif
@@ -540,7 +553,7 @@ __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned ch
     for (int q = 0; q < LH_PF; ++q)
         if (q < LH_K) S.load8(ring[q], q);
     lh_unroll_encode<0>::run(acc, ring, S);
-#if LH_AL && LH_ALS
+#if LH_ALS
     {
         const long long s0o = (long long)__builtin_amdgcn_readfirstlane((int)wave) * LH_SPW;
         const long long nso = (stripes - s0o) < LH_SPW ? (stripes - s0o) : LH_SPW;
@@ -551,7 +564,7 @@ __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned ch
             const int src = c == 0 ? lane + LH_NCH - 1 : lane - 1;
             const int so = (int)((l.stripe - s0o) * out_stride);
 #pragma unroll
-            for (int r = 0; r < LH_M; ++r) lh_store_block_al(ro, so + r * LH_BYTES, c, src, acc[r], acc[r][0]);
+            for (int r = 0; r < LH_M; ++r) lh_store_block_al<LH_NT_ST ? 2 : 0>(ro, so + r * LH_BYTES, c, src, acc[r]);
             return;
         }
     }
@@ -793,9 +806,12 @@ __device__ __forceinline__ void lh_dec_phase_a(lh_word (&v)[LH_M][8], lh_word (&
 #ifndef LH_PB_PROBE
 #define LH_PB_PROBE 0  // timing probe only (tools/tune.py): V_i stored as output i, no phase-B XORs
 #endif
+struct lh_dsrc;
 __device__ __forceinline__ void lh_dec_phase_b(const lh_word (&v)[LH_M][8], const lh_plan_regs &pr,
-                                               unsigned char *base, bool last) {
+                                               unsigned char *base, bool last, const lh_dsrc &S, int soff) {
     (void)last;
+    (void)S;
+    (void)soff;
     const int e = pr.e;
 #if LH_PB_PROBE
 #pragma unroll
@@ -842,6 +858,13 @@ __device__ __forceinline__ void lh_dec_phase_b(const lh_word (&v)[LH_M][8], cons
                 lh_pin8(o);
 #endif
             }
+#if LH_ALS
+            {  // in place through the wave's buffer resource (S.rs), aligned words
+                const int lane = threadIdx.x & 63, c = lane % LH_NCH;
+                lh_store_block_al<LH_NT_ST ? 2 : 0>(S.rs, soff + (int)LH_BYTE(outw, i) * LH_BYTES, c,
+                                                    c == 0 ? lane + LH_NCH - 1 : lane - 1, o);
+            }
+#else
             unsigned char *dst = base + (long long)LH_BYTE(outw, i) * LH_BYTES;
 #pragma unroll
             for (int y = 0; y < 8; ++y)
@@ -849,6 +872,7 @@ __device__ __forceinline__ void lh_dec_phase_b(const lh_word (&v)[LH_M][8], cons
                 lh_store(dst + y * LH_SUB, lh_store_word(o[y], last));
 #else
                 lh_store(dst + y * LH_SUB, o[y]);
+#endif
 #endif
         }
     }
@@ -896,7 +920,11 @@ __device__ __forceinline__ void lh_decode_body(const lh_lane &l, long long wave,
 #endif
         lh_dec_phase_a<PF>(v, ring, pr, S);
     }
-    lh_dec_phase_b(v, pr, blocks + l.stripe * stripe_stride + l.ps, l.last);
+#if LH_BUF
+    lh_dec_phase_b(v, pr, blocks + l.stripe * stripe_stride + l.ps, l.last, S, S.lbase - l.p);
+#else
+    lh_dec_phase_b(v, pr, blocks + l.stripe * stripe_stride + l.ps, l.last, S, 0);
+#endif
 }
 
 __device__ __forceinline__ void lh_decode_wave(long long wave, unsigned char *__restrict__ blocks,
