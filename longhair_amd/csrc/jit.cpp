@@ -91,11 +91,11 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     // 8-byte lanes over whole stripes whose sub-blocks start off an 8-byte boundary (sub % 8
     // != 0), when the last chunk's valid bytes plus any sub-block's offset fit one word
     // (jit_codec.hip LH_VLAST + S_b <= 8: sub % 8 in {1, 2, 4}, e.g. 1296-byte blocks):
-    //  al = 2 (default): the outputs are stored as aligned words (LH_ALS; LONGHAIR_AMD_JIT_ALS=0
-    //         keeps the 2-byte-aligned stores);
-    //  al = 1 (LONGHAIR_AMD_JIT_AL=1): aligned column loads realigned across lanes by DPP
-    //         (LH_AL) -- slower: the realignment costs more than the misaligned loads
-    //         (profiles/r4c_ubench_floor_enc.txt: k29/m4 access pattern 0.554 vs 0.530 ms).
+    //  al = 2 (LONGHAIR_AMD_JIT_ALS=1): the outputs stored as aligned words (LH_ALS);
+    //  al = 1 (LONGHAIR_AMD_JIT_AL=1): aligned column loads realigned across lanes by DPP (LH_AL).
+    // Both off by default: measured slower on k29/m4 (profiles/r4d_tune_k29m4.txt: encode 0.591
+    // with aligned stores -- 132 VGPRs, 3 waves/SIMD -- against 0.563 ms; the aligned loads'
+    // access pattern 0.554 against 0.530 ms, profiles/r4c_ubench_floor_enc.txt).
     cfg->al = 0;
     if (W == 8 && nch2 <= 64 && sub % 8 != 0) {
         const int vlast = sub - 8 * (nch2 - 1);
@@ -105,7 +105,7 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
             const char *al = std::getenv("LONGHAIR_AMD_JIT_AL");
             const char *als = std::getenv("LONGHAIR_AMD_JIT_ALS");
             if (al && std::string(al) == "1") cfg->al = 1;
-            else if (!(als && std::string(als) == "0")) cfg->al = 2;
+            else if (als && std::string(als) == "1") cfg->al = 2;
         }
     }
     cfg->defines.clear();

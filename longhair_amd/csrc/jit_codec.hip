@@ -212,7 +212,7 @@ __device__ __forceinline__ void lh_column(lh_word (&acc)[LH_M][8], const lh_word
 #endif
 }
 
-// LH_AL = 1 (chosen by the host, jit.cpp: W = 8, whole stripes per wave, sub % 8 != 0):
+// LH_AL = 1 (a knob, jit.cpp: W = 8, whole stripes per wave, sub % 8 in {1, 2, 4}):
 // aligned column loads.  Sub-block b of a block starts (b * sub) % 8 = S_b bytes past an
 // 8-byte boundary, so a lane's 8 bytes [p, p + 8) of it straddle two aligned words: every
 // lane loads the aligned word at p - S_b and takes the bytes it lacks from the next lane's
@@ -220,12 +220,13 @@ __device__ __forceinline__ void lh_column(lh_word (&acc)[LH_M][8], const lh_word
 // constant per b).  Lanes own p = 8c; the last lane of a stripe (c = nch - 1) holds only
 // LH_VLAST valid bytes, which its own word supplies (the host checks LH_VLAST + S_b <= 8), and
 // stores [sub - 8, sub) assembled with the previous lane's word (DPP wave_shr:1).  The same
-// bytes as 2-byte-aligned 8-byte loads (LH_AL = 0), with 8-byte-aligned load addresses:
-// tools/ubench_floor.hip measures the two access patterns.
+// bytes as 2-byte-aligned 8-byte loads (LH_AL = 0), with 8-byte-aligned load addresses.
+// Off by default: the realignment costs more than the misaligned loads (the k29/m4 access
+// pattern 0.554 against 0.530 ms, tools/ubench_floor.hip, profiles/r4c_ubench_floor_enc.txt).
 #ifndef LH_AL
 #define LH_AL 0
 #endif
-// LH_ALS = 1 (host-chosen with LH_AL = 0, jit.cpp; a knob): the outputs are stored as
+// LH_ALS = 1 (with LH_AL = 0; jit.cpp, a knob): the outputs are stored as
 // 8-byte-aligned words.  Lanes own p = 8c, the last lane of a stripe p = sub - 8 (its chunk
 // overlaps the previous one).  In store instruction y, lane c stores the aligned word at
 // y * sub - S_y + 8c of the block (S_y = (y * sub) % 8): bytes 8 - S_y .. 7 of lane c - 1's
@@ -234,9 +235,9 @@ __device__ __forceinline__ void lh_column(lh_word (&acc)[LH_M][8], const lh_word
 // that sub-block (exactly its last 8 bytes).  The last lane stores its own chunk when it is
 // the aligned word (S_y = 8 - LH_VLAST) and otherwise nothing: the next instruction's lane 0
 // covers that word (an out-of-range buffer offset drops the store).  Every aligned word of
-// the block is stored once when LH_VLAST + max S_y <= 8, which the host checks.
-// profiles/r4c_ubench_floor_enc.txt: the k29/m4 access pattern with aligned stores 0.519 vs
-// 0.554 ms with the same loads and 2-byte-aligned stores.
+// the block is stored once when LH_VLAST + max S_y <= 8, which the host checks.  Off by
+// default (LONGHAIR_AMD_JIT_ALS=1): k29/m4 encode 0.591 against 0.563 ms, decode equal
+// (profiles/r4d_tune_k29m4.txt; the gathers cost the encode a wave per SIMD).
 #ifndef LH_ALS
 #define LH_ALS 0
 #endif
