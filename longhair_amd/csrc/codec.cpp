@@ -508,14 +508,14 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         // k128/m32 decode 3.94-3.98 ms whole, 4.17 at 1024 stripes, 6.7 at 128; k200/m56 0.60
         // whole, 0.69 at 32): the per-launch tails cost more than the V traffic saved.
         long long chunk = stripes;
-        if (wk->cfg.win_split)
+        if (wk->cfg.win_split == 1)
             if (const char *c = std::getenv("LONGHAIR_AMD_WIDE_CHUNK")) chunk = std::atoll(c) > 0 ? std::atoll(c) : stripes;
         // LONGHAIR_AMD_WIDE_OVERLAP=1 (with chunks): phase B of chunk c runs on a side stream,
         // overlapping phase A of chunk c + 1 on the caller's stream (fork / join by events, so
         // the call stays stream-ordered and capturable).  Also measured slower than the whole
         // batch (k128/m32 4.08-4.27 ms).
         bool overlap = false;
-        if (wk->cfg.win_split && chunk < stripes) {
+        if (wk->cfg.win_split == 1 && chunk < stripes) {
             const char *o = std::getenv("LONGHAIR_AMD_WIDE_OVERLAP");
             overlap = o && std::atoi(o) != 0;
         }
@@ -542,8 +542,8 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
             void *args[] = {(void *)&cb, &s1, (void *)&plan, &s2, (void *)&zero, &nn};
             LH_HIP(hipModuleLaunchKernel(wk->decode_wide, (unsigned)(n * cps), 1, 1, threads, 1, 1, 0, st, args,
                                          nullptr));
-            note_launch(wk->cfg.win_split ? "lh_jit_decode_wide" : "lh_jit_decode_wide(fused phase B)");
-            if (wk->cfg.win_split) {  // phase A left V_r in the recovery slots: phase B
+            note_launch(wk->cfg.win_split == 1 ? "lh_jit_decode_wide" : "lh_jit_decode_wide(fused phase B)");
+            if (wk->cfg.win_split == 1) {  // phase A left V_r in the recovery slots: phase B
                 InverseArgs ia{};
                 ia.blocks = cb;
                 ia.stride = stride;

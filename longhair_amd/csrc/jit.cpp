@@ -134,7 +134,12 @@ bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
     // k200/m56 0.87 -> 0.79), for the fused decode too (its V rows stay in the registers of
     // the wave that computed them).
     cfg->win_split = decode ? 1 : 0;
-    if (const char *sp = std::getenv("LONGHAIR_AMD_WIN_SPLIT")) cfg->win_split = decode && std::atoi(sp) ? 1 : 0;
+    // LONGHAIR_AMD_WIN_SPLIT: 1 split (default), 0 fused with the in-asm jump table, 2 fused
+    // with the table once per code object (as lh_inverse_gt_kernel)
+    if (const char *sp = std::getenv("LONGHAIR_AMD_WIN_SPLIT")) {
+        const int v = std::atoi(sp);
+        cfg->win_split = decode ? (v == 1 ? 1 : v == 2 ? 2 : 0) : 0;
+    }
     // At most 16 rows per wave, spread evenly over the ceil(m / 16) waves: the waves meet
     // at a barrier every column, so the fullest one sets the pace (k200/m56: 14-row groups
     // instead of 16 + 16 + 16 + 8, encode 0.414 -> 0.396 ms, decode 0.810 -> 0.788 ms).
@@ -188,12 +193,14 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
     const int NG = (m + R - 1) / R, D = PF + 1;
     const int ndma = (NG == 1 || priv) ? 2 : (g < 2 ? 1 : 0);  // DMA instructions per column, this wave
     const std::string toff = priv ? " + " + std::to_string(g * 2048) : "";  // this wave's ring slot
-    const bool split = elim && c.win_split;  // V_r goes back in place of R_r (lh_inverse_kernel follows)
+    const bool split = elim && c.win_split == 1;  // V_r goes back in place of R_r (lh_inverse_gt_kernel follows)
+    const bool fgt = elim && c.win_split == 2;     // fused, multiply through the per-code-object table
     os << "__device__ __forceinline__ void lh_wg" << g << "(" << (elim ? "" : "const ") << "unsigned char *__restrict__ base, "
        << (elim ? "const unsigned char *__restrict__ zero, const unsigned int (&slv)[LH_NQ], unsigned int *__restrict__ lv, "
                   "const unsigned char *__restrict__ pl"
                 : "unsigned char *__restrict__ o")
        << (lds ? ", const unsigned char *__restrict__ sb, const unsigned char *__restrict__ zb" : "")
+       << (fgt ? ", const unsigned glo, const unsigned ghi" : "")
        << ") {\n";
     {  // (Starting the accumulators at R_r, loaded before the column loop, measured equal:
        // k128/m32 decode 4.12 / 4.11 ms, k200/m56 0.83 / 0.81 ms.)
@@ -322,6 +329,10 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
            << "        }\n    }\n"
            << "    unsigned acc[8][8];\n"
            << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n#pragma unroll\n      for (int y = 0; y < 8; ++y) acc[i][y] = 0;\n";
+        if (fgt)  // lane r: the body address of output ob + i for row r (coefficient 0 past e: body 0)
+            os << "    unsigned tg[8];\n"
+               << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n"
+               << "      tg[i] = glo + (((i < 4 ? cpk0 : cpk1) >> (8 * (i & 3))) & 0xFFu) * 68u;\n";
         for (int r = r0; r < r1; ++r) {
             const std::string a = "a" + std::to_string(r - r0) + "_";
             // the pin orders this row's table build after the previous row's multiply (both
@@ -336,8 +347,11 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
                 os << "      tl[" << q << "] = " << (pre ? "tl[" + std::to_string(pre) + "] ^ " : "") << a << low << ";\n"
                    << "      th[" << q << "] = " << (pre ? "th[" + std::to_string(pre) + "] ^ " : "") << a << 4 + low << ";\n";
             }
-            os << "      lh_mul8((unsigned)__builtin_amdgcn_readlane((int)cpk0, " << r << "), "
-               << "(unsigned)__builtin_amdgcn_readlane((int)cpk1, " << r << "), acc, tl, th);\n    }\n";
+            if (fgt)
+                os << "      lh_mul8g<" << r << ">(acc, tl, th, tg, ghi);\n    }\n";
+            else
+                os << "      lh_mul8((unsigned)__builtin_amdgcn_readlane((int)cpk0, " << r << "), "
+                   << "(unsigned)__builtin_amdgcn_readlane((int)cpk1, " << r << "), acc, tl, th);\n    }\n";
         }
         os << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n"
            << "      if (ob + i < e)\n"
@@ -375,7 +389,7 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
        << "    const unsigned char *base, const unsigned char *zero) {\n"
        << "  const unsigned int s = (unsigned int)__builtin_amdgcn_readlane((int)slv[i / 64], i % 64);\n"
        << "  return s == 0xFFu ? zero : base + (long long)s * " << c.bytes << ";\n}\n";
-    if (!c.win_split) {
+    if (c.win_split != 1) {
         // The computed-jump multiply (inv_jump.inc, the in-asm table reached by GPR indexing,
         // the 8 accumulators of each output pinned to v[40 + 8i ..]).
         os << lh_inv_jump_source;
@@ -385,12 +399,24 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
            << "               LH_INV_JUMPI_INS(tl, th) : \"s88\", \"s89\", \"s90\", \"s91\", \"s92\", \"s93\", \"s94\",\n"
            << "               \"s95\", \"s96\", \"s97\", \"scc\");\n}\n";
     }
+    if (c.win_split == 2) {
+        // The 256 bodies once in this code object (never-launched holder kernel, hidden symbol
+        // lh_inv_gtab), entered per output by v_readlane + s_set_gpr_idx_idx + s_swappc
+        // (kernels.hip lh_inverse_gt_kernel; tables pinned to v8..v38, accumulators v40..v103).
+        // (the row is a literal lane select here: an inline constant of v_readlane)
+        os << "__global__ void lh_inv_gtab_holder() { asm volatile(LH_INV_GTAB_TEXT); }\n"
+           << "template <int R>\n"
+           << "__device__ __forceinline__ void lh_mul8g(unsigned (&acc)[8][8], const unsigned (&tl)[16],\n"
+           << "    const unsigned (&th)[16], const unsigned (&t)[8], unsigned hi) {\n"
+           << "  asm volatile(LH_INV_JUMPG8_ASM : LH_INV_JUMPG8_OUTS(acc) : LH_INV_JUMPG_INS(tl, th, t), [r] \"n\"(R),\n"
+           << "               [hi] \"s\"(hi) : \"s92\", \"s93\", \"s94\", \"s95\", \"s97\", \"scc\");\n}\n";
+    }
     for (int g = 0; g < NG; ++g) emit_win_group(os, c, G, g);
     os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
        << "lh_jit_decode_wide(unsigned char *__restrict__ blocks, long long stride,\n"
        << "                   const unsigned char *__restrict__ plan, long long plan_stride,\n"
        << "                   const unsigned char *__restrict__ zero_page, int stripes) {\n";
-    if (!c.win_split) os << "  __shared__ unsigned int lv[8 * 8 * 64];  // phase B: 8 outputs x 8 sub-rows x 64 lanes\n";
+    if (c.win_split != 1) os << "  __shared__ unsigned int lv[8 * 8 * 64];  // phase B: 8 outputs x 8 sub-rows x 64 lanes\n";
     os << "  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
        << "  const int lane = threadIdx.x & 63;\n"
        << "  const long long stripe = blockIdx.x / " << CPS << ";\n"
@@ -405,15 +431,28 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
        << "  const int chunk = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << ";\n"
        << "  unsigned char *b = blocks + stripe * stride + chunk + lane * " << c.W << ";\n"
        << "  const unsigned char *z = zero_page + chunk + lane * " << c.W << ";\n";
-    if (!c.win_split)
+    if (c.win_split != 1)
         os << "  for (int i = threadIdx.x; i < 8 * 8 * 64; i += blockDim.x) lv[i] = 0u;\n"
            << "  __syncthreads();\n";
-    const std::string lvarg = c.win_split ? "nullptr" : "lv";
-    std::string dargs = "(b, z, slv, " + lvarg + ", pl)";
+    std::string gargs;
+    if (c.win_split == 2) {
+        // the table's address (PC-relative); a table straddling a 4 GiB boundary cannot be
+        // reached with one high word: then the in-asm table (LONGHAIR_AMD_WIN_SPLIT=0) is the way
+        os << "  unsigned glo, ghi;\n"
+           << "  asm volatile(\"s_getpc_b64 s[92:93]\\n\"\n"
+           << "               \"s_add_u32 s92, s92, lh_inv_gtab@rel32@lo+4\\n\"\n"
+           << "               \"s_addc_u32 s93, s93, lh_inv_gtab@rel32@hi+12\\n\"\n"
+           << "               \"s_mov_b32 %0, s92\\n\"\n"
+           << "               \"s_mov_b32 %1, s93\\n\" : \"=s\"(glo), \"=s\"(ghi) : : \"s92\", \"s93\", \"scc\");\n"
+           << "  if (glo > 0xFFFFFFFFu - 256u * 68u) __builtin_trap();\n";
+        gargs = ", glo, ghi";
+    }
+    const std::string lvarg = c.win_split == 1 ? "nullptr" : "lv";
+    std::string dargs = "(b, z, slv, " + lvarg + ", pl" + gargs + ")";
     if (c.win_lds) {
         os << "  const unsigned char *sb = blocks + stripe * stride + chunk;\n"
            << "  const unsigned char *zb = zero_page + chunk;\n";
-        dargs = "(b, z, slv, " + lvarg + ", pl, sb, zb)";
+        dargs = "(b, z, slv, " + lvarg + ", pl, sb, zb" + gargs + ")";
     }
     for (int g = 0; g < NG; ++g) os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << dargs << ";\n";
     os << "}\n";

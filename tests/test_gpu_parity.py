@@ -292,18 +292,22 @@ def test_decode_batch_vs_oracle(lh, oracle, path, k, m, nbytes, stripes, e):
     _decode_batch_vs_oracle(lh, oracle, k, m, nbytes, stripes, e)
 
 
+@pytest.mark.parametrize("split", ["0", "2"])
 @pytest.mark.parametrize("k,m,nbytes,stripes", [(40, 20, 4096, 8), (100, 16, 2048, 6), (128, 32, 8192, 4),
                                                 (200, 56, 65536, 3), (250, 6, 2048, 8)])
-def test_wide_decode_fused_variant(lh, oracle, monkeypatch, k, m, nbytes, stripes):
+def test_wide_decode_fused_variant(lh, oracle, monkeypatch, split, k, m, nbytes, stripes):
     """Large-m decode with the fused phase A + B kernel (LONGHAIR_AMD_WIN_SPLIT=0: V in the
     registers of the wave that computed it, each wave's share of 8 outputs at a time reduced
-    in an LDS tile): the launch trace shows that kernel ran and no separate phase B; random e
-    up to e_max (several 8-output batches at m = 32 and 56).  (The phase-B kernel of the split
-    form is tested in test_gpu_boundaries.py.)"""
-    monkeypatch.setenv("LONGHAIR_AMD_WIN_SPLIT", "0")
+    in an LDS tile; =2: the same with the multiply through the per-code-object jump table): the
+    launch trace shows that kernel ran and no separate phase B; random e up to e_max (several
+    8-output batches at m = 32 and 56).  (The phase-B kernel of the split form is tested in
+    test_gpu_boundaries.py.)"""
+    monkeypatch.setenv("LONGHAIR_AMD_WIN_SPLIT", split)
     assert lh.batch_path(k, m, nbytes, True) == "jit-wide"
     _decode_batch_vs_oracle(lh, oracle, k, m, nbytes, stripes, None)
-    assert lh.last_launch() == ["lh_plan_kernel(closed form)", "lh_jit_decode_wide(fused phase B)"]
+    trace = lh.last_launch()
+    assert len(trace) == 2 and trace[0].startswith("lh_plan_")
+    assert trace[1] == "lh_jit_decode_wide(fused phase B)"
 
 
 def _decode_batch_vs_oracle(lh, oracle, k, m, nbytes, stripes, e):

@@ -17,7 +17,7 @@ TESTS = [(29, 2, 1296), (29, 3, 1296), (29, 8, 1296), (4, 2, 16), (10, 6, 8), (1
          (3, 250, 24), (2, 2, 8), (29, 4, 1304), (9, 7, 72), (29, 2, 16), (10, 8, 24),
          (128, 32, 1024), (5, 3, 8), (100, 16, 2048), (40, 20, 4096), (250, 6, 2048), (10, 6, 24), (3, 2, 8),
          (64, 4, 4096), (64, 3, 4096), (64, 2, 8192)]
-# Shapes whose fused large-m decode (LONGHAIR_AMD_WIN_SPLIT=0) the GPU tests run.
+# Shapes whose fused large-m decode (LONGHAIR_AMD_WIN_SPLIT=0 and 2) the GPU tests run.
 VARIANT_SHAPES = [(40, 20, 4096), (100, 16, 2048), (128, 32, 8192), (200, 56, 65536), (250, 6, 2048)]
 
 
@@ -61,7 +61,7 @@ def main():
             jobs_list = [(s, part) for s in slow[:2] for part in ("dec", "enc")]
             jobs_list += [(s, None) for s in slow[2:] + [s for s in DEFAULT + TESTS if s not in slow]]
             # non-default kernels the GPU tests also run (test_wide_decode_fused_variant)
-            jobs_list += [(s, ("dec", {"LONGHAIR_AMD_WIN_SPLIT": "0"})) for s in VARIANT_SHAPES]
+            jobs_list += [(s, ("dec", {"LONGHAIR_AMD_WIN_SPLIT": v})) for v in ("0", "2") for s in VARIANT_SHAPES]
             # kernel-selection boundaries and the reference-main sweep (test_gpu_boundaries.py)
             bj, tb = boundary_jobs()
             have = {s for s, _ in jobs_list}
