@@ -80,6 +80,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="wall-time budget of the CPU baseline leg")
     ap.add_argument("--dropin-calls", type=int, default=-1,
                     help="per-call drop-in latency leg (host pointers, one stripe per call); 0 = off")
+    ap.add_argument("--ptr", default="on", choices=["on", "off"],
+                    help="also time the step through the pointer-table batch calls (after the timed region)")
     ap.add_argument("--pcie", default="on", choices=["on", "off"],
                     help="PCIe-inclusive leg: cauchy_256_*_host_batch from pinned host memory on every rank")
     ap.add_argument("--pcie-stripes", type=int, default=0,
@@ -513,6 +515,49 @@ def pcie_timed(lh, k, m, nbytes, xn, bn, rn, recn, b0, r0, world, rank, reps=3, 
                     f"{reps} (decode: the workload's erasure patterns, recovered blocks written back)"}
 
 
+def ptr_leg(lh, k, m, nbytes, X, D, rows0, rec_view, reps=5):
+    """The same step through the pointer-table calls (cauchy_256_*_batch_ptrs): tables that
+    point at the very blocks the strided step uses, so the bytes moved are the same and only
+    the addressing differs.  HIP-event times on the launch stream, mean of `reps`; the decoded
+    data is checked against X afterwards."""
+    import torch
+    stripes = X.shape[0]
+    s_idx = torch.arange(stripes, device="cuda", dtype=torch.int64).unsqueeze(1)
+
+    def table(t, n):
+        return (t.data_ptr() + s_idx * t.stride(0) + torch.arange(n, device="cuda", dtype=torch.int64) * t.stride(1)
+                ).contiguous()
+    dptr, rptr, bptr = table(X, k), table(rec_view, m), table(D, k)
+    rows = rows0.clone()
+    stream = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    enc = dec = 0.0
+    traces = {}
+    for i in range(reps + 1):
+        ev[0].record(stream)
+        lh.encode_batch_ptrs(k, m, nbytes, dptr, rptr, stream=stream)
+        ev[1].record(stream)
+        traces.setdefault("encode", lh.last_launch())
+        rows.copy_(rows0)
+        ev[2].record(stream)
+        lh.decode_batch_ptrs(k, m, nbytes, bptr, rows, stream=stream)
+        ev[3].record(stream)
+        traces.setdefault("decode", lh.last_launch())
+        torch.cuda.synchronize()
+        if i:  # the first pass warms up
+            enc += ev[0].elapsed_time(ev[1]) / reps
+            dec += ev[2].elapsed_time(ev[3]) / reps
+    order = rows.long().argsort(dim=1)
+    ok = bool(torch.equal(torch.gather(D, 1, order.unsqueeze(-1).expand(-1, -1, nbytes)), X))
+    return {"encode_ms": round(enc, 4), "decode_ms": round(dec, 4),
+            "encode_GBps": round(k * nbytes * stripes / (enc * 1e-3) / 1e9, 1),
+            "decode_GBps": round(k * nbytes * stripes / (dec * 1e-3) / 1e9, 1),
+            "encode_kernels": traces["encode"], "decode_kernels": traces["decode"], "ok": ok,
+            "what": "the step through cauchy_256_{encode,decode}_batch_ptrs: per-block device pointer tables "
+                    "(the reference's data_ptrs[] / Block.data per stripe) over the same buffers, "
+                    f"HIP events, mean of {reps}"}
+
+
 def load_profile(name):
     path = os.path.join(REPO, "profiles", name)
     return json.load(open(path)) if os.path.exists(path) else None
@@ -693,6 +738,8 @@ def main():
                     "frac_of_measured_floor": round(FLAT_FLOOR_MS / enc_ms, 4),
                     "floor_frac_of_hbm_peak": round(k * nbytes * stripes / (FLAT_FLOOR_MS * 1e-3) / 1e9
                                                     / HBM_PEAK_GBS, 4)})
+    if not dry and args.ptr == "on" and rec_index is None:
+        out["ptr_tables"] = ptr_leg(lh, k, m, nbytes, X, D, rows0, rec_view)
     if not dry and args.pcie == "on":
         # every rank at once: the node's host links and memory are shared
         out["pcie"] = pcie_leg(lh, args, k, m, nbytes, X, D, rows0, rec_view, rec_index, world, rank)

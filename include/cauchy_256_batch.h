@@ -40,6 +40,22 @@ int cauchy_256_decode_batch(int k, int m, int block_bytes, int stripes,
                             void *d_blocks, long long stripe_stride,
                             unsigned char *d_rows, signed char *d_status, void *stream);
 
+/* Scattered blocks: the reference's per-block pointers (data_ptrs[], cauchy_256.h:78;
+ * Block.data, cauchy_256.h:103) for a batch of stripes, e.g. packets left where a NIC put
+ * them.  The pointer tables are device arrays of device pointers, one row per stripe:
+ *   encode: d_data_ptrs[s * k + x] = data block x of stripe s,
+ *           d_recovery_ptrs[s * m + r] = recovery block r of stripe s;
+ *   decode: d_block_ptrs[s * k + i] = decode slot i of stripe s (Block.data), its row
+ *           d_rows[s * k + i] (Block.row), rewritten as by cauchy_256_decode_batch.
+ * Blocks may sit at any address (the register-network shapes read and write them in place;
+ * others go through a workspace chunk).  Same results, return codes and asynchronous
+ * semantics as cauchy_256_encode_batch / cauchy_256_decode_batch. */
+int cauchy_256_encode_batch_ptrs(int k, int m, int block_bytes, int stripes,
+                                 const void *const *d_data_ptrs, void *const *d_recovery_ptrs, void *stream);
+int cauchy_256_decode_batch_ptrs(int k, int m, int block_bytes, int stripes,
+                                 void *const *d_block_ptrs, unsigned char *d_rows, signed char *d_status,
+                                 void *stream);
+
 /* Host-memory batches: the same operations on stripes that live
  * in host memory, pipelined in chunks of `chunk_stripes` (0 = about 64 MiB for encode,
  * up to 256 MiB with at least 4 chunks for decode, the last chunks halving in size) over

@@ -119,6 +119,46 @@ def decode_batch(blocks, rows, m, status=None, stream=None):
     return status
 
 
+def _ptr_table(t, stripes, n):
+    import torch
+    assert t.dtype == torch.int64 and t.is_cuda and t.is_contiguous() and tuple(t.shape) == (stripes, n)
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def encode_batch_ptrs(k, m, block_bytes, data_ptrs, recovery_ptrs, stream=None):
+    """Encode stripes whose blocks sit anywhere in device memory (cauchy_256_encode_batch_ptrs).
+
+    data_ptrs:     int64 CUDA tensor [stripes, k] of device addresses (the reference's data_ptrs[]
+                   per stripe, cauchy_256.h:78);
+    recovery_ptrs: int64 CUDA tensor [stripes, m], where recovery block r of each stripe goes."""
+    stripes = data_ptrs.shape[0]
+    rc = lib().cauchy_256_encode_batch_ptrs(k, m, block_bytes, stripes, _ptr_table(data_ptrs, stripes, k),
+                                            _ptr_table(recovery_ptrs, stripes, m),
+                                            ctypes.c_void_p(_stream_handle(stream)))
+    if rc != 0:
+        raise LonghairError(rc, "cauchy_256_encode_batch_ptrs")
+
+
+def decode_batch_ptrs(k, m, block_bytes, block_ptrs, rows, status=None, stream=None):
+    """Decode stripes whose k received blocks sit anywhere in device memory, in place
+    (cauchy_256_decode_batch_ptrs; the reference's Block[] per stripe, cauchy_256.h:103).
+
+    block_ptrs: int64 CUDA tensor [stripes, k] (Block.data of each slot);
+    rows:       uint8 CUDA tensor [stripes, k] (Block.row), rewritten in place.
+    Returns `status` (int8 [stripes], 0 ok / -1 invalid rows)."""
+    import torch
+    stripes = block_ptrs.shape[0]
+    assert rows.dtype == torch.uint8 and rows.is_contiguous() and tuple(rows.shape) == (stripes, k)
+    if status is None:
+        status = torch.empty((stripes,), dtype=torch.int8, device=rows.device)
+    rc = lib().cauchy_256_decode_batch_ptrs(k, m, block_bytes, stripes, _ptr_table(block_ptrs, stripes, k),
+                                            ctypes.c_void_p(rows.data_ptr()), ctypes.c_void_p(status.data_ptr()),
+                                            ctypes.c_void_p(_stream_handle(stream)))
+    if rc != 0:
+        raise LonghairError(rc, "cauchy_256_decode_batch_ptrs")
+    return status
+
+
 def encode_host_batch(data, m, recovery=None, chunk_stripes=0):
     """Encode stripes held in host memory (numpy uint8 [stripes, k, bytes], ideally pinned
     via a pinned torch CPU tensor's .numpy()); pipelined H2D / kernel / D2H."""

@@ -26,6 +26,11 @@ EXPORTS = {
     "cauchy_256_decode_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
                                                ctypes.c_void_p, ctypes.c_void_p]),
+    "cauchy_256_encode_batch_ptrs": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "cauchy_256_decode_batch_ptrs": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                    ctypes.c_void_p]),
     "cauchy_256_encode_host_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                     ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
                                                     ctypes.c_longlong, ctypes.c_int]),

@@ -121,6 +121,7 @@ struct HostPinned {
 // Per-stream scratch (decode plans and the generic path's output workspace).
 struct Workspace {
     DevBuf plan, work;
+    DevBuf gather;  // pointer-table batches without a pointer form: the contiguous chunk
     // Side stream + events of the chunked large-m decode (phase B of chunk c on `side`
     // while phase A of chunk c + 1 runs on the caller's stream); created on first use.
     hipStream_t side = nullptr;
@@ -601,6 +602,177 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
     return kOk;
 }
 
+// ------------------------------------------------------------ pointer-table batches
+// The reference's per-block pointers (cauchy_256.h:78 data_ptrs[], :103 Block *) for a batch
+// of stripes, with the pointer tables in device memory: row s of a table holds stripe s's
+// block pointers.  Shapes with a register network (jit.cpp jit_ptr_config_for: the k29/m4
+// family) read and write the blocks where they lie (jit_codec.hip LH_PTR: a wave's table rows
+// staged in LDS).  Every other shape gathers each chunk of stripes into the stream's
+// workspace (lh_ptr_copy_kernel), runs the strided batch path on it and scatters the outputs
+// back: one extra read and write of the inputs, bit-identical results.
+static constexpr long long kPtrChunkBytes = 256ll << 20;
+
+static int gather_chunk(Device *d, hipStream_t st, long long per_stripe, int stripes, uint8_t **buf, int *chunk) {
+    const long long c = std::max(1ll, std::min((long long)stripes, kPtrChunkBytes / std::max(1ll, per_stripe)));
+    std::lock_guard<std::mutex> g(d->mu);
+    Workspace &w = d->ws[st];
+    if ((size_t)(c * per_stripe) > w.gather.size && capturing(st))
+        return capture_growth_error("per-stream gather chunk");
+    LH_HIP(w.gather.reserve((size_t)(c * per_stripe), st));
+    *buf = w.gather.ptr;
+    *chunk = (int)c;
+    return kOk;
+}
+
+static int ptr_copy(uint8_t *const *ptrs, int n, int ncopy, uint8_t *chunk, long long stride, int bytes, int stripes,
+                    bool scatter, const uint8_t *sel, int sel_min, hipStream_t st) {
+    PtrCopyArgs a{};
+    a.ptrs = ptrs;
+    a.chunk = chunk;
+    a.stride = stride;
+    a.sel = sel;
+    a.sel_min = sel_min;
+    a.n = n;
+    a.ncopy = ncopy;
+    a.bytes = bytes;
+    a.stripes = stripes;
+    a.scatter = scatter ? 1 : 0;
+    LH_HIP(launch_ptr_copy(a, st));
+    return kOk;
+}
+
+static int encode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *const *data_ptrs, uint8_t *const *rec_ptrs,
+                             hipStream_t st) {
+    if (k < 1 || m < 1 || bytes <= 0 || stripes < 0 || k > 256 || m > 256)
+        return fail(kInvalid, "invalid k, m, block_bytes or stripes");
+    if (stripes == 0) return kOk;
+    if (!data_ptrs || !rec_ptrs) return fail(kInvalid, "null pointer table");
+    Device *d = nullptr;
+    if (int rc = current_device(&d)) return rc;
+    JitConfig cfg;
+    if (jit_ptr_config_for(k, m, bytes, false, &cfg)) {
+        std::string err;
+        bool hard = false;
+        const JitKernels *jk = jit_lookup(d, cfg, true, &err, &hard);
+        if (jk) {
+            const long long blocks = jit_blocks(cfg, stripes);
+            if (blocks > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
+            long long in_stride = (long long)k * 8, out_stride = (long long)m * 8;
+            int n = stripes;
+            void *args[] = {(void *)&data_ptrs, &in_stride, (void *)&rec_ptrs, &out_stride, &n};
+            LH_HIP(hipModuleLaunchKernel(jk->encode, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr));
+            note_launch("lh_jit_encode(pointer table)");
+            return kOk;
+        }
+        if (hard) return fail(kHipError, err);
+    }
+    // Gather / strided encode / scatter, per chunk.  An invalid shape (m > 1 with k + m > 256
+    // or bytes % 8 != 0) still gets recovery block 0 first, as the reference.
+    const bool invalid = m > 1 && k > 1 && (k + m > 256 || bytes % 8 != 0);
+    const long long per = (long long)(k + m) * bytes;
+    uint8_t *buf = nullptr;
+    int chunk = 0;
+    if (int rc = gather_chunk(d, st, per, stripes, &buf, &chunk)) return rc;
+    for (int s0 = 0; s0 < stripes; s0 += chunk) {
+        const int n = std::min(chunk, stripes - s0);
+        uint8_t *dat = buf, *rec = buf + (long long)n * k * bytes;
+        if (int rc = ptr_copy(data_ptrs + (long long)s0 * k, k, k, dat, (long long)k * bytes, bytes, n, false, nullptr,
+                              0, st))
+            return rc;
+        const int rc = encode_batch(k, m, bytes, n, dat, (long long)k * bytes, rec, (long long)m * bytes, st, true);
+        if (rc != kOk && !(rc == kInvalid && invalid)) return rc;
+        if (int rc = ptr_copy(rec_ptrs + (long long)s0 * m, m, invalid ? 1 : m, rec, (long long)m * bytes, bytes, n,
+                              true, nullptr, 0, st))
+            return rc;
+    }
+    return invalid ? fail(kInvalid, "k + m > 256 or block_bytes % 8 != 0") : kOk;
+}
+
+static int decode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *const *block_ptrs, uint8_t *d_rows,
+                             int8_t *d_status, hipStream_t st) {
+    if (k < 1 || m < 1 || bytes <= 0 || stripes < 0 || k > 256 || m > 256)
+        return fail(kInvalid, "invalid k, m, block_bytes or stripes");
+    if (stripes == 0) return kOk;
+    if (m > 1 && k > 1 && (k + m > 256 || bytes % 8 != 0))
+        return fail(kInvalid, "k + m > 256 or block_bytes % 8 != 0");
+    if (!block_ptrs || !d_rows) return fail(kInvalid, "null pointer table or rows");
+    Device *d = nullptr;
+    if (int rc = current_device(&d)) return rc;
+    JitConfig cfg;
+    if (k > 1 && m > 1 && jit_ptr_config_for(k, m, bytes, true, &cfg)) {
+        std::string err;
+        bool hard = false;
+        const JitKernels *jk = jit_lookup(d, cfg, true, &err, &hard);
+        if (hard) return fail(kHipError, err);
+        if (jk) {
+            const uint8_t *zero = nullptr;
+            if (int rc = zero_page(d, (size_t)bytes, &zero, st)) return rc;
+            long long s1 = (long long)k * 8;
+            int n = stripes;
+            if (jk->decode_fused && std::getenv("LONGHAIR_AMD_NO_FUSED_PLAN") == nullptr) {
+                const uint8_t *gexp = d->gf_exp;
+                const int16_t *glog = d->gf_log;
+                void *args[] = {(void *)&block_ptrs, &s1, (void *)&d_rows, (void *)&d_status, (void *)&zero,
+                                (void *)&gexp, (void *)&glog, &n};
+                LH_HIP(hipModuleLaunchKernel(jk->decode_fused, (unsigned)jit_blocks(cfg, stripes), 1, 1, 256, 1, 1, 0,
+                                             st, args, nullptr));
+                note_launch("lh_jit_decode_fused(pointer table)");
+                return kOk;
+            }
+            const int e_max = k < m ? k : m;
+            const long long plan_stride = PlanView::bytes(k, m, e_max);
+            Workspace *w = nullptr;
+            if (int rc = workspace(d, st, (size_t)stripes * plan_stride, 0, &w)) return rc;
+            const uint8_t *G = nullptr, *points = nullptr;
+            if (int rc = device_generator(d, k, m, &G, &points, st)) return rc;
+            PlanArgs pa{};
+            pa.rows = d_rows;
+            pa.status = d_status;
+            pa.plan = w->plan.ptr;
+            pa.plan_stride = plan_stride;
+            pa.G = G;
+            pa.points = points;
+            pa.gf_exp = d->gf_exp;
+            pa.gf_log = d->gf_log;
+            pa.k = k;
+            pa.m = m;
+            pa.e_max = e_max;
+            pa.stripes = stripes;
+            pa.want_w = 0;
+            LH_HIP(launch_plan(pa, st));
+            long long s2 = plan_stride;
+            const uint8_t *plan = w->plan.ptr;
+            void *args[] = {(void *)&block_ptrs, &s1, (void *)&plan, &s2, (void *)&zero, &n};
+            LH_HIP(hipModuleLaunchKernel(jk->decode, (unsigned)jit_blocks(cfg, stripes), 1, 1, 256, 1, 1, 0, st, args,
+                                         nullptr));
+            note_launch("lh_jit_decode(pointer table)");
+            return kOk;
+        }
+    }
+    // Gather / strided decode / scatter, per chunk.  For k, m > 1 decode writes exactly the
+    // slots that held recovery rows (row >= k before the call: a copy of the chunk's rows
+    // rides at the end of the chunk); m = 1 and k = 1 write every slot back (the m = 1 path
+    // may write a slot holding an original row, cauchy_256.cpp:487-535).
+    const long long per = (long long)k * bytes + k;
+    uint8_t *buf = nullptr;
+    int chunk = 0;
+    if (int rc = gather_chunk(d, st, per, stripes, &buf, &chunk)) return rc;
+    const bool by_row = k > 1 && m > 1;
+    for (int s0 = 0; s0 < stripes; s0 += chunk) {
+        const int n = std::min(chunk, stripes - s0);
+        uint8_t *blk = buf, *rows0 = buf + (long long)n * k * bytes;
+        uint8_t *const *tab = block_ptrs + (long long)s0 * k;
+        if (int rc = ptr_copy(tab, k, k, blk, (long long)k * bytes, bytes, n, false, nullptr, 0, st)) return rc;
+        if (by_row) LH_HIP(hipMemcpyAsync(rows0, d_rows + (long long)s0 * k, (size_t)n * k, hipMemcpyDeviceToDevice, st));
+        if (int rc = decode_batch(k, m, bytes, n, blk, (long long)k * bytes, d_rows + (long long)s0 * k,
+                                  d_status ? d_status + s0 : nullptr, st, true))
+            return rc;
+        if (int rc = ptr_copy(tab, k, k, blk, (long long)k * bytes, bytes, n, true, by_row ? rows0 : nullptr, k, st))
+            return rc;
+    }
+    return kOk;
+}
+
 // -------------------------------------------------------------- drop-in helpers
 static bool is_device_pointer(const void *p) {
     hipPointerAttribute_t attr;
@@ -1056,6 +1228,20 @@ LH_API int cauchy_256_decode_batch(int k, int m, int block_bytes, int stripes, v
                             (int8_t *)d_status, (hipStream_t)stream, true);
 }
 
+LH_API int cauchy_256_encode_batch_ptrs(int k, int m, int block_bytes, int stripes, const void *const *d_data_ptrs,
+                                        void *const *d_recovery_ptrs, void *stream) {
+    lh::LaunchTrace trace;
+    return lh::encode_batch_ptrs(k, m, block_bytes, stripes, (uint8_t *const *)d_data_ptrs,
+                                 (uint8_t *const *)d_recovery_ptrs, (hipStream_t)stream);
+}
+
+LH_API int cauchy_256_decode_batch_ptrs(int k, int m, int block_bytes, int stripes, void *const *d_block_ptrs,
+                                        unsigned char *d_rows, signed char *d_status, void *stream) {
+    lh::LaunchTrace trace;
+    return lh::decode_batch_ptrs(k, m, block_bytes, stripes, (uint8_t *const *)d_block_ptrs, d_rows,
+                                 (int8_t *)d_status, (hipStream_t)stream);
+}
+
 LH_API int cauchy_256_encode_host_batch(int k, int m, int block_bytes, int stripes, const void *h_data,
                                         long long data_stride, void *h_recovery, long long recovery_stride,
                                         int chunk_stripes) {
@@ -1125,6 +1311,11 @@ LH_API int cauchy_256_jit_precompile(int k, int m, int block_bytes) {
         if (part && std::string(part) != (dec ? "dec" : "enc")) continue;
         if (lh::jit_config_for(k, m, block_bytes, dec == 1, &cfg)) {
             if (!lh::compile_code_object(cfg, &code, &err)) return lh::fail(lh::kHipError, err);
+            // the pointer-table form (cauchy_256_*_batch_ptrs) as well, with LONGHAIR_AMD_PRECOMPILE_PTR=1
+            const char *ptr = std::getenv("LONGHAIR_AMD_PRECOMPILE_PTR");
+            if (ptr && std::string(ptr) == "1" && lh::jit_ptr_config_for(k, m, block_bytes, dec == 1, &cfg) &&
+                !lh::compile_code_object(cfg, &code, &err))
+                return lh::fail(lh::kHipError, err);
         } else if (lh::jit_win_config_for(k, m, block_bytes, &cfg, dec == 1) &&
                    !lh::compile_code_object(cfg, &code, &err)) {
             return lh::fail(lh::kHipError, err);

@@ -113,6 +113,14 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     return true;
 }
 
+bool jit_ptr_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
+    if (!jit_config_for(k, m, bytes, decode, cfg)) return false;
+    if ((long long)(cfg->spw ? cfg->spw : 1) * k > 1024) return false;  // LDS: 4 waves x 8 B x spw x (k + 1) <= 35 KiB
+    cfg->ptr = 1;
+    cfg->al = 0;  // (the aligned forms address through buffer resources)
+    return true;
+}
+
 bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
     if (const char *env = std::getenv("LONGHAIR_AMD_PATH")) {
         if (std::string(env) == "generic") return false;
@@ -559,6 +567,7 @@ std::string jit_source_for(const JitConfig &c) {
     os << "#define LH_K " << c.k << "\n#define LH_M " << c.m << "\n#define LH_BYTES " << c.bytes
        << "\n#define LH_SUB " << c.sub << "\n#define LH_W " << c.W << "\n#define LH_NCH " << c.nch
        << "\n#define LH_SPW " << (c.spw ? c.spw : 1) << "\n#define LH_WPS " << (c.wps ? c.wps : 1) << "\n";
+    if (c.ptr) os << "#define LH_PTR 1\n#define LH_BUF 0\n";
     if (c.al == 1) os << "#define LH_AL 1\n";
     if (c.al == 2) os << "#define LH_ALS 1\n";
     const std::vector<uint8_t> g = generator_matrix(c.k, c.m);
@@ -587,7 +596,7 @@ std::string jit_source_for(const JitConfig &c) {
 
 JitCache::Key JitCache::key_of(const JitConfig &cfg) {
     return Key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines,
-               cfg.al * 10000000 + cfg.win_split * 1000000 + cfg.win * 100000 + cfg.win_lds * 10000 +
+               cfg.ptr * 100000000 + cfg.al * 10000000 + cfg.win_split * 1000000 + cfg.win * 100000 + cfg.win_lds * 10000 +
                    cfg.rows_per_wave * 100 + cfg.win_pf);
 }
 

@@ -28,6 +28,8 @@ struct JitConfig {
     int win_split = 1;    // windowed decode: phase A writes V in place, lh_inverse_gt_kernel does phase B
                           // (0: the fused kernel, phase B from an LDS tile of V)
     int al = 0;           // register networks: 2 aligned output stores (LH_ALS), 1 aligned column loads (LH_AL)
+    int ptr = 0;          // register networks: blocks addressed through a pointer table (LH_PTR,
+                          // cauchy_256_*_batch_ptrs)
     int lanes_per_launch_unit() const { return 64; }
 };
 
@@ -45,6 +47,11 @@ struct JitKernels {
 // is served by the generic kernel (too many recovery rows for the register budget, or
 // a network too large for the instruction cache).
 bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg);
+
+// The pointer-table form of a register-network configuration (cauchy_256_*_batch_ptrs):
+// false when the shape has none (no register network, or a wave's stripes hold more block
+// pointers than its LDS share: spw * k > 1024).
+bool jit_ptr_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg);
 
 // Windowed large-m encode configuration (m too large for the register-resident network).
 bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode = false);

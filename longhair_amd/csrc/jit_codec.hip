@@ -82,6 +82,12 @@ __device__ __forceinline__ lh_word lh_load(const unsigned char *p) {
 // for 64-bit global addresses (profiles/r2_ubench_pattern.txt).
 #define LH_BUF 1
 #endif
+#ifndef LH_PTR
+#define LH_PTR 0
+#endif
+#if LH_PTR && LH_BUF
+#error "LH_PTR: scattered blocks are addressed by 64-bit pointers (LH_BUF 0)"
+#endif
 #ifndef LH_NT_DEC
 // Decode loads: default cache policy.  The decode writes its outputs in place, into lines
 // it (or a neighbour stripe's wave) read; non-temporal loads of those lines cost ~6 % in
@@ -455,6 +461,47 @@ __device__ __forceinline__ void lh_dopaque(lh_word (&acc)[LH_M][8]) {
     }
 }
 
+#if LH_PTR
+// Scattered blocks (cauchy_256_encode_batch_ptrs / cauchy_256_decode_batch_ptrs): the
+// kernel's block argument is a device table of block pointers, one row of LH_K pointers per
+// stripe (row stride `stride` bytes).  Each wave copies the rows of its stripes into LDS
+// (its own 8 * LH_SPW * (LH_K + 1) bytes; the host keeps 4 waves' worth <= 33 KiB); every column
+// address is then an LDS read, counted by lgkmcnt and so never waiting behind the block loads
+// in flight (vmcnt), unlike a pointer fetched from memory per column.  The lanes of a stripe
+// fill its row (they share the stripe's early exits, so a partial wave fills what it reads).
+// An index the compiler cannot see through: the LDS read of a column's pointer stays next to
+// that column's loads (each asm is ordered after the previous column's accumulator pins)
+// instead of every column's pointer being read up front and held in registers (k29/m4 fused
+// decode: 192 VGPRs, 2 waves/SIMD, with them hoisted).
+__device__ __forceinline__ int lh_late(int i) {
+    asm volatile("" : "+v"(i));
+    return i;
+}
+// Entry LH_K of a row is `extra` (decode: the zero page, so an absent column is one more
+// table index, not a 64-bit select: with the select the k29/m4 fused decode took 192 VGPRs
+// instead of 157).
+__device__ __forceinline__ const unsigned long long *lh_ptab(const lh_lane &l, const unsigned char *tab,
+                                                            long long stride, const unsigned char *extra) {
+    __shared__ unsigned long long lh_pt[4][LH_SPW * (LH_K + 1)];
+    const int lane = threadIdx.x & 63;
+#if LH_NCH <= 64
+    const int sl = lane / LH_NCH, c = lane - sl * LH_NCH, step = LH_NCH;
+#else
+    const int sl = 0, c = lane, step = 64;
+#endif
+    unsigned long long *row = &lh_pt[threadIdx.x >> 6][sl * (LH_K + 1)];
+    const unsigned long long *src = (const unsigned long long *)(tab + l.stripe * stride);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous stripe group's reads
+    __builtin_amdgcn_wave_barrier();
+    for (int x = c; x < LH_K; x += step) row[x] = src[x];
+    if (c == 0) row[LH_K] = (unsigned long long)extra;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return row;
+}
+#endif
+
 // Encode column source of a lane: with LH_BUF one buffer resource over the wave's stripes
 // (column x at soffset x * LH_BYTES, a wave-uniform SGPR; sub-block b in the immediate
 // offset; one 32-bit lane offset), else the lane's 64-bit chunk pointer.
@@ -480,6 +527,17 @@ struct lh_esrc {
 #pragma unroll
         for (int b = 0; b < 8; ++b) d[b] = load(x, b);
 #endif
+    }
+#elif LH_PTR
+    const unsigned long long *pt;  // LDS: the lane's stripe's LH_K block pointers
+    int p;
+    __device__ __forceinline__ lh_word load(int x, int b) const {
+        return lh_load((const unsigned char *)pt[x] + p + b * LH_SUB);
+    }
+    __device__ __forceinline__ void load8(lh_word (&d)[8], int x) const {
+        const unsigned char *q = (const unsigned char *)pt[lh_late(x)] + p;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) d[b] = lh_load(q + b * LH_SUB);
     }
 #else
     const unsigned char *base;
@@ -546,6 +604,9 @@ __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned ch
 #endif
     S.rs = __builtin_amdgcn_make_buffer_rsrc((void *)(in + s0 * in_stride), 0, (int)(nst * in_stride), 0x00020000);
     S.lbase = (int)((l.stripe - s0) * in_stride) + l.p;
+#elif LH_PTR
+    S.pt = lh_ptab(l, in, in_stride, nullptr);
+    S.p = l.p;
 #else
     S.base = in + l.stripe * in_stride + l.p;
 #endif
@@ -569,6 +630,17 @@ __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned ch
             return;
         }
     }
+#endif
+#if LH_PTR
+    // out: the recovery blocks' pointer table, LH_M per stripe (row stride out_stride bytes)
+    const unsigned long long *ot = (const unsigned long long *)(out + l.stripe * out_stride);
+#pragma unroll
+    for (int r = 0; r < LH_M; ++r) {
+        unsigned char *o = (unsigned char *)ot[r] + l.ps;
+#pragma unroll
+        for (int y = 0; y < 8; ++y) lh_store(o + y * LH_SUB, acc[r][y]);
+    }
+    return;
 #endif
     unsigned char *o = out + l.stripe * out_stride + l.ps;
 #pragma unroll
@@ -663,12 +735,21 @@ __device__ __forceinline__ void lh_load_col(lh_word (&d)[8], const lh_dsrc &S, u
 #endif
 }
 #else
-// Column source of a lane: its stripe's chunk pointer and the zero page.
+// Column source of a lane: its stripe's chunk pointer (LH_PTR: its stripe's block pointers
+// in LDS and its chunk offset) and the zero page.
 struct lh_dsrc {
+#if LH_PTR
+    const unsigned long long *pt;  // LDS: the stripe's block pointers, then the zero page
+    int p;
+    __device__ __forceinline__ const unsigned char *col(unsigned int slot) const {
+        return (const unsigned char *)pt[lh_late(slot == 0xFFu ? LH_K : (int)slot)] + p;
+    }
+#else
     const unsigned char *base, *zero;
     __device__ __forceinline__ const unsigned char *col(unsigned int slot) const {
         return (slot == 0xFFu) ? zero : base + (long long)slot * LH_BYTES;
     }
+#endif
 };
 #ifndef LH_ZSKIP
 #define LH_ZSKIP 0  // lanes of absent columns skip the zero-page load (exec-masked)
@@ -866,7 +947,11 @@ __device__ __forceinline__ void lh_dec_phase_b(const lh_word (&v)[LH_M][8], cons
                                                     c == 0 ? lane + LH_NCH - 1 : lane - 1, o);
             }
 #else
+#if LH_PTR
+            unsigned char *dst = (unsigned char *)S.pt[LH_BYTE(outw, i)] + soff;  // soff: the lane's store offset
+#else
             unsigned char *dst = base + (long long)LH_BYTE(outw, i) * LH_BYTES;
+#endif
 #pragma unroll
             for (int y = 0; y < 8; ++y)
 #if LH_AL
@@ -894,6 +979,9 @@ __device__ __forceinline__ lh_dsrc lh_make_dsrc(const lh_lane &l, long long wave
 #endif
     S.rs = __builtin_amdgcn_make_buffer_rsrc(blocks + s0 * stripe_stride, 0, (int)(nst * stripe_stride), 0x00020000);
     S.lbase = (int)((l.stripe - s0) * stripe_stride) + l.p;
+#elif LH_PTR
+    S.pt = lh_ptab(l, blocks, stripe_stride, zero_page);
+    S.p = l.p;
 #else
     S.base = blocks + l.stripe * stripe_stride + l.p;
     S.zero = zero_page + l.p;
@@ -923,6 +1011,8 @@ __device__ __forceinline__ void lh_decode_body(const lh_lane &l, long long wave,
     }
 #if LH_BUF
     lh_dec_phase_b(v, pr, blocks + l.stripe * stripe_stride + l.ps, l.last, S, S.lbase - l.p);
+#elif LH_PTR
+    lh_dec_phase_b(v, pr, nullptr, l.last, S, l.ps);
 #else
     lh_dec_phase_b(v, pr, blocks + l.stripe * stripe_stride + l.ps, l.last, S, 0);
 #endif

@@ -19,6 +19,8 @@
 //                           solution).
 //   lh_writeback_kernel     pinned-host decode pipeline: recovered blocks straight into
 //                           the caller's pinned buffer.
+//   lh_ptr_copy_kernel      pointer-table batches on the paths without a pointer form:
+//                           scattered blocks into a contiguous chunk and back.
 //
 // Lanes own W-byte columns of a stripe's sub-blocks: a lane loads the same byte range of
 // all 8 sub-blocks of a block and produces the same range of all 8 output sub-blocks, so
@@ -919,6 +921,40 @@ __global__ void __launch_bounds__(1024) lh_inverse_gt_kernel(lh::InverseArgs a) 
     lh_inverse_gt_body(a, lvA, lvB, tlo, thi);
 }
 
+// ---------------------------------------------------------- pointer-table gather / scatter
+// One wave per (stripe, block): 16 B per lane when both addresses and the block size allow,
+// else 8 B, else single bytes (the caller's blocks may sit at any alignment).  Wave-uniform
+// choice: every lane of the wave copies the same block.
+__global__ void __launch_bounds__(256) lh_ptr_copy_kernel(lh::PtrCopyArgs a) {
+    const long long item = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (item >= (long long)a.stripes * a.ncopy) return;
+    const long long s = item / a.ncopy;
+    const int j = (int)(item - s * a.ncopy);
+    const long long t = s * a.n + j;  // table entry
+    if (a.scatter && a.sel && a.sel[t] < a.sel_min) return;
+    uint8_t *blk = a.ptrs[t];
+    uint8_t *lin = a.chunk + s * a.stride + (long long)j * a.bytes;
+    const uint8_t *src = a.scatter ? lin : blk;
+    uint8_t *dst = a.scatter ? blk : lin;
+    const uintptr_t al = (uintptr_t)src | (uintptr_t)dst | (uintptr_t)a.bytes;
+    if ((al & 15) == 0) {
+        for (int o = lane * 16; o < a.bytes; o += 64 * 16) {
+            uint4 v;
+            __builtin_memcpy(&v, src + o, 16);
+            __builtin_memcpy(dst + o, &v, 16);
+        }
+    } else if ((al & 7) == 0) {
+        for (int o = lane * 8; o < a.bytes; o += 64 * 8) {
+            uint2 v;
+            __builtin_memcpy(&v, src + o, 8);
+            __builtin_memcpy(dst + o, &v, 8);
+        }
+    } else {
+        for (int o = lane; o < a.bytes; o += 64) dst[o] = src[o];
+    }
+}
+
 // ------------------------------------------------------------------ pinned-host write-back
 // One workgroup per stripe: the slots whose row was a recovery row before the decode are
 // the slots decode may have written (its outputs; an invalid stripe is untouched, so the
@@ -1012,6 +1048,14 @@ hipError_t launch_scatter(const ScatterArgs &a, hipStream_t st) {
     const long long lanes = (long long)a.stripes * a.e_max * ((a.bytes + 15) / 16);
     hipLaunchKernelGGL(lh_scatter_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a);
     note_launch("lh_scatter_kernel");
+    return hipGetLastError();
+}
+
+hipError_t launch_ptr_copy(const PtrCopyArgs &a, hipStream_t st) {
+    const long long waves = (long long)a.stripes * a.ncopy;
+    if (waves <= 0) return hipSuccess;
+    hipLaunchKernelGGL(lh_ptr_copy_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
+    note_launch(a.scatter ? "lh_ptr_copy_kernel(scatter)" : "lh_ptr_copy_kernel(gather)");
     return hipGetLastError();
 }
 

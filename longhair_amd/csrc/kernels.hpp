@@ -127,6 +127,20 @@ struct WritebackArgs {
     int k, bytes, stripes;
 };
 
+// Pointer-table batches (cauchy_256_*_batch_ptrs) on the paths without a pointer form:
+// block j of stripe s lives at ptrs[s * n + j].  gather: into a contiguous chunk (stripe s,
+// block j at chunk + s * stride + j * bytes); scatter: back from it, only the blocks with
+// sel[s * n + j] >= sel_min when sel is set (decode: the slots that held recovery rows).
+// Only the first ncopy blocks of each stripe are copied.
+struct PtrCopyArgs {
+    uint8_t *const *ptrs;         // [stripe][n]
+    uint8_t *chunk;
+    long long stride;
+    const uint8_t *sel;           // [stripe][n] or NULL
+    int sel_min;
+    int n, ncopy, bytes, stripes, scatter;
+};
+
 // Launch trace (codec.cpp): every launch site records the kernel it enqueued, so the
 // calling thread can ask which kernels its last batch call ran (cauchy_256_last_launch).
 void note_launch(const char *kernel);
@@ -137,5 +151,6 @@ hipError_t launch_frame(const FrameArgs &a, hipStream_t st);
 hipError_t launch_xor_reduce(const XorArgs &a, hipStream_t st);
 hipError_t launch_scatter(const ScatterArgs &a, hipStream_t st);
 hipError_t launch_plan(const PlanArgs &a, hipStream_t st);
+hipError_t launch_ptr_copy(const PtrCopyArgs &a, hipStream_t st);
 
 }  // namespace lh
