@@ -515,11 +515,13 @@ def pcie_timed(lh, k, m, nbytes, xn, bn, rn, recn, b0, r0, world, rank, reps=3, 
                     f"{reps} (decode: the workload's erasure patterns, recovered blocks written back)"}
 
 
-def ptr_leg(lh, k, m, nbytes, X, D, rows0, rec_view, reps=5):
+def ptr_leg(lh, k, m, nbytes, X, D, rows0, rec_view, rec_index=None, reps=5):
     """The same step through the pointer-table calls (cauchy_256_*_batch_ptrs): tables that
     point at the very blocks the strided step uses, so the bytes moved are the same and only
-    the addressing differs.  HIP-event times on the launch stream, mean of `reps`; the decoded
-    data is checked against X afterwards."""
+    the addressing differs.  With random erasures (rec_index) the received recovery slots
+    point straight at the encode's output blocks, where the strided step copies them into the
+    decode buffer first (that copy is outside both timings).  HIP-event times on the launch
+    stream, mean of `reps`; the decoded data is checked against X afterwards."""
     import torch
     stripes = X.shape[0]
     s_idx = torch.arange(stripes, device="cuda", dtype=torch.int64).unsqueeze(1)
@@ -528,6 +530,8 @@ def ptr_leg(lh, k, m, nbytes, X, D, rows0, rec_view, reps=5):
         return (t.data_ptr() + s_idx * t.stride(0) + torch.arange(n, device="cuda", dtype=torch.int64) * t.stride(1)
                 ).contiguous()
     dptr, rptr, bptr = table(X, k), table(rec_view, m), table(D, k)
+    if rec_index is not None:
+        bptr.view(-1)[rec_index[0]] = rec_view.data_ptr() + rec_index[1] * nbytes
     rows = rows0.clone()
     stream = torch.cuda.current_stream()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
@@ -548,7 +552,11 @@ def ptr_leg(lh, k, m, nbytes, X, D, rows0, rec_view, reps=5):
             enc += ev[0].elapsed_time(ev[1]) / reps
             dec += ev[2].elapsed_time(ev[3]) / reps
     order = rows.long().argsort(dim=1)
-    ok = bool(torch.equal(torch.gather(D, 1, order.unsqueeze(-1).expand(-1, -1, nbytes)), X))
+    got = D
+    if rec_index is not None:
+        got = D.clone()
+        got.view(-1, nbytes)[rec_index[0]] = rec_view.reshape(-1, nbytes)[rec_index[1]]
+    ok = bool(torch.equal(torch.gather(got, 1, order.unsqueeze(-1).expand(-1, -1, nbytes)), X))
     return {"encode_ms": round(enc, 4), "decode_ms": round(dec, 4),
             "encode_GBps": round(k * nbytes * stripes / (enc * 1e-3) / 1e9, 1),
             "decode_GBps": round(k * nbytes * stripes / (dec * 1e-3) / 1e9, 1),
@@ -738,8 +746,8 @@ def main():
                     "frac_of_measured_floor": round(FLAT_FLOOR_MS / enc_ms, 4),
                     "floor_frac_of_hbm_peak": round(k * nbytes * stripes / (FLAT_FLOOR_MS * 1e-3) / 1e9
                                                     / HBM_PEAK_GBS, 4)})
-    if not dry and args.ptr == "on" and rec_index is None:
-        out["ptr_tables"] = ptr_leg(lh, k, m, nbytes, X, D, rows0, rec_view)
+    if not dry and args.ptr == "on":
+        out["ptr_tables"] = ptr_leg(lh, k, m, nbytes, X, D, rows0, rec_view, rec_index)
     if not dry and args.pcie == "on":
         # every rank at once: the node's host links and memory are shared
         out["pcie"] = pcie_leg(lh, args, k, m, nbytes, X, D, rows0, rec_view, rec_index, world, rank)

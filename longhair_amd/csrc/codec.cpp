@@ -666,6 +666,23 @@ static int encode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
         }
         if (hard) return fail(kHipError, err);
     }
+    if (jit_win_ptr_config_for(k, m, bytes, &cfg)) {
+        std::string err;
+        bool hard = false;
+        const JitKernels *jk = jit_lookup(d, cfg, true, &err, &hard);
+        if (jk && jk->encode_win) {
+            const long long blocks = (long long)stripes * (cfg.sub / (64 * cfg.W));
+            if (blocks > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
+            const unsigned threads = 64u * (unsigned)((m + cfg.rows_per_wave - 1) / cfg.rows_per_wave);
+            long long in_stride = (long long)k * 8, out_stride = (long long)m * 8;
+            int n = stripes;
+            void *args[] = {(void *)&data_ptrs, &in_stride, (void *)&rec_ptrs, &out_stride, &n};
+            LH_HIP(hipModuleLaunchKernel(jk->encode_win, (unsigned)blocks, 1, 1, threads, 1, 1, 0, st, args, nullptr));
+            note_launch("lh_jit_encode_win(pointer table)");
+            return kOk;
+        }
+        if (hard) return fail(kHipError, err);
+    }
     // Gather / strided encode / scatter, per chunk.  An invalid shape (m > 1 with k + m > 256
     // or bytes % 8 != 0) still gets recovery block 0 first, as the reference.
     const bool invalid = m > 1 && k > 1 && (k + m > 256 || bytes % 8 != 0);
@@ -746,6 +763,59 @@ static int decode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
             LH_HIP(hipModuleLaunchKernel(jk->decode, (unsigned)jit_blocks(cfg, stripes), 1, 1, 256, 1, 1, 0, st, args,
                                          nullptr));
             note_launch("lh_jit_decode(pointer table)");
+            return kOk;
+        }
+    }
+    // Large m: the planner, the windowed phase A reading the slots through the table (V_r
+    // back in place of R_r) and phase B through the same table.
+    if (k > 1 && m > 1 && !jit_config_for(k, m, bytes, true, &cfg) && jit_win_ptr_config_for(k, m, bytes, &cfg, true)) {
+        std::string err;
+        bool hard = false;
+        const JitKernels *wk = jit_lookup(d, cfg, true, &err, &hard);
+        if (hard) return fail(kHipError, err);
+        if (wk && wk->decode_wide) {
+            const int e_max = k < m ? k : m;
+            const long long plan_stride = PlanView::bytes(k, m, e_max);
+            const long long cps = cfg.sub / (64 * cfg.W);
+            if ((long long)stripes * cps > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
+            Workspace *w = nullptr;
+            if (int rc = workspace(d, st, (size_t)stripes * plan_stride, 0, &w)) return rc;
+            const uint8_t *G = nullptr, *points = nullptr, *zero = nullptr;
+            if (int rc = device_generator(d, k, m, &G, &points, st)) return rc;
+            if (int rc = zero_page(d, (size_t)bytes, &zero, st)) return rc;
+            PlanArgs pa{};
+            pa.rows = d_rows;
+            pa.status = d_status;
+            pa.plan = w->plan.ptr;
+            pa.plan_stride = plan_stride;
+            pa.G = G;
+            pa.points = points;
+            pa.gf_exp = d->gf_exp;
+            pa.gf_log = d->gf_log;
+            pa.k = k;
+            pa.m = m;
+            pa.e_max = e_max;
+            pa.stripes = stripes;
+            pa.want_w = 0;
+            LH_HIP(launch_plan(pa, st));
+            const unsigned threads = 64u * (unsigned)((m + cfg.rows_per_wave - 1) / cfg.rows_per_wave);
+            long long s1 = (long long)k * 8, s2 = plan_stride;
+            const uint8_t *plan = w->plan.ptr;
+            int n = stripes;
+            void *args[] = {(void *)&block_ptrs, &s1, (void *)&plan, &s2, (void *)&zero, &n};
+            LH_HIP(hipModuleLaunchKernel(wk->decode_wide, (unsigned)(stripes * cps), 1, 1, threads, 1, 1, 0, st, args,
+                                         nullptr));
+            note_launch("lh_jit_decode_wide(pointer table)");
+            InverseArgs ia{};
+            ia.ptrs = block_ptrs;
+            ia.plan = plan;
+            ia.plan_stride = plan_stride;
+            ia.k = k;
+            ia.m = m;
+            ia.e_max = e_max;
+            ia.bytes = bytes;
+            ia.stripes = stripes;
+            LH_HIP(launch_inverse(ia, st));
             return kOk;
         }
     }
@@ -1316,9 +1386,12 @@ LH_API int cauchy_256_jit_precompile(int k, int m, int block_bytes) {
             if (ptr && std::string(ptr) == "1" && lh::jit_ptr_config_for(k, m, block_bytes, dec == 1, &cfg) &&
                 !lh::compile_code_object(cfg, &code, &err))
                 return lh::fail(lh::kHipError, err);
-        } else if (lh::jit_win_config_for(k, m, block_bytes, &cfg, dec == 1) &&
-                   !lh::compile_code_object(cfg, &code, &err)) {
-            return lh::fail(lh::kHipError, err);
+        } else if (lh::jit_win_config_for(k, m, block_bytes, &cfg, dec == 1)) {
+            if (!lh::compile_code_object(cfg, &code, &err)) return lh::fail(lh::kHipError, err);
+            const char *ptr = std::getenv("LONGHAIR_AMD_PRECOMPILE_PTR");
+            if (ptr && std::string(ptr) == "1" && lh::jit_win_ptr_config_for(k, m, block_bytes, &cfg, dec == 1) &&
+                !lh::compile_code_object(cfg, &code, &err))
+                return lh::fail(lh::kHipError, err);
         }
     }
     return 0;

@@ -121,6 +121,14 @@ bool jit_ptr_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     return true;
 }
 
+bool jit_win_ptr_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
+    if (!jit_win_config_for(k, m, bytes, cfg, decode)) return false;
+    cfg->ptr = 1;
+    cfg->win_lds = 1;                 // (the pointer form stages columns by LDS-DMA)
+    cfg->win_split = decode ? 1 : 0;  // (and writes V back for lh_inverse_gt_kernel)
+    return true;
+}
+
 bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
     if (const char *env = std::getenv("LONGHAIR_AMD_PATH")) {
         if (std::string(env) == "generic") return false;
@@ -203,6 +211,17 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
     const std::string toff = priv ? " + " + std::to_string(g * 2048) : "";  // this wave's ring slot
     const bool split = elim && c.win_split == 1;  // V_r goes back in place of R_r (lh_inverse_gt_kernel follows)
     const bool fgt = elim && c.win_split == 2;     // fused, multiply through the per-code-object table
+    // c.ptr (pointer-table batches; LDS staging and the split decode only): the stripe's
+    // block pointers ride in VGPR lanes (ptl: k slots / columns, otl: m recovery blocks) and
+    // lh_pp reads one as a wave-uniform pointer; coff = the workgroup's byte offset in every
+    // block, loff = the lane's.
+    if (c.ptr)
+        os << "__device__ __forceinline__ void lh_wg" << g << "(const unsigned long long (&ptl)[LH_NP], "
+           << (elim ? "const unsigned char *__restrict__ zb, const unsigned int (&slv)[LH_NQ], "
+                      "const unsigned char *__restrict__ pl"
+                    : "const unsigned long long (&otl)[LH_NPO]")
+           << ", const int coff, const int loff) {\n";
+    else
     os << "__device__ __forceinline__ void lh_wg" << g << "(" << (elim ? "" : "const ") << "unsigned char *__restrict__ base, "
        << (elim ? "const unsigned char *__restrict__ zero, const unsigned int (&slv)[LH_NQ], unsigned int *__restrict__ lv, "
                   "const unsigned char *__restrict__ pl"
@@ -217,7 +236,9 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
     }
     auto dcol = [&](int x) {  // uniform base of column x for the DMA (stripe + chunk, or zero page)
         std::ostringstream e;
-        if (elim) e << "lh_slot(slv, " << x << ", sb, zb)";
+        if (c.ptr && elim) e << "lh_pslot(slv, ptl, " << x << ", coff, zb)";
+        else if (c.ptr) e << "(lh_pp(ptl, " << x << ") + coff)";
+        else if (elim) e << "lh_slot(slv, " << x << ", sb, zb)";
         else e << "(sb + " << (long long)x * c.bytes << "LL)";
         return e.str();
     };
@@ -305,8 +326,11 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
     if (split) {  // V_r = R_r + sum_x ...: read R_r, store V_r over it (absent rows: nothing)
         for (int r = r0; r < r1; ++r) {
             os << "  {\n    const unsigned int s = (unsigned int)__builtin_amdgcn_readlane((int)slv[" << (k + r) / 64
-               << "], " << (k + r) % 64 << ");\n    if (s != 0xFFu) {\n"
-               << "      unsigned char *rp = base + (long long)s * " << c.bytes << ";\n";
+               << "], " << (k + r) % 64 << ");\n    if (s != 0xFFu) {\n";
+            if (c.ptr)
+                os << "      unsigned char *rp = lh_pp(ptl, (int)s) + loff;\n";
+            else
+                os << "      unsigned char *rp = base + (long long)s * " << c.bytes << ";\n";
             for (int y = 0; y < 8; ++y)
                 os << "      const unsigned int r" << y << " = lh_ld_r(rp + " << y * c.sub << ");\n";
             for (int y = 0; y < 8; ++y)
@@ -373,6 +397,13 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
            << "        lv[(i * 8 + y) * 64 + lnb] = 0u;\n      }\n    }\n"
            << "    __syncthreads();  // the tile is clear for the next batch\n"
            << "  }\n";
+    } else if (c.ptr) {
+        for (int r = r0; r < r1; ++r) {
+            os << "  {\n    unsigned char *op = lh_pp(otl, " << r << ") + loff;\n";
+            for (int y = 0; y < 8; ++y)
+                os << "    lh_st(op + " << y * c.sub << ", a" << (r - r0) << "_" << y << ");\n";
+            os << "  }\n";
+        }
     } else {
         for (int r = r0; r < r1; ++r)
             for (int y = 0; y < 8; ++y)
@@ -419,7 +450,39 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
            << "  asm volatile(LH_INV_JUMPG8_ASM : LH_INV_JUMPG8_OUTS(acc) : LH_INV_JUMPG_INS(tl, th, t), [r] \"n\"(R),\n"
            << "               [hi] \"s\"(hi) : \"s92\", \"s93\", \"s94\", \"s95\", \"s97\", \"scc\");\n}\n";
     }
+    if (c.ptr)
+        os << "__device__ __forceinline__ const unsigned char *lh_pslot(const unsigned int (&slv)[LH_NQ],\n"
+           << "    const unsigned long long (&ptl)[LH_NP], const int i, const int coff, const unsigned char *zb) {\n"
+           << "  const int s = __builtin_amdgcn_readlane((int)slv[i / 64], i % 64);\n"
+           << "  return s == 0xFF ? zb : lh_pp(ptl, s) + coff;\n}\n";
     for (int g = 0; g < NG; ++g) emit_win_group(os, c, G, g);
+    if (c.ptr) {
+        // blocks: the pointer table, k slot pointers per stripe (row stride `stride` bytes)
+        os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
+           << "lh_jit_decode_wide(unsigned char *__restrict__ blocks, long long stride,\n"
+           << "                   const unsigned char *__restrict__ plan, long long plan_stride,\n"
+           << "                   const unsigned char *__restrict__ zero_page, int stripes) {\n"
+           << "  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
+           << "  const int lane = threadIdx.x & 63;\n"
+           << "  const long long stripe = blockIdx.x / " << CPS << ";\n"
+           << "  if (stripe >= stripes) return;\n"
+           << "  const unsigned char *pl = plan + stripe * plan_stride;\n"
+           << "  if (pl[0] == 0) return;  // workgroup-uniform\n"
+           << "  unsigned int slv[LH_NQ];\n"
+           << "#pragma unroll\n  for (int q = 0; q < LH_NQ; ++q) {\n"
+           << "    const int i = q * 64 + lane;\n"
+           << "    slv[q] = i < " << km << " ? (unsigned int)pl[" << 16 + e_max << " + i] : 0xFFu;\n"
+           << "  }\n"
+           << "  unsigned long long ptl[LH_NP];\n"
+           << "  lh_ptab_lanes(ptl, (const unsigned long long *)(blocks + stripe * stride), " << c.k << ");\n"
+           << "  const int coff = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << ";\n"
+           << "  const unsigned char *zb = zero_page + coff;\n";
+        for (int g = 0; g < NG; ++g)
+            os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << "(ptl, zb, slv, pl, coff, coff + lane * "
+               << c.W << ");\n";
+        os << "}\n";
+        return;
+    }
     os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
        << "lh_jit_decode_wide(unsigned char *__restrict__ blocks, long long stride,\n"
        << "                   const unsigned char *__restrict__ plan, long long plan_stride,\n"
@@ -489,6 +552,22 @@ static std::string win_source_for(const JitConfig &c) {
        << "                                   (__attribute__((address_space(3))) void *)lds, 16, 0, LH_NT ? 2 : 0);\n}\n"
        << "// s_waitcnt vmcnt(N) with expcnt / lgkmcnt untouched (gfx9 encoding)\n"
        << "#define lh_wait_vm(N) __builtin_amdgcn_s_waitcnt(((N) & 15) | (((N) >> 4) << 14) | (7 << 4) | (15 << 8))\n";
+    if (c.ptr)
+        os << "#define LH_NP " << (c.k + 63) / 64 << "\n#define LH_NPO " << (c.m + 63) / 64 << "\n"
+           << "// entry i of a pointer table held in VGPR lanes (lane i % 64 of t[i / 64]), wave-uniform\n"
+           << "template <int N>\n"
+           << "__device__ __forceinline__ unsigned char *lh_pp(const unsigned long long (&t)[N], const int i) {\n"
+           << "  unsigned lo = 0, hi = 0;\n"
+           << "#pragma unroll\n  for (int q = 0; q < N; ++q)\n"
+           << "    if ((i >> 6) == q) {\n"
+           << "      lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)t[q], i & 63);\n"
+           << "      hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(t[q] >> 32), i & 63);\n"
+           << "    }\n"
+           << "  return (unsigned char *)(((unsigned long long)hi << 32) | lo);\n}\n"
+           << "template <int N>\n"
+           << "__device__ __forceinline__ void lh_ptab_lanes(unsigned long long (&t)[N], const unsigned long long *row, int n) {\n"
+           << "  const int lane = threadIdx.x & 63;\n"
+           << "#pragma unroll\n  for (int q = 0; q < N; ++q) t[q] = q * 64 + lane < n ? row[q * 64 + lane] : 0ull;\n}\n";
     // One __shared__ object per LDS ring slot: the compiler's LDS-DMA wait tracking tells
     // distinct objects apart, so reading tile x % D does not wait for the DMA into another.
     if (c.win_lds)
@@ -514,6 +593,24 @@ static std::string win_source_for(const JitConfig &c) {
         return os.str();
     }
     for (int g = 0; g < NG; ++g) emit_win_group(os, c, G, g);
+    if (c.ptr) {
+        // in / out: the pointer tables (k data, m recovery block pointers per stripe)
+        os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
+           << "lh_jit_encode_win(const unsigned char *__restrict__ in, long long in_stride,\n"
+           << "                  unsigned char *__restrict__ out, long long out_stride, int stripes) {\n"
+           << "  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
+           << "  const long long stripe = blockIdx.x / " << CPS << ";\n"
+           << "  if (stripe >= stripes) return;\n"
+           << "  unsigned long long ptl[LH_NP], otl[LH_NPO];\n"
+           << "  lh_ptab_lanes(ptl, (const unsigned long long *)(in + stripe * in_stride), " << c.k << ");\n"
+           << "  lh_ptab_lanes(otl, (const unsigned long long *)(out + stripe * out_stride), " << c.m << ");\n"
+           << "  const int coff = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << ";\n";
+        for (int g = 0; g < NG; ++g)
+            os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << "(ptl, otl, coff, coff + (int)(threadIdx.x & 63) * "
+               << c.W << ");\n";
+        os << "}\n";
+        return os.str();
+    }
     os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
        << "lh_jit_encode_win(const unsigned char *__restrict__ in, long long in_stride,\n"
        << "                  unsigned char *__restrict__ out, long long out_stride, int stripes) {\n"

@@ -55,6 +55,8 @@ bool jit_ptr_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg);
 
 // Windowed large-m encode configuration (m too large for the register-resident network).
 bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode = false);
+// Its pointer-table form (LDS-staged columns, split decode).
+bool jit_win_ptr_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode = false);
 
 // Number of ones in the expanded generator (= XORs of the straight-line network).
 long long generator_ones(int k, int m);

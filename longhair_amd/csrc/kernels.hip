@@ -662,6 +662,8 @@ struct lh_pb_ctx {
     uint32_t rslot;
     unsigned long long used;
     uint8_t *sbase, *base;
+    uint8_t *const *ptab;  // pointer-table batches: the stripe's k slot pointers, else NULL
+    int coff;              // the workgroup's byte offset in every block (its 2 KiB chunk)
     int dof0, dof1;
     __device__ __forceinline__ lh_pb_ctx(const lh::InverseArgs &a_, const uint8_t *pl)
         : a(a_), pv(pl, a_.k, a_.m, a_.e_max) {
@@ -674,7 +676,9 @@ struct lh_pb_ctx {
         rslot = lane < m ? (uint32_t)pv.rec_slot(lane) : 0xFFu;
         used = __ballot(rslot != 0xFFu);
         const int cps = a.bytes >> 11;
-        sbase = a.blocks + (blockIdx.x / cps) * a.stride + (int)(blockIdx.x % cps) * 256;  // wave-uniform
+        coff = (int)(blockIdx.x % cps) * 256;
+        ptab = a.ptrs ? a.ptrs + (blockIdx.x / cps) * a.k : nullptr;
+        sbase = ptab ? nullptr : a.blocks + (blockIdx.x / cps) * a.stride + coff;  // wave-uniform
         base = sbase + lane * 4;
         dof0 = (lane >> 4) * sub + (lane & 15) * 16;
         dof1 = dof0 + 4 * sub;
@@ -684,7 +688,7 @@ struct lh_pb_ctx {
         for (int q = 0; q < g && rest; ++q) rest &= rest - 1;
         for (int j = g; rest && j < 8; j += nw) {
             const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)rslot, __builtin_ctzll(rest));
-            const uint8_t *src = sbase + (long long)slot * a.bytes;
+            const uint8_t *src = slot_base(slot);
             uint8_t *dst = (uint8_t *)buf + j * 2048;
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + dof0),
                                              (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
@@ -692,6 +696,10 @@ struct lh_pb_ctx {
                                              (__attribute__((address_space(3))) void *)(dst + 1024), 16, 0, 0);
             for (int q = 0; q < nw && rest; ++q) rest &= rest - 1;
         }
+    }
+    // The workgroup's chunk of slot `slot` (wave-uniform).
+    __device__ __forceinline__ const uint8_t *slot_base(uint32_t slot) const {
+        return ptab ? ptab[slot] + coff : sbase + (long long)slot * a.bytes;
     }
     __device__ __forceinline__ static unsigned long long skip_tile(unsigned long long rest) {
         for (int j = 0; rest && j < 8; ++j) rest &= rest - 1;
@@ -740,7 +748,7 @@ struct lh_pb_ctx {
         }
     }
     __device__ __forceinline__ void store(int out, const uint32_t (&acc)[8]) const {
-        uint8_t *dst = base + (long long)pv.out_slot(out) * a.bytes;
+        uint8_t *dst = (uint8_t *)slot_base(pv.out_slot(out)) + lane * 4;
 #pragma unroll
         for (int y = 0; y < 8; ++y) __builtin_nontemporal_store(acc[y], (uint32_t *)(dst + (long long)y * sub));
     }

@@ -111,6 +111,8 @@ struct InverseArgs {
     int k, m, e_max, bytes, stripes;
     int pack;                     // lh_inverse_gt_kernel: 8 consecutive outputs per wave
     int jump_fallback;            // lh_inverse_gt_kernel: take the in-asm table (tests)
+    uint8_t *const *ptrs;         // pointer-table batches: slot j of stripe s at ptrs[s*k + j]
+                                  // (blocks and stride unused), else NULL
 };
 
 hipError_t launch_inverse(const InverseArgs &a, hipStream_t st);

@@ -7,7 +7,8 @@ addresses included), so no two blocks of a stripe are adjacent or in order.  Res
 bit-identical to the strided batch calls on the same inputs (those are checked against the
 oracle in test_gpu_parity.py) and, on a sample of stripes, to the C oracle directly.  The
 launch trace shows which form ran: the specialised kernels reading the blocks in place
-("(pointer table)") or the gather / strided / scatter form."""
+("(pointer table)": the register networks and the windowed large-m kernels with the phase-B
+kernel) or the gather / strided / scatter form."""
 import numpy as np
 import pytest
 
@@ -62,7 +63,10 @@ ENCODE = [
     (29, 8, 1296, 70, "lh_jit_encode(pointer table)"),
     (10, 6, 24, 130, "lh_jit_encode(pointer table)"),
     (64, 5, 4096, 9, "lh_jit_encode(pointer table)"),
-    (128, 32, 8192, 3, "lh_ptr_copy_kernel(gather)"),   # windowed large-m encode: gathered
+    (128, 32, 8192, 3, "lh_jit_encode_win(pointer table)"),   # windowed large-m encode
+    (40, 20, 4096, 6, "lh_jit_encode_win(pointer table)"),
+    (200, 56, 65536, 2, "lh_jit_encode_win(pointer table)"),
+    (40, 20, 1024, 5, "lh_ptr_copy_kernel(gather)"),    # large m, sub % 256 != 0: generic, gathered
     (200, 3, 64, 5, "lh_ptr_copy_kernel(gather)"),      # k > 128: generic kernels, gathered
     (10, 1, 100, 7, "lh_ptr_copy_kernel(gather)"),      # m = 1, any block size
     (1, 3, 40, 5, "lh_ptr_copy_kernel(gather)"),        # k = 1 copies
@@ -112,7 +116,10 @@ DECODE = [
     (29, 8, 1296, 70, "lh_jit_decode(pointer table)"),
     (10, 6, 24, 130, "lh_jit_decode(pointer table)"),
     (64, 3, 4096, 9, "lh_jit_decode_fused(pointer table)"),
-    (128, 32, 8192, 3, "lh_ptr_copy_kernel(gather)"),
+    (128, 32, 8192, 3, "lh_jit_decode_wide(pointer table)"),  # planner, phase A and phase B through the table
+    (40, 20, 4096, 6, "lh_jit_decode_wide(pointer table)"),
+    (200, 56, 65536, 3, "lh_jit_decode_wide(pointer table)"),
+    (40, 20, 1024, 5, "lh_ptr_copy_kernel(gather)"),
     (200, 3, 64, 5, "lh_ptr_copy_kernel(gather)"),
     (10, 1, 100, 7, "lh_ptr_copy_kernel(gather)"),
     (1, 3, 40, 5, "lh_ptr_copy_kernel(gather)"),
