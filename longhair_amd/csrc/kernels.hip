@@ -89,6 +89,11 @@ __device__ __forceinline__ void mul2(const Word<W> (&in)[8], Word<W> (&out)[8]) 
 
 // ------------------------------------------------------------------ generic apply
 // Grid: x covers (stripe, column chunk) lanes; y covers output tiles of LH_TILE_OUT rows.
+// The next input column's words are loaded before the current one is combined (one column
+// in flight per lane while the 64 masked XORs per output of this one issue).  When every lane
+// of a wave codes the same stripe (the encode's coefficients are the same for all stripes;
+// the decode's are per stripe, uniform when a stripe spans whole waves) the coefficient is a
+// scalar load and its bit masks are scalar work.
 template <int W>
 __global__ void __launch_bounds__(256) lh_apply_generic_kernel(lh::ApplyArgs a) {
     constexpr int TO = lh::kGenericTileOut;
@@ -107,6 +112,9 @@ __global__ void __launch_bounds__(256) lh_apply_generic_kernel(lh::ApplyArgs a) 
 
     const uint8_t *in = a.in + s * a.in_stride + p;
     const uint8_t *coef = a.coef + s * a.coef_stride + (long long)i0 * a.n_in;
+    const bool uni = a.coef_stride == 0 ||
+                     __all(s == (((long long)__builtin_amdgcn_readfirstlane((int)(s >> 32)) << 32) |
+                                 (unsigned)__builtin_amdgcn_readfirstlane((int)s)));
 
     Word<W> acc[TO][8];
 #pragma unroll
@@ -114,25 +122,40 @@ __global__ void __launch_bounds__(256) lh_apply_generic_kernel(lh::ApplyArgs a) 
 #pragma unroll
         for (int y = 0; y < 8; ++y) wzero(acc[i][y]);
 
-    for (int j = 0; j < a.n_in; ++j) {
-        Word<W> lad[8][8];  // lad[t] = B(2^t) * d
+    auto run = [&](auto uniform) {
+        constexpr bool U = decltype(uniform)::value;
+        Word<W> cur[8];
 #pragma unroll
-        for (int b = 0; b < 8; ++b) lad[0][b] = wload<W>(in + (long long)j * a.bytes + b * a.sub);
+        for (int b = 0; b < 8; ++b) cur[b] = wload<W>(in + b * a.sub);
+        for (int j = 0; j < a.n_in; ++j) {
+            Word<W> nxt[8];
+            const int jn = j + 1 < a.n_in ? j + 1 : j;  // (the last column reloads itself)
 #pragma unroll
-        for (int q = 1; q < 8; ++q) mul2<W>(lad[q - 1], lad[q]);
+            for (int b = 0; b < 8; ++b) nxt[b] = wload<W>(in + (long long)jn * a.bytes + b * a.sub);
+            Word<W> lad[8][8];  // lad[t] = B(2^t) * d
 #pragma unroll
-        for (int i = 0; i < TO; ++i) {
-            if (i < ni) {
-                const uint32_t e = coef[i * a.n_in + j];
+            for (int b = 0; b < 8; ++b) lad[0][b] = cur[b];
 #pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const uint32_t mask = 0u - ((e >> q) & 1u);
+            for (int q = 1; q < 8; ++q) mul2<W>(lad[q - 1], lad[q]);
 #pragma unroll
-                    for (int y = 0; y < 8; ++y) wxor_masked(acc[i][y], lad[q][y], mask);
+            for (int i = 0; i < TO; ++i) {
+                if (i < ni) {
+                    uint32_t e = coef[i * a.n_in + j];
+                    if (U) e = (uint32_t)__builtin_amdgcn_readfirstlane((int)e);
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const uint32_t mask = 0u - ((e >> q) & 1u);
+#pragma unroll
+                        for (int y = 0; y < 8; ++y) wxor_masked(acc[i][y], lad[q][y], mask);
+                    }
                 }
             }
+#pragma unroll
+            for (int b = 0; b < 8; ++b) cur[b] = nxt[b];
         }
-    }
+    };
+    if (uni) run(std::true_type{});
+    else run(std::false_type{});
     uint8_t *out = a.out + s * a.out_stride + (long long)i0 * a.bytes + p;
 #pragma unroll
     for (int i = 0; i < TO; ++i)
