@@ -687,6 +687,9 @@ struct lh_pb_ctx {
     uint8_t *sbase, *base;
     uint8_t *const *ptab;  // pointer-table batches: the stripe's k slot pointers, else NULL
     int coff;              // the workgroup's byte offset in every block (its 2 KiB chunk)
+    // pointer-table batches: lane r holds the block pointer of recovery row r (vp) and of
+    // output r (op), fetched once, so a DMA or a store never waits for a pointer load
+    unsigned long long vp, op;
     int dof0, dof1;
     __device__ __forceinline__ lh_pb_ctx(const lh::InverseArgs &a_, const uint8_t *pl)
         : a(a_), pv(pl, a_.k, a_.m, a_.e_max) {
@@ -703,6 +706,11 @@ struct lh_pb_ctx {
         ptab = a.ptrs ? a.ptrs + (blockIdx.x / cps) * a.k : nullptr;
         sbase = ptab ? nullptr : a.blocks + (blockIdx.x / cps) * a.stride + coff;  // wave-uniform
         base = sbase + lane * 4;
+        vp = op = 0;
+        if (ptab) {
+            if (rslot != 0xFFu) vp = (unsigned long long)ptab[rslot];
+            if (lane < e) op = (unsigned long long)ptab[pv.out_slot(lane)];
+        }
         dof0 = (lane >> 4) * sub + (lane & 15) * 16;
         dof1 = dof0 + 4 * sub;
     }
@@ -710,8 +718,9 @@ struct lh_pb_ctx {
     __device__ __forceinline__ void issue(unsigned long long rest, uint32_t *buf) const {
         for (int q = 0; q < g && rest; ++q) rest &= rest - 1;
         for (int j = g; rest && j < 8; j += nw) {
-            const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)rslot, __builtin_ctzll(rest));
-            const uint8_t *src = slot_base(slot);
+            const int r = __builtin_ctzll(rest);
+            const uint8_t *src = ptab ? lane_ptr(vp, r) + coff
+                                      : sbase + (long long)(uint32_t)__builtin_amdgcn_readlane((int)rslot, r) * a.bytes;
             uint8_t *dst = (uint8_t *)buf + j * 2048;
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + dof0),
                                              (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
@@ -720,9 +729,11 @@ struct lh_pb_ctx {
             for (int q = 0; q < nw && rest; ++q) rest &= rest - 1;
         }
     }
-    // The workgroup's chunk of slot `slot` (wave-uniform).
-    __device__ __forceinline__ const uint8_t *slot_base(uint32_t slot) const {
-        return ptab ? ptab[slot] + coff : sbase + (long long)slot * a.bytes;
+    // Lane r's pointer of a per-lane table, wave-uniform.
+    __device__ __forceinline__ static uint8_t *lane_ptr(unsigned long long t, int r) {
+        const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)t, r);
+        const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(t >> 32), r);
+        return (uint8_t *)(((unsigned long long)hi << 32) | lo);
     }
     __device__ __forceinline__ static unsigned long long skip_tile(unsigned long long rest) {
         for (int j = 0; rest && j < 8; ++j) rest &= rest - 1;
@@ -771,7 +782,7 @@ struct lh_pb_ctx {
         }
     }
     __device__ __forceinline__ void store(int out, const uint32_t (&acc)[8]) const {
-        uint8_t *dst = (uint8_t *)slot_base(pv.out_slot(out)) + lane * 4;
+        uint8_t *dst = ptab ? lane_ptr(op, out) + coff + lane * 4 : base + (long long)pv.out_slot(out) * a.bytes;
 #pragma unroll
         for (int y = 0; y < 8; ++y) __builtin_nontemporal_store(acc[y], (uint32_t *)(dst + (long long)y * sub));
     }
