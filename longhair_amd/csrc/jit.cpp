@@ -215,11 +215,15 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
     // block pointers ride in VGPR lanes (ptl: k slots / columns, otl: m recovery blocks) and
     // lh_pp reads one as a wave-uniform pointer; coff = the workgroup's byte offset in every
     // block, loff = the lane's.
+    // (Decode: cpl instead, lane i of cpl[i / 64] = the block pointer of stream column i --
+    // original i < k or recovery row i - k -- through the stripe's slot map, the zero page
+    // for an absent one: resolved once per workgroup, so a column's base is two v_readlane
+    // with constant lane selects.)
     if (c.ptr)
-        os << "__device__ __forceinline__ void lh_wg" << g << "(const unsigned long long (&ptl)[LH_NP], "
-           << (elim ? "const unsigned char *__restrict__ zb, const unsigned int (&slv)[LH_NQ], "
+        os << "__device__ __forceinline__ void lh_wg" << g << "("
+           << (elim ? "const unsigned long long (&cpl)[LH_NQ], const unsigned int (&slv)[LH_NQ], "
                       "const unsigned char *__restrict__ pl"
-                    : "const unsigned long long (&otl)[LH_NPO]")
+                    : "const unsigned long long (&ptl)[LH_NP], const unsigned long long (&otl)[LH_NPO]")
            << ", const int coff, const int loff) {\n";
     else
     os << "__device__ __forceinline__ void lh_wg" << g << "(" << (elim ? "" : "const ") << "unsigned char *__restrict__ base, "
@@ -236,7 +240,7 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
     }
     auto dcol = [&](int x) {  // uniform base of column x for the DMA (stripe + chunk, or zero page)
         std::ostringstream e;
-        if (c.ptr && elim) e << "lh_pslot(slv, ptl, " << x << ", coff, zb)";
+        if (c.ptr && elim) e << "(lh_pp(cpl, " << x << ") + coff)";
         else if (c.ptr) e << "(lh_pp(ptl, " << x << ") + coff)";
         else if (elim) e << "lh_slot(slv, " << x << ", sb, zb)";
         else e << "(sb + " << (long long)x * c.bytes << "LL)";
@@ -328,7 +332,7 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
             os << "  {\n    const unsigned int s = (unsigned int)__builtin_amdgcn_readlane((int)slv[" << (k + r) / 64
                << "], " << (k + r) % 64 << ");\n    if (s != 0xFFu) {\n";
             if (c.ptr)
-                os << "      unsigned char *rp = lh_pp(ptl, (int)s) + loff;\n";
+                os << "      unsigned char *rp = lh_pp(cpl, " << k + r << ") + loff;\n";
             else
                 os << "      unsigned char *rp = base + (long long)s * " << c.bytes << ";\n";
             for (int y = 0; y < 8; ++y)
@@ -450,11 +454,6 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
            << "  asm volatile(LH_INV_JUMPG8_ASM : LH_INV_JUMPG8_OUTS(acc) : LH_INV_JUMPG_INS(tl, th, t), [r] \"n\"(R),\n"
            << "               [hi] \"s\"(hi) : \"s92\", \"s93\", \"s94\", \"s95\", \"s97\", \"scc\");\n}\n";
     }
-    if (c.ptr)
-        os << "__device__ __forceinline__ const unsigned char *lh_pslot(const unsigned int (&slv)[LH_NQ],\n"
-           << "    const unsigned long long (&ptl)[LH_NP], const int i, const int coff, const unsigned char *zb) {\n"
-           << "  const int s = __builtin_amdgcn_readlane((int)slv[i / 64], i % 64);\n"
-           << "  return s == 0xFF ? zb : lh_pp(ptl, s) + coff;\n}\n";
     for (int g = 0; g < NG; ++g) emit_win_group(os, c, G, g);
     if (c.ptr) {
         // blocks: the pointer table, k slot pointers per stripe (row stride `stride` bytes)
@@ -473,12 +472,13 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
            << "    const int i = q * 64 + lane;\n"
            << "    slv[q] = i < " << km << " ? (unsigned int)pl[" << 16 + e_max << " + i] : 0xFFu;\n"
            << "  }\n"
-           << "  unsigned long long ptl[LH_NP];\n"
-           << "  lh_ptab_lanes(ptl, (const unsigned long long *)(blocks + stripe * stride), " << c.k << ");\n"
-           << "  const int coff = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << ";\n"
-           << "  const unsigned char *zb = zero_page + coff;\n";
+           << "  const unsigned long long *tab = (const unsigned long long *)(blocks + stripe * stride);\n"
+           << "  unsigned long long cpl[LH_NQ];\n"
+           << "#pragma unroll\n  for (int q = 0; q < LH_NQ; ++q)\n"
+           << "    cpl[q] = slv[q] == 0xFFu ? (unsigned long long)zero_page : tab[slv[q]];\n"
+           << "  const int coff = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << ";\n";
         for (int g = 0; g < NG; ++g)
-            os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << "(ptl, zb, slv, pl, coff, coff + lane * "
+            os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << "(cpl, slv, pl, coff, coff + lane * "
                << c.W << ");\n";
         os << "}\n";
         return;

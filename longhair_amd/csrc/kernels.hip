@@ -684,14 +684,15 @@ struct lh_pb_ctx {
     lh::PlanView pv;
     uint32_t rslot;
     unsigned long long used;
-    uint8_t *sbase, *base;
+    uint8_t *sbase;        // the stripe's first block (strided batches)
     uint8_t *const *ptab;  // pointer-table batches: the stripe's k slot pointers, else NULL
-    int coff;              // the workgroup's byte offset in every block (its 2 KiB chunk)
+    int c0, nch;           // this workgroup's 2 KiB chunks: c0 .. c0 + nch - 1 of every block
     // pointer-table batches: lane r holds the block pointer of recovery row r (vp) and of
     // output r (op), fetched once, so a DMA or a store never waits for a pointer load
     unsigned long long vp, op;
     int dof0, dof1;
-    __device__ __forceinline__ lh_pb_ctx(const lh::InverseArgs &a_, const uint8_t *pl)
+    __device__ __forceinline__ lh_pb_ctx(const lh::InverseArgs &a_, const uint8_t *pl, long long stripe, int c0_,
+                                         int nch_)
         : a(a_), pv(pl, a_.k, a_.m, a_.e_max) {
         nw = (int)(blockDim.x >> 6);
         g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -701,11 +702,10 @@ struct lh_pb_ctx {
         sub = a.bytes >> 3;
         rslot = lane < m ? (uint32_t)pv.rec_slot(lane) : 0xFFu;
         used = __ballot(rslot != 0xFFu);
-        const int cps = a.bytes >> 11;
-        coff = (int)(blockIdx.x % cps) * 256;
-        ptab = a.ptrs ? a.ptrs + (blockIdx.x / cps) * a.k : nullptr;
-        sbase = ptab ? nullptr : a.blocks + (blockIdx.x / cps) * a.stride + coff;  // wave-uniform
-        base = sbase + lane * 4;
+        c0 = c0_;
+        nch = nch_;
+        ptab = a.ptrs ? a.ptrs + stripe * a.k : nullptr;
+        sbase = ptab ? nullptr : a.blocks + stripe * a.stride;  // wave-uniform
         vp = op = 0;
         if (ptab) {
             if (rslot != 0xFFu) vp = (unsigned long long)ptab[rslot];
@@ -714,13 +714,21 @@ struct lh_pb_ctx {
         dof0 = (lane >> 4) * sub + (lane & 15) * 16;
         dof1 = dof0 + 4 * sub;
     }
-    // DMA of the tile starting at `rest` into `buf`: this wave moves tile positions g, g + nw, ...
-    __device__ __forceinline__ void issue(unsigned long long rest, uint32_t *buf) const {
+    // Lane r's pointer of a per-lane table, wave-uniform.
+    __device__ __forceinline__ static uint8_t *lane_ptr(unsigned long long t, int r) {
+        const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)t, r);
+        const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(t >> 32), r);
+        return (uint8_t *)(((unsigned long long)hi << 32) | lo);
+    }
+    // DMA of the tile starting at `rest` of chunk `ch` into `buf`: this wave moves tile
+    // positions g, g + nw, ...
+    __device__ __forceinline__ void issue(int ch, unsigned long long rest, uint32_t *buf) const {
         for (int q = 0; q < g && rest; ++q) rest &= rest - 1;
         for (int j = g; rest && j < 8; j += nw) {
             const int r = __builtin_ctzll(rest);
-            const uint8_t *src = ptab ? lane_ptr(vp, r) + coff
-                                      : sbase + (long long)(uint32_t)__builtin_amdgcn_readlane((int)rslot, r) * a.bytes;
+            const uint8_t *src = ptab ? lane_ptr(vp, r) + ch * 256
+                                      : sbase + (long long)(uint32_t)__builtin_amdgcn_readlane((int)rslot, r) * a.bytes +
+                                            ch * 256;
             uint8_t *dst = (uint8_t *)buf + j * 2048;
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + dof0),
                                              (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
@@ -728,12 +736,6 @@ struct lh_pb_ctx {
                                              (__attribute__((address_space(3))) void *)(dst + 1024), 16, 0, 0);
             for (int q = 0; q < nw && rest; ++q) rest &= rest - 1;
         }
-    }
-    // Lane r's pointer of a per-lane table, wave-uniform.
-    __device__ __forceinline__ static uint8_t *lane_ptr(unsigned long long t, int r) {
-        const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)t, r);
-        const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(t >> 32), r);
-        return (uint8_t *)(((unsigned long long)hi << 32) | lo);
     }
     __device__ __forceinline__ static unsigned long long skip_tile(unsigned long long rest) {
         for (int j = 0; rest && j < 8; ++j) rest &= rest - 1;
@@ -746,27 +748,35 @@ struct lh_pb_ctx {
         __builtin_amdgcn_s_waitcnt(0xF | (7 << 4) | (3 << 14));
         __builtin_amdgcn_s_barrier();
     }
-    // The tile loop: compute(rest, buf) multiplies the rows of the tile starting at `rest`.
-    template <class F>
-    __device__ __forceinline__ void tiles(uint32_t *lvA, uint32_t *lvB, F &&compute) const {
+    // The tile loop over the workgroup's chunks: compute(rest, buf) multiplies the rows of the
+    // tile starting at `rest`; done(ch) runs after the last tile of chunk ch (the outputs).
+    // The pipeline runs across chunks: the DMA of a chunk's first tile is issued while the
+    // previous chunk's last tile is computed.  Before done(ch) every wave has waited for its
+    // DMAs of chunk ch and passed a barrier after them, so all of the chunk's V rows have been
+    // read and its recovery slots may be overwritten; the DMA in flight reads the next chunk's
+    // bytes, which no store of chunk ch touches.
+    template <class F, class D>
+    __device__ __forceinline__ void tiles(uint32_t *lvA, uint32_t *lvB, F &&compute, D &&done) const {
+        int ch = c0;
         unsigned long long todo = used;
-        issue(todo, lvA);
+        issue(ch, todo, lvA);
+        bool inA = true;
         while (true) {  // workgroup-uniform
-            publish();  // tile in A; every wave is done with B
+            publish();  // tile in its buffer; every wave is done with the other one
             unsigned long long next = skip_tile(todo);
-            if (next) issue(next, lvB);
-            compute(todo, lvA);
+            int nch_ = ch;
+            if (!next && ch + 1 < c0 + nch) {
+                nch_ = ch + 1;
+                next = used;
+            }
+            if (next) issue(nch_, next, inA ? lvB : lvA);
+            compute(todo, inA ? lvA : lvB);
+            if (nch_ != ch || !next) done(ch);
+            if (!next) break;
             todo = next;
-            if (!todo) break;
-            publish();  // tile in B; every wave is done with A
-            next = skip_tile(todo);
-            if (next) issue(next, lvA);
-            compute(todo, lvB);
-            todo = next;
-            if (!todo) break;
+            ch = nch_;
+            inA = !inA;
         }
-        // Every wave waited for its DMAs before the last barrier: every V row has been read,
-        // so the recovery slots may be overwritten.
     }
     // Row j of a tile: the 16-entry tables of V_r's sub-blocks 0..3 and 4..7.
     __device__ __forceinline__ void tables(const uint32_t *buf, int j, uint32_t (&tl)[16], uint32_t (&th)[16]) const {
@@ -781,21 +791,34 @@ struct lh_pb_ctx {
             th[q] = pre ? (th[pre] ^ v[4 + low]) : v[4 + low];
         }
     }
-    __device__ __forceinline__ void store(int out, const uint32_t (&acc)[8]) const {
-        uint8_t *dst = ptab ? lane_ptr(op, out) + coff + lane * 4 : base + (long long)pv.out_slot(out) * a.bytes;
+    __device__ __forceinline__ void store(int ch, int out, const uint32_t (&acc)[8]) const {
+        uint8_t *dst = (ptab ? lane_ptr(op, out) : sbase + (long long)pv.out_slot(out) * a.bytes) + ch * 256 + lane * 4;
 #pragma unroll
         for (int y = 0; y < 8; ++y) __builtin_nontemporal_store(acc[y], (uint32_t *)(dst + (long long)y * sub));
+    }
+};
+
+// The workgroup's stripe and chunks: a.chunks_per_wg consecutive 2 KiB chunks of one stripe.
+struct lh_pb_span {
+    long long stripe;
+    int c0, nch;
+    __device__ __forceinline__ explicit lh_pb_span(const lh::InverseArgs &a) {
+        const int cps = a.bytes >> 11, cpw = a.chunks_per_wg > 0 ? a.chunks_per_wg : 1;
+        const int wps = (cps + cpw - 1) / cpw;  // workgroups per stripe
+        stripe = blockIdx.x / wps;
+        c0 = (int)(blockIdx.x % wps) * cpw;
+        nch = cps - c0 < cpw ? cps - c0 : cpw;
     }
 };
 
 // Fallback form: outputs g, g + nw, ... (at most 8) per wave, the in-asm table.
 __device__ __forceinline__ void lh_inverse_dma_body(const lh::InverseArgs &a, uint32_t *__restrict__ lvA,
                                                     uint32_t *__restrict__ lvB) {
-    const long long stripe = blockIdx.x / (a.bytes >> 11);
-    if (stripe >= a.stripes) return;  // workgroup-uniform
-    const uint8_t *pl = a.plan + stripe * a.plan_stride;
+    const lh_pb_span sp(a);
+    if (sp.stripe >= a.stripes) return;  // workgroup-uniform
+    const uint8_t *pl = a.plan + sp.stripe * a.plan_stride;
     if (pl[0] == 0) return;  // workgroup-uniform
-    const lh_pb_ctx C(a, pl);
+    const lh_pb_ctx C(a, pl, sp.stripe, sp.c0, sp.nch);
     const int nout = C.g < C.e ? (C.e - C.g + C.nw - 1) / C.nw : 0;
     uint32_t cpk0 = 0, cpk1 = 0;  // lane r: this wave's coefficients for recovery row r
     if (C.rslot != 0xFFu) {
@@ -823,10 +846,14 @@ __device__ __forceinline__ void lh_inverse_dma_body(const lh::InverseArgs &a, ui
             lh_mul_jump_idx8((uint32_t)__builtin_amdgcn_readlane((int)cpk0, r),
                              (uint32_t)__builtin_amdgcn_readlane((int)cpk1, r), acc, tl, th);
         }
-    });
+    }, [&](int ch) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-        if (i < nout) C.store(C.g + i * C.nw, acc[i]);
+        for (int i = 0; i < 8; ++i) {
+            if (i < nout) C.store(ch, C.g + i * C.nw, acc[i]);
+#pragma unroll
+            for (int y = 0; y < 8; ++y) acc[i][y] = 0;
+        }
+    });
 }
 
 // ---- the default: the 256 bodies once per code object, in the never-launched kernel below
@@ -884,11 +911,11 @@ __device__ __forceinline__ bool lh_mul_jump_g(uint32_t (&acc)[8][8], const uint3
 // wave-uniform) so no slot jumps for an unused output.
 __device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uint32_t *__restrict__ lvA,
                                                    uint32_t *__restrict__ lvB, uint32_t tlo, uint32_t thi) {
-    const long long stripe = blockIdx.x / (a.bytes >> 11);
-    if (stripe >= a.stripes) return;  // workgroup-uniform
-    const uint8_t *pl = a.plan + stripe * a.plan_stride;
+    const lh_pb_span sp(a);
+    if (sp.stripe >= a.stripes) return;  // workgroup-uniform
+    const uint8_t *pl = a.plan + sp.stripe * a.plan_stride;
     if (pl[0] == 0) return;  // workgroup-uniform
-    const lh_pb_ctx C(a, pl);
+    const lh_pb_ctx C(a, pl, sp.stripe, sp.c0, sp.nch);
     const bool pack = a.pack != 0;
     int nout = pack ? C.e - 8 * C.g : (C.g < C.e ? (C.e - C.g + C.nw - 1) / C.nw : 0);
     nout = nout < 0 ? 0 : (nout > 8 ? 8 : nout);
@@ -918,14 +945,17 @@ __device__ __forceinline__ void lh_inverse_gt_body(const lh::InverseArgs &a, uin
                     if (ok) ok = lh_mul_jump_g<N>(acc, tl, th, t, __builtin_ctzll(rest), tlo, thi);
                 }
             }
+        }, [&](int ch) {
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                if (!ok)
+#pragma unroll
+                    for (int y = 0; y < 8; ++y) acc[i][y] = 0xDEADBEEFu;
+                C.store(ch, out_of(i), acc[i]);
+#pragma unroll
+                for (int y = 0; y < 8; ++y) acc[i][y] = 0;
+            }
         });
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-            if (!ok)
-#pragma unroll
-                for (int y = 0; y < 8; ++y) acc[i][y] = 0xDEADBEEFu;
-            C.store(out_of(i), acc[i]);
-        }
     };
     switch (nout) {  // wave-uniform
         case 0: run(std::integral_constant<int, 0>{}); break;
@@ -1060,7 +1090,15 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     const char *fb = std::getenv("LONGHAIR_AMD_INV_FALLBACK");
     g.pack = pk ? (std::atoi(pk) ? 1 : 0) : (a.e_max <= 32 ? 1 : 0);
     g.jump_fallback = fb && std::atoi(fb) ? 1 : 0;
-    hipLaunchKernelGGL(lh_inverse_gt_kernel, dim3((unsigned)blocks), dim3(64u * (unsigned)((a.e_max + 7) / 8)), 0, st, g);
+    // Chunks per workgroup (LONGHAIR_AMD_INV_CHUNKS, default 1): a workgroup runs its tile
+    // pipeline across that many consecutive 2 KiB chunks of its stripe.
+    const int cps = a.bytes / 2048;
+    int cpw = 1;
+    if (const char *c = std::getenv("LONGHAIR_AMD_INV_CHUNKS")) cpw = std::atoi(c);
+    cpw = cpw < 1 ? 1 : (cpw > cps ? cps : cpw);
+    g.chunks_per_wg = cpw;
+    const long long wgs = (long long)a.stripes * ((cps + cpw - 1) / cpw);
+    hipLaunchKernelGGL(lh_inverse_gt_kernel, dim3((unsigned)wgs), dim3(64u * (unsigned)((a.e_max + 7) / 8)), 0, st, g);
     note_launch(g.jump_fallback ? "lh_inverse_gt_kernel(fallback)" : "lh_inverse_gt_kernel");
     return hipGetLastError();
 }

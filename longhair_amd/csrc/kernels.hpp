@@ -111,6 +111,7 @@ struct InverseArgs {
     int k, m, e_max, bytes, stripes;
     int pack;                     // lh_inverse_gt_kernel: 8 consecutive outputs per wave
     int jump_fallback;            // lh_inverse_gt_kernel: take the in-asm table (tests)
+    int chunks_per_wg;            // lh_inverse_gt_kernel: consecutive 2 KiB chunks per workgroup (>= 1)
     uint8_t *const *ptrs;         // pointer-table batches: slot j of stripe s at ptrs[s*k + j]
                                   // (blocks and stride unused), else NULL
 };

@@ -25,7 +25,7 @@ VARIANTS = [
 KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID", "LONGHAIR_AMD_NO_FUSED_PLAN",
          "LONGHAIR_AMD_PLAN_THREADS",
          "LONGHAIR_AMD_WIN_ROWS", "LONGHAIR_AMD_WIN_PF", "LONGHAIR_AMD_WIN_LDS",
-         "LONGHAIR_AMD_WIN_SPLIT", "LONGHAIR_AMD_INV_PACK", "LONGHAIR_AMD_JIT_AL", "LONGHAIR_AMD_JIT_ALS"]
+         "LONGHAIR_AMD_WIN_SPLIT", "LONGHAIR_AMD_INV_PACK", "LONGHAIR_AMD_INV_CHUNKS", "LONGHAIR_AMD_JIT_AL", "LONGHAIR_AMD_JIT_ALS"]
 # Large-m (windowed) variants: rows per wave and columns in flight.
 VARIANTS_WIN = [
     ("base", {}),
