@@ -1090,10 +1090,13 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     const char *fb = std::getenv("LONGHAIR_AMD_INV_FALLBACK");
     g.pack = pk ? (std::atoi(pk) ? 1 : 0) : (a.e_max <= 32 ? 1 : 0);
     g.jump_fallback = fb && std::atoi(fb) ? 1 : 0;
-    // Chunks per workgroup (LONGHAIR_AMD_INV_CHUNKS, default 1): a workgroup runs its tile
-    // pipeline across that many consecutive 2 KiB chunks of its stripe.
+    // Chunks per workgroup (LONGHAIR_AMD_INV_CHUNKS, default 2): a workgroup runs its tile
+    // pipeline across that many consecutive 2 KiB chunks of its stripe, so the pipeline's
+    // start (plan, jump targets, first tile's DMA) is paid once per pair of chunks
+    // (profiles/r4k_tune_*_inv_chunks.txt: k200/m56 decode 0.665 -> 0.617 ms with 2, 0.635 with
+    // 4; k128/m32 3.634 ms with 1, 2 or 4).
     const int cps = a.bytes / 2048;
-    int cpw = 1;
+    int cpw = 2;
     if (const char *c = std::getenv("LONGHAIR_AMD_INV_CHUNKS")) cpw = std::atoi(c);
     cpw = cpw < 1 ? 1 : (cpw > cps ? cps : cpw);
     g.chunks_per_wg = cpw;

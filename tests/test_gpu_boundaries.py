@@ -166,6 +166,16 @@ def test_phase_b_variant(lh, oracle, monkeypatch, env, m, kernel):
     assert dec == ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", kernel], dec
 
 
+@pytest.mark.parametrize("chunks", ["1", "2", "3"])
+def test_phase_b_chunks_per_workgroup(lh, oracle, monkeypatch, chunks):
+    """Phase-B workgroups over consecutive 2 KiB chunks of a stripe (LONGHAIR_AMD_INV_CHUNKS,
+    the tile pipeline carried across chunks): 6144-byte blocks = 3 chunks, so 2 per
+    workgroup leaves a one-chunk remainder; against the oracle."""
+    monkeypatch.setenv("LONGHAIR_AMD_INV_CHUNKS", chunks)
+    enc, dec = roundtrip(lh, oracle, 40, 20, 6144, 7, seed=int(chunks) * 7)
+    assert dec == ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_gt_kernel"], dec
+
+
 def _sweep_ms(k):
     return sorted({m for m in list(range(1, 9)) + [16, 32, 64, 256 - k] if 1 <= m and k + m <= 256})
 

@@ -16,7 +16,7 @@ DEFAULT = [(29, 4, 1296), (128, 32, 8192), (200, 56, 65536)]
 TESTS = [(29, 2, 1296), (29, 3, 1296), (29, 8, 1296), (4, 2, 16), (10, 6, 8), (17, 6, 520), (64, 5, 4096),
          (3, 250, 24), (2, 2, 8), (29, 4, 1304), (9, 7, 72), (29, 2, 16), (10, 8, 24),
          (128, 32, 1024), (5, 3, 8), (100, 16, 2048), (40, 20, 4096), (250, 6, 2048), (10, 6, 24), (3, 2, 8),
-         (64, 4, 4096), (64, 3, 4096), (64, 2, 8192)]
+         (64, 4, 4096), (64, 3, 4096), (64, 2, 8192), (40, 20, 6144)]
 # Shapes whose pointer-table modules (cauchy_256_*_batch_ptrs, LH_PTR) the GPU tests run
 # (tests/test_gpu_ptrs.py; the north-star shape is benchmarked through them too).
 PTR_SHAPES = [(29, 4, 1296), (29, 8, 1296), (10, 6, 24), (64, 5, 4096), (64, 3, 4096), (40, 20, 4096),
