@@ -613,7 +613,9 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
 static constexpr long long kPtrChunkBytes = 256ll << 20;
 
 static int gather_chunk(Device *d, hipStream_t st, long long per_stripe, int stripes, uint8_t **buf, int *chunk) {
-    const long long c = std::max(1ll, std::min((long long)stripes, kPtrChunkBytes / std::max(1ll, per_stripe)));
+    long long cap = kPtrChunkBytes;
+    if (const char *e = std::getenv("LONGHAIR_AMD_PTR_CHUNK_BYTES")) cap = std::max(1ll, std::atoll(e));  // (tests)
+    const long long c = std::max(1ll, std::min((long long)stripes, cap / std::max(1ll, per_stripe)));
     std::lock_guard<std::mutex> g(d->mu);
     Workspace &w = d->ws[st];
     if ((size_t)(c * per_stripe) > w.gather.size && capturing(st))

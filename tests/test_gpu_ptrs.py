@@ -204,3 +204,29 @@ def test_decode_batch_ptrs_roundtrip_baseline_shape(lh):
     assert torch.equal(rows[:, k - 4:].long(), lost)
     got = _gather(rpool, rplace)
     assert torch.equal(got, torch.gather(data, 1, lost.unsqueeze(2).expand(stripes, 4, nbytes)))
+
+
+@pytest.mark.parametrize("k,m,nbytes", [(200, 3, 64), (10, 1, 100), (40, 20, 1024)])
+def test_ptrs_gather_in_chunks(lh, oracle, monkeypatch, k, m, nbytes):
+    """The gather / strided / scatter form over several workspace chunks (the chunk capped by
+    LONGHAIR_AMD_PTR_CHUNK_BYTES at 3 stripes for the encode, 3-4 for the decode; 11
+    stripes): encode and decode bit-identical to the strided calls."""
+    import torch
+    stripes = 11
+    monkeypatch.setenv("LONGHAIR_AMD_PTR_CHUNK_BYTES", str(3 * (k + m) * nbytes + 3 * k))
+    data, blocks, rows = _received(lh, k, m, nbytes, stripes, seed=k + m)
+    want = lh.encode_batch(data, m)
+    dpool, dptr, _ = _scatter(data, seed=5)
+    rpool, rptr, rplace = _scatter(torch.zeros((stripes, m, nbytes), dtype=torch.uint8, device="cuda"), seed=6)
+    lh.encode_batch_ptrs(k, m, nbytes, dptr, rptr)
+    torch.cuda.synchronize()
+    assert lh.last_launch()[0] == "lh_ptr_copy_kernel(gather)", lh.last_launch()
+    assert torch.equal(_gather(rpool, rplace), want)
+    sb, sr = torch.from_numpy(blocks).cuda(), torch.from_numpy(rows).cuda()
+    sstat = lh.decode_batch(sb, sr, m)
+    pool, ptrs, place = _scatter(torch.from_numpy(blocks).cuda(), seed=7)
+    pr = torch.from_numpy(rows).cuda()
+    pstat = lh.decode_batch_ptrs(k, m, nbytes, ptrs, pr)
+    torch.cuda.synchronize()
+    assert torch.equal(pstat, sstat) and torch.equal(pr, sr)
+    assert torch.equal(_gather(pool, place), sb)
