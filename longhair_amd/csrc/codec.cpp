@@ -644,7 +644,7 @@ static int ptr_copy(uint8_t *const *ptrs, int n, int ncopy, uint8_t *chunk, long
 }
 
 static int encode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *const *data_ptrs, uint8_t *const *rec_ptrs,
-                             hipStream_t st) {
+                             hipStream_t st, bool allow_compile = true) {
     if (k < 1 || m < 1 || bytes <= 0 || stripes < 0 || k > 256 || m > 256)
         return fail(kInvalid, "invalid k, m, block_bytes or stripes");
     if (stripes == 0) return kOk;
@@ -655,7 +655,7 @@ static int encode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
     if (jit_ptr_config_for(k, m, bytes, false, &cfg)) {
         std::string err;
         bool hard = false;
-        const JitKernels *jk = jit_lookup(d, cfg, true, &err, &hard);
+        const JitKernels *jk = jit_lookup(d, cfg, allow_compile, &err, &hard);
         if (jk) {
             const long long blocks = jit_blocks(cfg, stripes);
             if (blocks > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
@@ -671,7 +671,7 @@ static int encode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
     if (jit_win_ptr_config_for(k, m, bytes, &cfg)) {
         std::string err;
         bool hard = false;
-        const JitKernels *jk = jit_lookup(d, cfg, true, &err, &hard);
+        const JitKernels *jk = jit_lookup(d, cfg, allow_compile, &err, &hard);
         if (jk && jk->encode_win) {
             const long long blocks = (long long)stripes * (cfg.sub / (64 * cfg.W));
             if (blocks > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
@@ -698,7 +698,7 @@ static int encode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
         if (int rc = ptr_copy(data_ptrs + (long long)s0 * k, k, k, dat, (long long)k * bytes, bytes, n, false, nullptr,
                               0, st))
             return rc;
-        const int rc = encode_batch(k, m, bytes, n, dat, (long long)k * bytes, rec, (long long)m * bytes, st, true);
+        const int rc = encode_batch(k, m, bytes, n, dat, (long long)k * bytes, rec, (long long)m * bytes, st, allow_compile);
         if (rc != kOk && !(rc == kInvalid && invalid)) return rc;
         if (int rc = ptr_copy(rec_ptrs + (long long)s0 * m, m, invalid ? 1 : m, rec, (long long)m * bytes, bytes, n,
                               true, nullptr, 0, st))
@@ -708,7 +708,7 @@ static int encode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
 }
 
 static int decode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *const *block_ptrs, uint8_t *d_rows,
-                             int8_t *d_status, hipStream_t st) {
+                             int8_t *d_status, hipStream_t st, bool allow_compile = true) {
     if (k < 1 || m < 1 || bytes <= 0 || stripes < 0 || k > 256 || m > 256)
         return fail(kInvalid, "invalid k, m, block_bytes or stripes");
     if (stripes == 0) return kOk;
@@ -721,7 +721,7 @@ static int decode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
     if (k > 1 && m > 1 && jit_ptr_config_for(k, m, bytes, true, &cfg)) {
         std::string err;
         bool hard = false;
-        const JitKernels *jk = jit_lookup(d, cfg, true, &err, &hard);
+        const JitKernels *jk = jit_lookup(d, cfg, allow_compile, &err, &hard);
         if (hard) return fail(kHipError, err);
         if (jk) {
             const uint8_t *zero = nullptr;
@@ -773,7 +773,7 @@ static int decode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
     if (k > 1 && m > 1 && !jit_config_for(k, m, bytes, true, &cfg) && jit_win_ptr_config_for(k, m, bytes, &cfg, true)) {
         std::string err;
         bool hard = false;
-        const JitKernels *wk = jit_lookup(d, cfg, true, &err, &hard);
+        const JitKernels *wk = jit_lookup(d, cfg, allow_compile, &err, &hard);
         if (hard) return fail(kHipError, err);
         if (wk && wk->decode_wide) {
             const int e_max = k < m ? k : m;
@@ -837,7 +837,7 @@ static int decode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
         if (int rc = ptr_copy(tab, k, k, blk, (long long)k * bytes, bytes, n, false, nullptr, 0, st)) return rc;
         if (by_row) LH_HIP(hipMemcpyAsync(rows0, d_rows + (long long)s0 * k, (size_t)n * k, hipMemcpyDeviceToDevice, st));
         if (int rc = decode_batch(k, m, bytes, n, blk, (long long)k * bytes, d_rows + (long long)s0 * k,
-                                  d_status ? d_status + s0 : nullptr, st, true))
+                                  d_status ? d_status + s0 : nullptr, st, allow_compile))
             return rc;
         if (int rc = ptr_copy(tab, k, k, blk, (long long)k * bytes, bytes, n, true, by_row ? rows0 : nullptr, k, st))
             return rc;
@@ -1155,9 +1155,24 @@ static int dropin_encode(int k, int m, const unsigned char *data_ptrs[], void *r
     Device::DropinSlot *sl = nullptr;
     if (int rc = dropin_slot(d, &g, &sl)) return rc;
     const size_t in_n = (size_t)k * bytes, out_n = (size_t)m * bytes;
-    LH_HIP(sl->stage.reserve(in_n + out_n));
-    LH_HIP(sl->host_stage.reserve(in_n + out_n));
+    const size_t need = std::max(in_n + out_n, (size_t)(k + m) * 8);  // (the pointer table, all-device calls)
+    LH_HIP(sl->stage.reserve(need));
+    LH_HIP(sl->host_stage.reserve(need));
     hipStream_t st = sl->stream;
+    if (where == 0) {
+        // Every block in device memory: the pointer-table form reads them where they lie and
+        // writes the recovery blocks in place -- one host-to-device copy of k + m pointers
+        // instead of k + 1 block copies.
+        uint64_t *ht = (uint64_t *)sl->host_stage.ptr;
+        for (int x = 0; x < k; ++x) ht[x] = (uint64_t)(uintptr_t)data_ptrs[x];
+        for (int r = 0; r < m; ++r) ht[k + r] = (uint64_t)(uintptr_t)((uint8_t *)recovery + (size_t)r * bytes);
+        const size_t tn = (size_t)(k + m) * 8;
+        LH_HIP(hipMemcpyAsync(sl->stage.ptr, ht, tn, hipMemcpyHostToDevice, st));
+        uint8_t *const *dt = (uint8_t *const *)sl->stage.ptr;
+        const int rc = encode_batch_ptrs(k, m, bytes, 1, dt, dt + k, st, false);
+        LH_HIP(hipStreamSynchronize(st));
+        return rc;
+    }
     uint8_t *din = sl->stage.ptr, *dout = sl->stage.ptr + in_n;
     if (where == 1) {  // gather into pinned staging, one host-to-device copy
         for (int x = 0; x < k; ++x) std::memcpy(sl->host_stage.ptr + (size_t)x * bytes, data_ptrs[x], bytes);
@@ -1213,10 +1228,30 @@ static int dropin_decode(int k, int m, Block *blocks, int bytes) {
     // Device and host staging share one layout: [k blocks][256 rows][16 status], so each
     // direction is a single copy for host pointers.
     const size_t in_n = (size_t)k * bytes, tot = in_n + 256 + 16;
-    LH_HIP(sl->stage.reserve(tot));
-    LH_HIP(sl->host_stage.reserve(tot));
+    const size_t need = std::max(tot, (size_t)k * 8 + 256 + 16);  // (the pointer table, all-device calls)
+    LH_HIP(sl->stage.reserve(need));
+    LH_HIP(sl->host_stage.reserve(need));
     hipStream_t st = sl->stream;
     uint8_t *hs = sl->host_stage.ptr, *ds = sl->stage.ptr;
+    if (where == 0) {
+        // Every block in device memory: the pointer-table form decodes them in place -- one
+        // copy of [k pointers][rows] in, one of [rows][status] out.
+        uint64_t *ht = (uint64_t *)hs;
+        for (int i = 0; i < k; ++i) ht[i] = (uint64_t)(uintptr_t)blocks[i].data;
+        uint8_t *hr = hs + (size_t)k * 8, *dr = ds + (size_t)k * 8;
+        for (int i = 0; i < k; ++i) hr[i] = blocks[i].row;
+        LH_HIP(hipMemcpyAsync(ds, hs, (size_t)k * 8 + k, hipMemcpyHostToDevice, st));
+        const int rc = decode_batch_ptrs(k, m, bytes, 1, (uint8_t *const *)ds, dr, (int8_t *)(dr + 256), st, false);
+        if (rc != kOk) {
+            (void)hipStreamSynchronize(st);
+            return rc;
+        }
+        LH_HIP(hipMemcpyAsync(hr, dr, 256 + 16, hipMemcpyDeviceToHost, st));
+        LH_HIP(hipStreamSynchronize(st));
+        if ((int8_t)hr[256] != 0) return fail(kInvalid, "invalid or duplicated block rows");
+        for (int i = 0; i < k; ++i) blocks[i].row = hr[i];
+        return kOk;
+    }
     uint8_t *hrows = hs + in_n, *drows = ds + in_n;
     for (int i = 0; i < k; ++i) hrows[i] = blocks[i].row;
     if (where == 1) {

@@ -227,19 +227,70 @@ def test_dropin_mixed_pointers(lh):
     del torch
 
 
-def test_dropin_device_pointers(lh):
-    """Blocks that already live in device memory go through the same entry points."""
+@pytest.mark.parametrize("k,m,nbytes,trace", [
+    (29, 4, 1296, "lh_jit_encode(pointer table)"), (128, 32, 8192, "lh_jit_encode_win(pointer table)"),
+    (200, 3, 64, "lh_ptr_copy_kernel(gather)"), (10, 1, 100, "lh_ptr_copy_kernel(gather)"),
+    (1, 3, 40, "lh_ptr_copy_kernel(gather)")])
+def test_dropin_device_pointers(lh, oracle, k, m, nbytes, trace):
+    """Blocks that already live in device memory go through the same entry points: every
+    pointer in device memory takes the pointer-table form (one copy of the k + m pointers,
+    the blocks read and written where they lie), decode included; the results are the
+    oracle's, the rows rewritten as by the reference."""
     import torch
-    k, m, nbytes = 29, 4, 1296
-    data = lhutil.fill(77, k * nbytes)
-    ref_rc, ref_rec = lhutil.Oracle().encode(k, m, data, nbytes)
-    d = _gpu_tensor(data)
-    r = torch.zeros(m * nbytes, dtype=torch.uint8, device="cuda")
+    prev = lh.set_dispatch("gpu")
+    try:
+        data = lhutil.fill(77 + k, k * nbytes)
+        ref_rc, ref_rec = oracle.encode(k, m, data, nbytes)
+        pool = torch.zeros((k + m + 3) * (nbytes + 16), dtype=torch.uint8, device="cuda")
+        base = pool.data_ptr()
+        off = [((i * 7919) % (k + m + 3)) * (nbytes + 16) + (i % 5) for i in range(k + m)]  # scattered, odd offsets
+        for x in range(k):
+            pool[off[x]:off[x] + nbytes] = torch.from_numpy(data[x * nbytes:(x + 1) * nbytes].copy()).cuda()
+        r = torch.zeros(m * nbytes, dtype=torch.uint8, device="cuda")
+        ptrs = (ctypes.POINTER(ctypes.c_ubyte) * k)()
+        for x in range(k):
+            ptrs[x] = ctypes.cast(base + off[x], ctypes.POINTER(ctypes.c_ubyte))
+        assert lh.cauchy_256_encode(k, m, ptrs, r.data_ptr(), nbytes) == ref_rc == 0
+        assert trace in lh.last_launch(), lh.last_launch()
+        assert r.cpu().numpy().tobytes() == ref_rec.tobytes()
+        # decode: erase min(k, m) originals, recovery blocks into their own scattered places
+        e = min(k, m)
+        slots, rows = lhutil.erasure_case(k * 31 + m, k, m, e)
+        rec = ref_rec.reshape(m, nbytes)
+        blocks = (lh.Block * k)()
+        bufs = []
+        for i, (kind, x) in enumerate(slots):
+            o = off[k + x] if kind == "r" else off[x]
+            if kind == "r":
+                pool[o:o + nbytes] = torch.from_numpy(rec[x].copy()).cuda()
+            blocks[i].data = ctypes.cast(base + o, ctypes.POINTER(ctypes.c_ubyte))
+            blocks[i].row = rows[i]
+            bufs.append((data[x * nbytes:(x + 1) * nbytes] if kind == "d" else rec[x]).copy())
+        rc, exp_rows = oracle.decode(k, m, bufs, list(rows), nbytes)
+        assert lh.cauchy_256_decode(k, m, blocks, nbytes) == rc == 0
+        assert [blocks[i].row for i in range(k)] == exp_rows
+        got = pool.cpu().numpy()
+        for i, (kind, x) in enumerate(slots):
+            o = off[k + x] if kind == "r" else off[x]
+            assert got[o:o + nbytes].tobytes() == bufs[i].tobytes(), i
+    finally:
+        lh.set_dispatch(prev)
+
+
+def test_dropin_device_pointers_invalid_size(lh):
+    """All-device encode with m > 1 and block_bytes % 8 != 0: recovery block 0 is written and
+    -1 returned, as the reference (the pointer-table form's gathered path)."""
+    import torch
+    k, m, nbytes = 5, 3, 12
+    data = torch.randint(0, 256, (k, nbytes), dtype=torch.uint8, device="cuda")
+    r = torch.full((m, nbytes), 9, dtype=torch.uint8, device="cuda")
     ptrs = (ctypes.POINTER(ctypes.c_ubyte) * k)()
     for x in range(k):
-        ptrs[x] = ctypes.cast(d.data_ptr() + x * nbytes, ctypes.POINTER(ctypes.c_ubyte))
-    assert lh.cauchy_256_encode(k, m, ptrs, r.data_ptr(), nbytes) == 0
-    assert r.cpu().numpy().tobytes() == ref_rec.tobytes()
+        ptrs[x] = ctypes.cast(data.data_ptr() + x * nbytes, ctypes.POINTER(ctypes.c_ubyte))
+    assert lh.cauchy_256_encode(k, m, ptrs, r.data_ptr(), nbytes) == -1
+    got = r.cpu().numpy()
+    assert (got[0] == np.bitwise_xor.reduce(data.cpu().numpy(), axis=0)).all()
+    assert (got[1:] == 9).all()
 
 
 # ---------------------------------------------------------------- batched API
