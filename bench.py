@@ -401,6 +401,54 @@ def cpu_baseline(k, m, nbytes, budget_s, stripes, patterns=None):
     return out
 
 
+def device_per_call_us(lib, k, m, nbytes, calls, rounds=5):
+    """As per_call_us, with every block in device memory (the drop-in calls then take the
+    pointer-table form: one copy of the pointers, the blocks coded where they lie)."""
+    import torch
+    import lhutil
+    data = torch.from_numpy(lhutil.fill(7, k * nbytes)).cuda()
+    rec = torch.zeros(m * nbytes, dtype=torch.uint8, device="cuda")
+    ptrs = (ctypes.POINTER(ctypes.c_ubyte) * k)()
+    for x in range(k):
+        ptrs[x] = ctypes.cast(data.data_ptr() + x * nbytes, ctypes.POINTER(ctypes.c_ubyte))
+    rp = ctypes.c_void_p(rec.data_ptr())
+    for _ in range(5):
+        assert lib.cauchy_256_encode(k, m, ptrs, rp, nbytes) == 0
+    per = max(1, calls // rounds)
+    enc_t = []
+    for _ in range(rounds):
+        t0 = time.perf_counter()
+        for _ in range(per):
+            lib.cauchy_256_encode(k, m, ptrs, rp, nbytes)
+        enc_t.append((time.perf_counter() - t0) / per)
+    e = min(k, m)
+    n = per * rounds + 5
+    recs = rec.repeat(n).view(n, m * nbytes)  # a fresh copy of the recovery blocks per call
+    arrays = []
+    for i in range(n):
+        arr = (lhutil.Block * k)()
+        for j, x in enumerate(range(e, k)):
+            arr[j].data = ctypes.cast(data.data_ptr() + x * nbytes, ctypes.POINTER(ctypes.c_ubyte))
+            arr[j].row = x
+        for j in range(e):
+            arr[k - e + j].data = ctypes.cast(recs[i].data_ptr() + j * nbytes, ctypes.POINTER(ctypes.c_ubyte))
+            arr[k - e + j].row = k + j
+        arrays.append(arr)
+    for i in range(5):
+        assert lib.cauchy_256_decode(k, m, arrays[i], nbytes) == 0
+    dec_t = []
+    for r in range(rounds):
+        t0 = time.perf_counter()
+        for i in range(per):
+            lib.cauchy_256_decode(k, m, arrays[5 + r * per + i], nbytes)
+        dec_t.append((time.perf_counter() - t0) / per)
+    got = recs[n - 1].view(m, nbytes)[:e].cpu()
+    ok = bool(torch.equal(got, data.view(k, nbytes)[:e].cpu()))
+    return {"encode_us": round(min(enc_t) * 1e6, 2), "decode_us": round(min(dec_t) * 1e6, 2),
+            "encode_mean_us": round(sum(enc_t) / rounds * 1e6, 2), "decode_mean_us": round(sum(dec_t) / rounds * 1e6, 2),
+            "calls": per * rounds, "rounds": rounds, "ok": ok}
+
+
 def dropin_leg(lh, k, m, nbytes, calls):
     """Per-call latency of the product's drop-in cauchy_256_encode / cauchy_256_decode with
     host pointers, one stripe per call (the reference API shape), plus the ctypes call
@@ -428,6 +476,9 @@ def dropin_leg(lh, k, m, nbytes, calls):
     out["gpu"] = per_call_us(lib.cauchy_256_encode, lib.cauchy_256_decode, k, m, nbytes, calls, d0,
                              dropin_blocks(k, m, nbytes, d0))
     lh.set_dispatch(prev)
+    # blocks already in device memory (any policy runs them on the GPU)
+    out["gpu_device_blocks"] = device_per_call_us(lib, k, m, nbytes, calls)
+    out["gpu_device_blocks"]["kernels"] = lh.last_launch()
     # the recovered blocks of the last decoded array must equal the erased originals
     ref = lhutil.fill(7, k * nbytes).reshape(k, nbytes)
     rec = np.zeros(m * nbytes, dtype=np.uint8)
@@ -447,7 +498,8 @@ def dropin_leg(lh, k, m, nbytes, calls):
         noop()
     out["ctypes_overhead_us"] = round((time.perf_counter() - t0) / calls * 1e6, 2)
     out["dispatch"] = (f"top level: the default policy ({out['policy']}), served by the {out['engine']}; "
-                       "out['gpu']: the same calls forced onto the GPU")
+                       "out['gpu']: the same calls forced onto the GPU; out['gpu_device_blocks']: the blocks "
+                       "in device memory (pointer-table form)")
     return out
 
 
