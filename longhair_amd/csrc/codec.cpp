@@ -107,12 +107,13 @@ struct DevBuf {
 struct HostPinned {
     uint8_t *ptr = nullptr;
     size_t size = 0;
+    unsigned flags = hipHostMallocDefault;  // hipHostMallocCoherent: read and written by kernels
     hipError_t reserve(size_t n) {
         if (n <= size) return hipSuccess;
         if (ptr) (void)hipHostFree(ptr);
         ptr = nullptr;
         size = 0;
-        hipError_t e = hipHostMalloc(&ptr, n, hipHostMallocDefault);
+        hipError_t e = hipHostMalloc(&ptr, n, flags);
         if (e == hipSuccess) size = n;
         return e;
     }
@@ -150,6 +151,10 @@ struct Device {
         hipStream_t stream = nullptr;  // created on first use
         DevBuf stage;
         HostPinned host_stage;
+        // all-device drop-in calls: the pointer table, rows and status, read and written by
+        // the kernels straight from host memory (coherent: never cached on the device, so a
+        // later call's table is never read stale), no copies
+        HostPinned ptab{nullptr, 0, hipHostMallocCoherent | hipHostMallocMapped};
     };
     static constexpr int kDropinSlots = 4;  // GPU_MAX_HW_QUEUES is 4 by default
     DropinSlot dropin[kDropinSlots];
@@ -835,7 +840,7 @@ static int decode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
         uint8_t *blk = buf, *rows0 = buf + (long long)n * k * bytes;
         uint8_t *const *tab = block_ptrs + (long long)s0 * k;
         if (int rc = ptr_copy(tab, k, k, blk, (long long)k * bytes, bytes, n, false, nullptr, 0, st)) return rc;
-        if (by_row) LH_HIP(hipMemcpyAsync(rows0, d_rows + (long long)s0 * k, (size_t)n * k, hipMemcpyDeviceToDevice, st));
+        if (by_row) LH_HIP(hipMemcpyAsync(rows0, d_rows + (long long)s0 * k, (size_t)n * k, hipMemcpyDefault, st));
         if (int rc = decode_batch(k, m, bytes, n, blk, (long long)k * bytes, d_rows + (long long)s0 * k,
                                   d_status ? d_status + s0 : nullptr, st, allow_compile))
             return rc;
@@ -1163,12 +1168,11 @@ static int dropin_encode(int k, int m, const unsigned char *data_ptrs[], void *r
         // Every block in device memory: the pointer-table form reads them where they lie and
         // writes the recovery blocks in place -- one host-to-device copy of k + m pointers
         // instead of k + 1 block copies.
-        uint64_t *ht = (uint64_t *)sl->host_stage.ptr;
+        LH_HIP(sl->ptab.reserve((size_t)(256 + 256) * 8 + 512));
+        uint64_t *ht = (uint64_t *)sl->ptab.ptr;
         for (int x = 0; x < k; ++x) ht[x] = (uint64_t)(uintptr_t)data_ptrs[x];
         for (int r = 0; r < m; ++r) ht[k + r] = (uint64_t)(uintptr_t)((uint8_t *)recovery + (size_t)r * bytes);
-        const size_t tn = (size_t)(k + m) * 8;
-        LH_HIP(hipMemcpyAsync(sl->stage.ptr, ht, tn, hipMemcpyHostToDevice, st));
-        uint8_t *const *dt = (uint8_t *const *)sl->stage.ptr;
+        uint8_t *const *dt = (uint8_t *const *)sl->ptab.ptr;
         const int rc = encode_batch_ptrs(k, m, bytes, 1, dt, dt + k, st, false);
         LH_HIP(hipStreamSynchronize(st));
         return rc;
@@ -1236,17 +1240,17 @@ static int dropin_decode(int k, int m, Block *blocks, int bytes) {
     if (where == 0) {
         // Every block in device memory: the pointer-table form decodes them in place -- one
         // copy of [k pointers][rows] in, one of [rows][status] out.
-        uint64_t *ht = (uint64_t *)hs;
+        LH_HIP(sl->ptab.reserve((size_t)(256 + 256) * 8 + 512));
+        uint64_t *ht = (uint64_t *)sl->ptab.ptr;
         for (int i = 0; i < k; ++i) ht[i] = (uint64_t)(uintptr_t)blocks[i].data;
-        uint8_t *hr = hs + (size_t)k * 8, *dr = ds + (size_t)k * 8;
+        uint8_t *hr = sl->ptab.ptr + (size_t)256 * 8;  // rows, then status at +256
         for (int i = 0; i < k; ++i) hr[i] = blocks[i].row;
-        LH_HIP(hipMemcpyAsync(ds, hs, (size_t)k * 8 + k, hipMemcpyHostToDevice, st));
-        const int rc = decode_batch_ptrs(k, m, bytes, 1, (uint8_t *const *)ds, dr, (int8_t *)(dr + 256), st, false);
+        hr[256] = 0;
+        const int rc = decode_batch_ptrs(k, m, bytes, 1, (uint8_t *const *)ht, hr, (int8_t *)(hr + 256), st, false);
         if (rc != kOk) {
             (void)hipStreamSynchronize(st);
             return rc;
         }
-        LH_HIP(hipMemcpyAsync(hr, dr, 256 + 16, hipMemcpyDeviceToHost, st));
         LH_HIP(hipStreamSynchronize(st));
         if ((int8_t)hr[256] != 0) return fail(kInvalid, "invalid or duplicated block rows");
         for (int i = 0; i < k; ++i) blocks[i].row = hr[i];
