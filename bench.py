@@ -575,6 +575,7 @@ def ptr_leg(lh, k, m, nbytes, X, D, rows0, rec_view, rec_index=None, reps=5):
     decode buffer first (that copy is outside both timings).  HIP-event times on the launch
     stream, mean of `reps`; the decoded data is checked against X afterwards."""
     import torch
+    lh.prepare_ptrs(k, m, nbytes)  # the pointer-table modules (cached at build time for the configs)
     stripes = X.shape[0]
     s_idx = torch.arange(stripes, device="cuda", dtype=torch.int64).unsqueeze(1)
 

@@ -55,6 +55,10 @@ int cauchy_256_encode_batch_ptrs(int k, int m, int block_bytes, int stripes,
 int cauchy_256_decode_batch_ptrs(int k, int m, int block_bytes, int stripes,
                                  void *const *d_block_ptrs, unsigned char *d_rows, signed char *d_status,
                                  void *stream);
+/* Optional: compile the pointer-table forms of the shape's specialised kernels now
+ * (synchronous), so the first pointer-table calls already code the blocks in place instead
+ * of gathering them while the modules compile in the background.  0 or -3. */
+int cauchy_256_batch_prepare_ptrs(int k, int m, int block_bytes);
 
 /* Host-memory batches: the same operations on stripes that live
  * in host memory, pipelined in chunks of `chunk_stripes` (0 = about 64 MiB for encode,

@@ -159,6 +159,14 @@ def decode_batch_ptrs(k, m, block_bytes, block_ptrs, rows, status=None, stream=N
     return status
 
 
+def prepare_ptrs(k, m, block_bytes):
+    """Compile the pointer-table forms of the shape's specialised kernels now
+    (cauchy_256_batch_prepare_ptrs)."""
+    rc = lib().cauchy_256_batch_prepare_ptrs(k, m, block_bytes)
+    if rc != 0:
+        raise LonghairError(rc, "cauchy_256_batch_prepare_ptrs")
+
+
 def encode_host_batch(data, m, recovery=None, chunk_stripes=0):
     """Encode stripes held in host memory (numpy uint8 [stripes, k, bytes], ideally pinned
     via a pinned torch CPU tensor's .numpy()); pipelined H2D / kernel / D2H."""

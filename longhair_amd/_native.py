@@ -38,6 +38,7 @@ EXPORTS = {
                                                     ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_int]),
     "cauchy_256_batch_prepare": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "cauchy_256_batch_prepare_ptrs": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "cauchy_256_batch_prepare_stream": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                        ctypes.c_void_p]),
     "cauchy_256_last_launch": (ctypes.c_char_p, []),

@@ -1403,6 +1403,20 @@ LH_API int cauchy_256_batch_prepare_stream(int k, int m, int block_bytes, int ma
     return 0;
 }
 
+LH_API int cauchy_256_batch_prepare_ptrs(int k, int m, int block_bytes) {
+    lh::Device *d = nullptr;
+    if (int rc = lh::current_device(&d)) return rc;
+    std::string err;
+    for (int dec = 0; dec < 2; ++dec) {
+        lh::JitConfig cfg;
+        const bool reg = lh::jit_config_for(k, m, block_bytes, dec == 1, &cfg);
+        if (reg ? lh::jit_ptr_config_for(k, m, block_bytes, dec == 1, &cfg)
+                : lh::jit_win_ptr_config_for(k, m, block_bytes, &cfg, dec == 1))
+            if (!d->jit.get(cfg, &err)) return lh::fail(lh::kHipError, err);
+    }
+    return 0;
+}
+
 LH_API int cauchy_256_batch_prepare(int k, int m, int block_bytes, int max_stripes) {
     return cauchy_256_batch_prepare_stream(k, m, block_bytes, max_stripes, nullptr);
 }

@@ -230,3 +230,10 @@ def test_ptrs_gather_in_chunks(lh, oracle, monkeypatch, k, m, nbytes):
     torch.cuda.synchronize()
     assert torch.equal(pstat, sstat) and torch.equal(pr, sr)
     assert torch.equal(_gather(pool, place), sb)
+
+
+@pytest.mark.parametrize("k,m,nbytes", [(29, 4, 1296), (128, 32, 8192), (200, 3, 64)])
+def test_prepare_ptrs(lh, k, m, nbytes):
+    """cauchy_256_batch_prepare_ptrs: the pointer-table modules of a shape (cached at build
+    time here), nothing for a shape without specialised kernels."""
+    lh.prepare_ptrs(k, m, nbytes)
