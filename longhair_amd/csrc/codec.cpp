@@ -393,6 +393,35 @@ static int encode_batch(int k, int m, int bytes, int stripes, const uint8_t *d_d
 }
 
 // ------------------------------------------------------------------------ decode
+// The per-stripe erasure planner (lh_plan_kernel / lh_plan_small_kernel) into the stream's
+// plan workspace (reserved with `work_bytes` of generic-path workspace beside it).
+// LONGHAIR_AMD_PLAN_GJ (knob): Gauss-Jordan even where the closed form applies.
+static int run_planner(Device *d, hipStream_t st, int k, int m, int e_max, int stripes, uint8_t *d_rows,
+                       int8_t *d_status, size_t work_bytes, bool want_w, Workspace **out) {
+    const long long plan_stride = PlanView::bytes(k, m, e_max);
+    Workspace *w = nullptr;
+    if (int rc = workspace(d, st, (size_t)stripes * plan_stride, work_bytes, &w)) return rc;
+    const uint8_t *G = nullptr, *points = nullptr;
+    if (int rc = device_generator(d, k, m, &G, &points, st)) return rc;
+    PlanArgs pa{};
+    pa.rows = d_rows;
+    pa.status = d_status;
+    pa.plan = w->plan.ptr;
+    pa.plan_stride = plan_stride;
+    pa.G = G;
+    pa.points = std::getenv("LONGHAIR_AMD_PLAN_GJ") ? nullptr : points;
+    pa.gf_exp = d->gf_exp;
+    pa.gf_log = d->gf_log;
+    pa.k = k;
+    pa.m = m;
+    pa.e_max = e_max;
+    pa.stripes = stripes;
+    pa.want_w = want_w ? 1 : 0;
+    LH_HIP(launch_plan(pa, st));
+    *out = w;
+    return kOk;
+}
+
 static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks, long long stride,
                         uint8_t *d_rows, int8_t *d_status, hipStream_t st, bool allow_compile) {
     if (k < 1 || m < 1 || bytes <= 0 || stripes < 0 || k > 256 || m > 256)
@@ -450,25 +479,7 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
     }
     const size_t work_bytes = (generic && !wk) ? (size_t)stripes * e_max * bytes : 0;
     Workspace *w = nullptr;
-    if (int rc = workspace(d, st, (size_t)stripes * plan_stride, work_bytes, &w)) return rc;
-    const uint8_t *G = nullptr, *points = nullptr;
-    if (int rc = device_generator(d, k, m, &G, &points, st)) return rc;
-
-    PlanArgs pa{};
-    pa.rows = d_rows;
-    pa.status = d_status;
-    pa.plan = w->plan.ptr;
-    pa.plan_stride = plan_stride;
-    pa.G = G;
-    pa.points = std::getenv("LONGHAIR_AMD_PLAN_GJ") ? nullptr : points;  // knob: Gauss-Jordan always
-    pa.gf_exp = d->gf_exp;
-    pa.gf_log = d->gf_log;
-    pa.k = k;
-    pa.m = m;
-    pa.e_max = e_max;
-    pa.stripes = stripes;
-    pa.want_w = (generic && !wk) ? 1 : 0;
-    LH_HIP(launch_plan(pa, st));
+    if (int rc = run_planner(d, st, k, m, e_max, stripes, d_rows, d_status, work_bytes, generic && !wk, &w)) return rc;
     if (k <= 1) return kOk;
 
     if (m == 1) {
@@ -746,24 +757,7 @@ static int decode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
             const int e_max = k < m ? k : m;
             const long long plan_stride = PlanView::bytes(k, m, e_max);
             Workspace *w = nullptr;
-            if (int rc = workspace(d, st, (size_t)stripes * plan_stride, 0, &w)) return rc;
-            const uint8_t *G = nullptr, *points = nullptr;
-            if (int rc = device_generator(d, k, m, &G, &points, st)) return rc;
-            PlanArgs pa{};
-            pa.rows = d_rows;
-            pa.status = d_status;
-            pa.plan = w->plan.ptr;
-            pa.plan_stride = plan_stride;
-            pa.G = G;
-            pa.points = points;
-            pa.gf_exp = d->gf_exp;
-            pa.gf_log = d->gf_log;
-            pa.k = k;
-            pa.m = m;
-            pa.e_max = e_max;
-            pa.stripes = stripes;
-            pa.want_w = 0;
-            LH_HIP(launch_plan(pa, st));
+            if (int rc = run_planner(d, st, k, m, e_max, stripes, d_rows, d_status, 0, false, &w)) return rc;
             long long s2 = plan_stride;
             const uint8_t *plan = w->plan.ptr;
             void *args[] = {(void *)&block_ptrs, &s1, (void *)&plan, &s2, (void *)&zero, &n};
@@ -786,25 +780,9 @@ static int decode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
             const long long cps = cfg.sub / (64 * cfg.W);
             if ((long long)stripes * cps > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
             Workspace *w = nullptr;
-            if (int rc = workspace(d, st, (size_t)stripes * plan_stride, 0, &w)) return rc;
-            const uint8_t *G = nullptr, *points = nullptr, *zero = nullptr;
-            if (int rc = device_generator(d, k, m, &G, &points, st)) return rc;
+            const uint8_t *zero = nullptr;
             if (int rc = zero_page(d, (size_t)bytes, &zero, st)) return rc;
-            PlanArgs pa{};
-            pa.rows = d_rows;
-            pa.status = d_status;
-            pa.plan = w->plan.ptr;
-            pa.plan_stride = plan_stride;
-            pa.G = G;
-            pa.points = points;
-            pa.gf_exp = d->gf_exp;
-            pa.gf_log = d->gf_log;
-            pa.k = k;
-            pa.m = m;
-            pa.e_max = e_max;
-            pa.stripes = stripes;
-            pa.want_w = 0;
-            LH_HIP(launch_plan(pa, st));
+            if (int rc = run_planner(d, st, k, m, e_max, stripes, d_rows, d_status, 0, false, &w)) return rc;
             const unsigned threads = 64u * (unsigned)((m + cfg.rows_per_wave - 1) / cfg.rows_per_wave);
             long long s1 = (long long)k * 8, s2 = plan_stride;
             const uint8_t *plan = w->plan.ptr;
