@@ -740,6 +740,7 @@ static int decode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
         const JitKernels *jk = jit_lookup(d, cfg, allow_compile, &err, &hard);
         if (hard) return fail(kHipError, err);
         if (jk) {
+            if (jit_blocks(cfg, stripes) > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
             const uint8_t *zero = nullptr;
             if (int rc = zero_page(d, (size_t)bytes, &zero, st)) return rc;
             long long s1 = (long long)k * 8;

@@ -1137,6 +1137,7 @@ hipError_t launch_scatter(const ScatterArgs &a, hipStream_t st) {
 hipError_t launch_ptr_copy(const PtrCopyArgs &a, hipStream_t st) {
     const long long waves = (long long)a.stripes * a.ncopy;
     if (waves <= 0) return hipSuccess;
+    if ((waves + 3) / 4 > 0x7FFFFFFF) return hipErrorInvalidValue;
     hipLaunchKernelGGL(lh_ptr_copy_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
     note_launch(a.scatter ? "lh_ptr_copy_kernel(scatter)" : "lh_ptr_copy_kernel(gather)");
     return hipGetLastError();
