@@ -708,7 +708,13 @@ const JitKernels *JitCache::peek(const JitConfig &cfg) {
 // the compile options, so a shape is compiled once per machine (the large-m windowed
 // modules take about a minute).  Directory: $LONGHAIR_AMD_CACHE_DIR, else jit_cache/
 // next to liblonghair_amd.so (it travels with the repository), else ~/.cache/longhair_amd.
-static const char *kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+// GVN's memory-dependence analysis and load PRE find nothing to do in the straight-line
+// networks (every column is loaded once; the accumulator pins are memory side effects that
+// make the analysis expensive): off, the generated code is byte-identical (checked on the
+// k29/m4, k64/m5 and k128/m32 modules) and the large register networks compile ~30 % faster
+// (k64/m5/4096: 113 -> 81 s).
+static const char *kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-mllvm", "-enable-gvn-memdep=false",
+                              "-mllvm", "-enable-load-pre=false"};
 
 static uint64_t fnv1a(const std::string &s, uint64_t h = 1469598103934665603ull) {
     for (unsigned char ch : s) h = (h ^ ch) * 1099511628211ull;
