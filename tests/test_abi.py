@@ -107,6 +107,29 @@ def test_launch_trace_empty_without_gpu():
     assert longhair_amd.last_launch() == []
 
 
+def test_pointer_table_calls_validate_before_the_device():
+    """cauchy_256_{encode,decode}_batch_ptrs: parameter checks as the strided calls, before any
+    device work (so they hold without a GPU); a call with work and no device fails loudly."""
+    import torch
+    import longhair_amd
+    lib = longhair_amd.lib()
+    tab = (ctypes.c_void_p * 8)()
+    rows = (ctypes.c_ubyte * 8)()
+    assert lib.cauchy_256_encode_batch_ptrs(4, 2, 16, 0, tab, tab, None) == 0      # no stripes: nothing to do
+    assert lib.cauchy_256_encode_batch_ptrs(0, 2, 16, 1, tab, tab, None) == -1     # k < 1
+    assert lib.cauchy_256_encode_batch_ptrs(4, 257, 16, 1, tab, tab, None) == -1   # m > 256
+    assert lib.cauchy_256_encode_batch_ptrs(4, 2, 16, 1, None, tab, None) == -1    # no table
+    assert lib.cauchy_256_decode_batch_ptrs(4, 2, 16, 0, tab, rows, None, None) == 0
+    assert lib.cauchy_256_decode_batch_ptrs(4, 2, 12, 1, tab, rows, None, None) == -1  # bytes % 8, m > 1
+    assert lib.cauchy_256_decode_batch_ptrs(250, 7, 16, 1, tab, rows, None, None) == -1  # k + m > 256
+    assert lib.cauchy_256_decode_batch_ptrs(4, 2, 16, 1, None, rows, None, None) == -1
+    assert lib.cauchy_256_decode_batch_ptrs(4, 2, 16, 1, tab, None, None, None) == -1
+    if not torch.cuda.is_available():
+        assert lib.cauchy_256_encode_batch_ptrs(4, 2, 16, 1, tab, tab, None) == -2
+        assert lib.cauchy_256_decode_batch_ptrs(4, 2, 16, 1, tab, rows, None, None) == -2
+        assert longhair_amd.last_launch() == []
+
+
 def test_inv_jump_table_is_generated():
     """inv_jump.inc (the computed-jump bodies of lh_inverse_gt_kernel) is exactly what
     tools/gen_inv_jump.py renders: no hand edits, no stale generator."""
