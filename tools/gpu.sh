@@ -15,6 +15,7 @@
 #   sq[:CFG]         one SQ counter pass (waves, cycles, waits, VALU/VMEM issue)
 #   pcie             tools/pcie_bench.py k29m4 k200m56
 #   ubench:NAME[:G]  tools/NAME (built here beforehand) with optional group list G (commas)
+#   stress[:SECONDS]  tools/stress.py: random shapes, strided and pointer-table calls vs the oracle
 #   tune:VARIANTS[@k m bytes stripes]  tools/tune.py with TUNE_VARIANTS=VARIANTS (env TUNE_ROUNDS)
 #   bench2           bench.py --gpus 2 --share-gpu (the N>1 control path on one GPU)
 #   benchg[:CFG]     bench.py on the generic kernels only (LONGHAIR_AMD_PATH=generic), 5 steps
@@ -86,6 +87,10 @@ for step in "$@"; do
       [ "$name" != "$arg" ] && groups=${arg#*:}
       timeout -k 10 300 "tools/$name" ${groups//,/ } > "$OUT/$name.txt" 2>&1 || fail "$step" "$OUT/$name.txt"
       cat "$OUT/$name.txt" ;;
+    stress)
+      secs=${arg:-120}
+      timeout -k 10 $((secs + 120)) python -u tools/stress.py "$secs" > "$OUT/stress.txt" 2>&1 || fail "$step" "$OUT/stress.txt"
+      tail -3 "$OUT/stress.txt" ;;
     tune)
       n=$((${n:-0} + 1))
       targs=""
