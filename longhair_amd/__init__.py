@@ -14,7 +14,6 @@ goes through the HIP library and fails loudly (LonghairError / non-zero codes) w
 device or no library is available.
 """
 import ctypes
-import os
 
 from ._native import Block, lib, library_path  # noqa: F401
 
@@ -65,6 +64,35 @@ def _addr(x):
     raise TypeError(f"cannot take the address of {type(x)}")
 
 
+def _require(cond, msg, exc=ValueError):
+    """API argument check that survives `python -O` (unlike assert): a bad tensor must raise,
+    never reach a kernel as a wrong pointer."""
+    if not cond:
+        raise exc(msg)
+
+
+def _cuda_tensor(t, dtype, name, shape=None, contiguous=False, device=None):
+    """`t` must be a CUDA tensor of `dtype` (and `shape`, contiguity, `device` when given)."""
+    import torch
+    _require(isinstance(t, torch.Tensor), f"{name} must be a torch tensor", TypeError)
+    _require(t.dtype == dtype, f"{name} must be {dtype}, got {t.dtype}", TypeError)
+    _require(t.is_cuda, f"{name} must be a CUDA (device) tensor")
+    if shape is not None:
+        _require(tuple(t.shape) == tuple(shape), f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
+    if contiguous:
+        _require(t.is_contiguous(), f"{name} must be contiguous")
+    if device is not None:
+        _require(t.device == device, f"{name} must be on {device}, got {t.device}")
+
+
+def _block_tensor(t, name):
+    """uint8 CUDA tensor [stripes, blocks, bytes] with contiguous blocks (any stripe stride)."""
+    import torch
+    _cuda_tensor(t, torch.uint8, name)
+    _require(t.dim() == 3, f"{name} must be [stripes, blocks, block_bytes]")
+    _require(t.stride(2) == 1 and t.stride(1) == t.shape[2], f"{name}: blocks must be contiguous within a stripe")
+
+
 def _stream_handle(stream):
     if stream is None:
         import torch
@@ -79,12 +107,13 @@ def encode_batch(data, m, recovery=None, stream=None):
     Returns the recovery tensor [stripes, m, block_bytes] (allocated if not given).
     Runs asynchronously on `stream` (default: torch's current stream)."""
     import torch
-    assert data.dtype == torch.uint8 and data.is_cuda and data.dim() == 3
-    assert data.stride(2) == 1 and data.stride(1) == data.shape[2]
+    _block_tensor(data, "data")
     stripes, k, nbytes = data.shape
     if recovery is None:
         recovery = torch.empty((stripes, m, nbytes), dtype=torch.uint8, device=data.device)
-    assert recovery.stride(2) == 1 and recovery.stride(1) == nbytes and recovery.shape[1] == m
+    _block_tensor(recovery, "recovery")
+    _require(tuple(recovery.shape) == (stripes, m, nbytes), f"recovery must be [{stripes}, {m}, {nbytes}]")
+    _require(recovery.device == data.device, "recovery must be on data's device")
     rc = lib().cauchy_256_encode_batch(k, m, nbytes, stripes, ctypes.c_void_p(data.data_ptr()),
                                        ctypes.c_longlong(data.stride(0)),
                                        ctypes.c_void_p(recovery.data_ptr()),
@@ -103,12 +132,12 @@ def decode_batch(blocks, rows, m, status=None, stream=None):
     rows:   uint8 CUDA tensor [stripes, k] -- each slot's Block.row; rewritten in place.
     Returns `status` (int8 [stripes], 0 ok / -1 invalid rows)."""
     import torch
-    assert blocks.dtype == torch.uint8 and blocks.is_cuda and blocks.dim() == 3
-    assert blocks.stride(2) == 1 and blocks.stride(1) == blocks.shape[2]
+    _block_tensor(blocks, "blocks")
     stripes, k, nbytes = blocks.shape
-    assert rows.dtype == torch.uint8 and rows.is_contiguous() and tuple(rows.shape) == (stripes, k)
+    _cuda_tensor(rows, torch.uint8, "rows", (stripes, k), True, blocks.device)
     if status is None:
         status = torch.empty((stripes,), dtype=torch.int8, device=blocks.device)
+    _cuda_tensor(status, torch.int8, "status", (stripes,), True, blocks.device)
     rc = lib().cauchy_256_decode_batch(k, m, nbytes, stripes, ctypes.c_void_p(blocks.data_ptr()),
                                        ctypes.c_longlong(blocks.stride(0)),
                                        ctypes.c_void_p(rows.data_ptr()),
@@ -119,9 +148,9 @@ def decode_batch(blocks, rows, m, status=None, stream=None):
     return status
 
 
-def _ptr_table(t, stripes, n):
+def _ptr_table(t, stripes, n, name="pointer table"):
     import torch
-    assert t.dtype == torch.int64 and t.is_cuda and t.is_contiguous() and tuple(t.shape) == (stripes, n)
+    _cuda_tensor(t, torch.int64, name, (stripes, n), True)
     return ctypes.c_void_p(t.data_ptr())
 
 
@@ -132,8 +161,8 @@ def encode_batch_ptrs(k, m, block_bytes, data_ptrs, recovery_ptrs, stream=None):
                    per stripe, cauchy_256.h:78);
     recovery_ptrs: int64 CUDA tensor [stripes, m], where recovery block r of each stripe goes."""
     stripes = data_ptrs.shape[0]
-    rc = lib().cauchy_256_encode_batch_ptrs(k, m, block_bytes, stripes, _ptr_table(data_ptrs, stripes, k),
-                                            _ptr_table(recovery_ptrs, stripes, m),
+    rc = lib().cauchy_256_encode_batch_ptrs(k, m, block_bytes, stripes, _ptr_table(data_ptrs, stripes, k, "data_ptrs"),
+                                            _ptr_table(recovery_ptrs, stripes, m, "recovery_ptrs"),
                                             ctypes.c_void_p(_stream_handle(stream)))
     if rc != 0:
         raise LonghairError(rc, "cauchy_256_encode_batch_ptrs")
@@ -148,10 +177,12 @@ def decode_batch_ptrs(k, m, block_bytes, block_ptrs, rows, status=None, stream=N
     Returns `status` (int8 [stripes], 0 ok / -1 invalid rows)."""
     import torch
     stripes = block_ptrs.shape[0]
-    assert rows.dtype == torch.uint8 and rows.is_contiguous() and tuple(rows.shape) == (stripes, k)
+    table = _ptr_table(block_ptrs, stripes, k, "block_ptrs")
+    _cuda_tensor(rows, torch.uint8, "rows", (stripes, k), True, block_ptrs.device)
     if status is None:
         status = torch.empty((stripes,), dtype=torch.int8, device=rows.device)
-    rc = lib().cauchy_256_decode_batch_ptrs(k, m, block_bytes, stripes, _ptr_table(block_ptrs, stripes, k),
+    _cuda_tensor(status, torch.int8, "status", (stripes,), True, block_ptrs.device)
+    rc = lib().cauchy_256_decode_batch_ptrs(k, m, block_bytes, stripes, table,
                                             ctypes.c_void_p(rows.data_ptr()), ctypes.c_void_p(status.data_ptr()),
                                             ctypes.c_void_p(_stream_handle(stream)))
     if rc != 0:
@@ -171,7 +202,8 @@ def encode_host_batch(data, m, recovery=None, chunk_stripes=0):
     """Encode stripes held in host memory (numpy uint8 [stripes, k, bytes], ideally pinned
     via a pinned torch CPU tensor's .numpy()); pipelined H2D / kernel / D2H."""
     import numpy as np
-    assert data.dtype == np.uint8 and data.ndim == 3 and data.flags.c_contiguous
+    _require(data.dtype == np.uint8 and data.ndim == 3 and data.flags.c_contiguous,
+             "data must be a C-contiguous uint8 array [stripes, k, block_bytes]")
     stripes, k, nbytes = data.shape
     if recovery is None:
         recovery = np.empty((stripes, m, nbytes), dtype=np.uint8)
@@ -186,9 +218,11 @@ def decode_host_batch(blocks, rows, m, chunk_stripes=0):
     """Decode stripes held in host memory in place (numpy uint8 [stripes, k, bytes] and
     rows [stripes, k]); returns the int8 status per stripe."""
     import numpy as np
-    assert blocks.dtype == np.uint8 and blocks.ndim == 3 and blocks.flags.c_contiguous
+    _require(blocks.dtype == np.uint8 and blocks.ndim == 3 and blocks.flags.c_contiguous,
+             "blocks must be a C-contiguous uint8 array [stripes, k, block_bytes]")
     stripes, k, nbytes = blocks.shape
-    assert rows.dtype == np.uint8 and rows.shape == (stripes, k) and rows.flags.c_contiguous
+    _require(rows.dtype == np.uint8 and rows.shape == (stripes, k) and rows.flags.c_contiguous,
+             f"rows must be a C-contiguous uint8 array [{stripes}, {k}]")
     status = np.zeros(stripes, dtype=np.int8)
     rc = lib().cauchy_256_decode_host_batch(k, m, nbytes, stripes, blocks.ctypes.data, blocks.strides[0],
                                             rows.ctypes.data, status.ctypes.data, chunk_stripes)
@@ -204,10 +238,11 @@ def frame_batch(data, recovery, packets=None, stream=None):
     import torch
     stripes, k, nbytes = data.shape
     m = recovery.shape[1]
-    assert data.stride(2) == 1 and data.stride(1) == nbytes and recovery.stride(2) == 1 and recovery.stride(1) == nbytes
+    _block_tensor(data, "data")
+    _block_tensor(recovery, "recovery")
     if packets is None:
         packets = torch.empty((stripes, k + m, nbytes + 1), dtype=torch.uint8, device=data.device)
-    assert packets.is_contiguous() and tuple(packets.shape) == (stripes, k + m, nbytes + 1)
+    _cuda_tensor(packets, torch.uint8, "packets", (stripes, k + m, nbytes + 1), True, data.device)
     rc = lib().cauchy_256_frame_batch(k, m, nbytes, stripes, ctypes.c_void_p(data.data_ptr()), data.stride(0),
                                       ctypes.c_void_p(recovery.data_ptr()), recovery.stride(0),
                                       ctypes.c_void_p(packets.data_ptr()), packets.stride(0),
@@ -221,13 +256,16 @@ def unframe_batch(packets, blocks=None, rows=None, stream=None):
     """The k packets received per stripe (uint8 CUDA tensor [S, k, B + 1], any order)
     -> (blocks [S, k, B], rows [S, k]), the layout decode_batch takes."""
     import torch
-    assert packets.is_contiguous() and packets.dtype == torch.uint8
+    _cuda_tensor(packets, torch.uint8, "packets", None, True)
+    _require(packets.dim() == 3, "packets must be [stripes, k, block_bytes + 1]")
     stripes, k, b1 = packets.shape
     if blocks is None:
         blocks = torch.empty((stripes, k, b1 - 1), dtype=torch.uint8, device=packets.device)
     if rows is None:
         rows = torch.empty((stripes, k), dtype=torch.uint8, device=packets.device)
-    assert blocks.stride(2) == 1 and blocks.stride(1) == b1 - 1 and rows.is_contiguous()
+    _block_tensor(blocks, "blocks")
+    _require(tuple(blocks.shape) == (stripes, k, b1 - 1), "blocks must be [stripes, k, block_bytes]")
+    _cuda_tensor(rows, torch.uint8, "rows", (stripes, k), True, packets.device)
     rc = lib().cauchy_256_unframe_batch(k, b1 - 1, stripes, ctypes.c_void_p(packets.data_ptr()), packets.stride(0),
                                         ctypes.c_void_p(blocks.data_ptr()), blocks.stride(0),
                                         ctypes.c_void_p(rows.data_ptr()), ctypes.c_void_p(_stream_handle(stream)))
@@ -281,14 +319,6 @@ def batch_path(k, m, block_bytes, decode=False):
     return {0: "generic", 1: "jit", 2: "jit-fused", 3: "jit-win", 4: "jit-wide"}[code]
 
 
-def _phase_b_kernel(k, m):
-    """Phase-B kernel of the split large-m decode (kernels.hip launch_inverse); the
-    authoritative record of a call is last_launch()."""
-    if os.environ.get("LONGHAIR_AMD_WIN_SPLIT") == "0":
-        return []
-    return ["lh_inverse_gt_kernel"]
-
-
 def kernel_names(k, m, block_bytes):
     """Names of the kernels one encode_batch / decode_batch launches for this shape."""
     enc = {"generic": ["lh_apply_generic_kernel"], "jit": ["lh_jit_encode"],
@@ -296,7 +326,7 @@ def kernel_names(k, m, block_bytes):
     dec = {"generic": ["lh_plan_kernel", "lh_apply_generic_kernel", "lh_scatter_kernel"],
            "jit": ["lh_plan_small_kernel" if min(k, m) <= 8 else "lh_plan_kernel", "lh_jit_decode"],
            "jit-fused": ["lh_jit_decode_fused"],
-           "jit-wide": ["lh_plan_kernel", "lh_jit_decode_wide"] + _phase_b_kernel(k, m),
+           "jit-wide": ["lh_plan_kernel", "lh_jit_decode_wide", "lh_inverse_gt_kernel"],
            }[batch_path(k, m, block_bytes, True)]
     if m == 1 or k == 1:
         enc, dec = ["lh_xor_reduce_kernel"], ["lh_plan_kernel", "lh_xor_reduce_kernel"]

@@ -15,7 +15,8 @@ class Block(ctypes.Structure):
     _fields_ = [("data", ctypes.POINTER(ctypes.c_ubyte)), ("row", ctypes.c_ubyte)]
 
 
-# Every symbol include/cauchy_256.h, cauchy_256_batch.h and cauchy_256_dispatch.h declare.
+# Every symbol include/cauchy_256.h, cauchy_256_batch.h, cauchy_256_dispatch.h and (test-only)
+# cauchy_256_test.h declare.
 EXPORTS = {
     "_cauchy_256_init": (ctypes.c_int, [ctypes.c_int]),
     "cauchy_256_encode": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
@@ -54,6 +55,7 @@ EXPORTS = {
     "cauchy_256_set_dispatch": (ctypes.c_int, [ctypes.c_int, ctypes.c_longlong]),
     "cauchy_256_get_dispatch": (ctypes.c_int, []),
     "cauchy_256_host_isa": (ctypes.c_char_p, []),
+    "cauchy_256_debug_throw_next": (None, []),
 }
 
 

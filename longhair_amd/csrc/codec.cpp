@@ -13,6 +13,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <stdexcept>
 #include <thread>
 #include <string>
 #include <vector>
@@ -34,6 +35,34 @@ thread_local std::string g_last_launch;  // kernels enqueued by this thread's la
 static int fail(int code, const std::string &msg) {
     g_last_error = msg;
     return code;
+}
+
+// The C ABI's exception barrier (LH_TRY / LH_CATCH below): called inside a catch block.
+static int internal_error() noexcept {
+    const char *what = "unknown exception";
+    try {
+        throw;
+    } catch (const std::bad_alloc &) {
+        what = "out of host memory";
+    } catch (const std::exception &e) {
+        what = e.what();
+    } catch (...) {
+    }
+    try {
+        g_last_error = std::string("longhair_amd: internal error: ") + what;
+    } catch (...) {
+    }
+    return kHipError;
+}
+
+// Test-only (cauchy_256_debug_throw_next, include/cauchy_256_test.h): the calling thread's
+// next guarded entry point throws inside its guard.
+thread_local int g_throw_next = 0;
+static void test_hook() {
+    if (g_throw_next) {
+        g_throw_next = 0;
+        throw std::runtime_error("exception injected by cauchy_256_debug_throw_next");
+    }
 }
 
 void note_launch(const char *kernel) {
@@ -123,10 +152,6 @@ struct HostPinned {
 struct Workspace {
     DevBuf plan, work;
     DevBuf gather;  // pointer-table batches without a pointer form: the contiguous chunk
-    // Side stream + events of the chunked large-m decode (phase B of chunk c on `side`
-    // while phase A of chunk c + 1 runs on the caller's stream); created on first use.
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_a = nullptr, ev_join = nullptr;
 };
 
 // Per-device state.
@@ -271,10 +296,6 @@ static int workspace(Device *d, hipStream_t st, size_t plan_bytes, size_t work_b
 static long long jit_blocks(const JitConfig &cfg, int stripes) {
     const long long waves = cfg.spw ? (stripes + cfg.spw - 1) / cfg.spw : (long long)stripes * cfg.wps;
     long long blocks = (waves + 3) / 4;
-    if (const char *g = std::getenv("LONGHAIR_AMD_GRID")) {
-        const long long cap = std::atoll(g);
-        if (cap > 0 && blocks > cap) blocks = cap;
-    }
     return blocks;
 }
 
@@ -519,68 +540,29 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         const long long cps = wcfg.sub / (64 * wcfg.W);
         if ((long long)stripes * cps > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
         const unsigned threads = 64u * (unsigned)((m + wcfg.rows_per_wave - 1) / wcfg.rows_per_wave);
-        // LONGHAIR_AMD_WIDE_CHUNK = N (knob, default: the whole batch): phase A then phase B
-        // per chunk of N stripes, so that a chunk's V could be read back from the 256 MiB
-        // Infinity Cache.  Measured slower at every chunk size (profiles/r3c_wide_chunk.txt:
-        // k128/m32 decode 3.94-3.98 ms whole, 4.17 at 1024 stripes, 6.7 at 128; k200/m56 0.60
-        // whole, 0.69 at 32): the per-launch tails cost more than the V traffic saved.
-        long long chunk = stripes;
-        if (wk->cfg.win_split == 1)
-            if (const char *c = std::getenv("LONGHAIR_AMD_WIDE_CHUNK")) chunk = std::atoll(c) > 0 ? std::atoll(c) : stripes;
-        // LONGHAIR_AMD_WIDE_OVERLAP=1 (with chunks): phase B of chunk c runs on a side stream,
-        // overlapping phase A of chunk c + 1 on the caller's stream (fork / join by events, so
-        // the call stays stream-ordered and capturable).  Also measured slower than the whole
-        // batch (k128/m32 4.08-4.27 ms).
-        bool overlap = false;
-        if (wk->cfg.win_split == 1 && chunk < stripes) {
-            const char *o = std::getenv("LONGHAIR_AMD_WIDE_OVERLAP");
-            overlap = o && std::atoi(o) != 0;
-        }
-        if (overlap && !w->side) {
-            if (capturing(st)) {
-                overlap = false;  // (created outside capture only)
-            } else {
-                LH_HIP(hipStreamCreateWithFlags(&w->side, hipStreamNonBlocking));
-                LH_HIP(hipEventCreateWithFlags(&w->ev_fork, hipEventDisableTiming));
-                LH_HIP(hipEventCreateWithFlags(&w->ev_a, hipEventDisableTiming));
-                LH_HIP(hipEventCreateWithFlags(&w->ev_join, hipEventDisableTiming));
-            }
-        }
-        if (overlap) {  // the side stream starts after everything enqueued on st so far
-            LH_HIP(hipEventRecord(w->ev_fork, st));
-            LH_HIP(hipStreamWaitEvent(w->side, w->ev_fork, 0));
-        }
-        for (long long s0 = 0; s0 < stripes; s0 += chunk) {
-            const int n = (int)std::min<long long>(chunk, stripes - s0);
-            uint8_t *cb = d_blocks + s0 * stride;
-            const uint8_t *plan = w->plan.ptr + s0 * plan_stride;
+        // Phase A then phase B over the whole batch.  (Round 3 also ran them per chunk of
+        // stripes, so a chunk's V could be read back from the Infinity Cache, optionally with
+        // phase B on a side stream: slower at every chunk size, profiles/r3c_wide_chunk.txt;
+        // removed in round 5.)
+        {
             long long s1 = stride, s2 = plan_stride;
-            int nn = n;
-            void *args[] = {(void *)&cb, &s1, (void *)&plan, &s2, (void *)&zero, &nn};
-            LH_HIP(hipModuleLaunchKernel(wk->decode_wide, (unsigned)(n * cps), 1, 1, threads, 1, 1, 0, st, args,
+            const uint8_t *plan = w->plan.ptr;
+            int nn = stripes;
+            void *args[] = {(void *)&d_blocks, &s1, (void *)&plan, &s2, (void *)&zero, &nn};
+            LH_HIP(hipModuleLaunchKernel(wk->decode_wide, (unsigned)(stripes * cps), 1, 1, threads, 1, 1, 0, st, args,
                                          nullptr));
-            note_launch(wk->cfg.win_split == 1 ? "lh_jit_decode_wide" : "lh_jit_decode_wide(fused phase B)");
-            if (wk->cfg.win_split == 1) {  // phase A left V_r in the recovery slots: phase B
-                InverseArgs ia{};
-                ia.blocks = cb;
-                ia.stride = stride;
-                ia.plan = plan;
-                ia.plan_stride = plan_stride;
-                ia.k = k;
-                ia.m = m;
-                ia.e_max = e_max;
-                ia.bytes = bytes;
-                ia.stripes = n;
-                if (overlap) {
-                    LH_HIP(hipEventRecord(w->ev_a, st));
-                    LH_HIP(hipStreamWaitEvent(w->side, w->ev_a, 0));
-                }
-                LH_HIP(launch_inverse(ia, overlap ? w->side : st));
-            }
-        }
-        if (overlap) {  // join: later work on st waits for the last phase B
-            LH_HIP(hipEventRecord(w->ev_join, w->side));
-            LH_HIP(hipStreamWaitEvent(st, w->ev_join, 0));
+            note_launch("lh_jit_decode_wide");
+            InverseArgs ia{};  // phase A left V_r in the recovery slots: phase B
+            ia.blocks = d_blocks;
+            ia.stride = stride;
+            ia.plan = plan;
+            ia.plan_stride = plan_stride;
+            ia.k = k;
+            ia.m = m;
+            ia.e_max = e_max;
+            ia.bytes = bytes;
+            ia.stripes = stripes;
+            LH_HIP(launch_inverse(ia, st));
         }
         return kOk;
     }
@@ -643,13 +625,16 @@ static int gather_chunk(Device *d, hipStream_t st, long long per_stripe, int str
 }
 
 static int ptr_copy(uint8_t *const *ptrs, int n, int ncopy, uint8_t *chunk, long long stride, int bytes, int stripes,
-                    bool scatter, const uint8_t *sel, int sel_min, hipStream_t st) {
+                    bool scatter, const uint8_t *sel, int sel_min, hipStream_t st, const int8_t *status = nullptr,
+                    bool m1 = false) {
     PtrCopyArgs a{};
     a.ptrs = ptrs;
     a.chunk = chunk;
     a.stride = stride;
     a.sel = sel;
     a.sel_min = sel_min;
+    a.status = status;
+    a.m1 = m1 ? 1 : 0;
     a.n = n;
     a.ncopy = ncopy;
     a.bytes = bytes;
@@ -805,15 +790,16 @@ static int decode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
             return kOk;
         }
     }
-    // Gather / strided decode / scatter, per chunk.  For k, m > 1 decode writes exactly the
-    // slots that held recovery rows (row >= k before the call: a copy of the chunk's rows
-    // rides at the end of the chunk); m = 1 and k = 1 write every slot back (the m = 1 path
-    // may write a slot holding an original row, cauchy_256.cpp:487-535).
+    // Gather / strided decode / scatter, per chunk.  Only the slots the decode may have
+    // changed go back, judged by the rows before the call (a copy of the chunk's rows rides
+    // at the end of the chunk): for k, m > 1 the slots that held recovery rows (row >= k) of
+    // the stripes it decoded (status 0); for m = 1 the one output slot of cauchy_decode_m1
+    // (which may hold an original row, cauchy_256.cpp:487-535); k = 1: the single slot.
     const long long per = (long long)k * bytes + k;
     uint8_t *buf = nullptr;
     int chunk = 0;
     if (int rc = gather_chunk(d, st, per, stripes, &buf, &chunk)) return rc;
-    const bool by_row = k > 1 && m > 1;
+    const bool by_row = k > 1;
     for (int s0 = 0; s0 < stripes; s0 += chunk) {
         const int n = std::min(chunk, stripes - s0);
         uint8_t *blk = buf, *rows0 = buf + (long long)n * k * bytes;
@@ -823,20 +809,28 @@ static int decode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
         if (int rc = decode_batch(k, m, bytes, n, blk, (long long)k * bytes, d_rows + (long long)s0 * k,
                                   d_status ? d_status + s0 : nullptr, st, allow_compile))
             return rc;
-        if (int rc = ptr_copy(tab, k, k, blk, (long long)k * bytes, bytes, n, true, by_row ? rows0 : nullptr, k, st))
+        if (int rc = ptr_copy(tab, k, k, blk, (long long)k * bytes, bytes, n, true, by_row ? rows0 : nullptr, k, st,
+                              d_status ? d_status + s0 : nullptr, m == 1))
             return rc;
     }
     return kOk;
 }
 
 // -------------------------------------------------------------- drop-in helpers
-static bool is_device_pointer(const void *p) {
+// Where a drop-in block lives: host memory (pageable or pinned), memory the current device's
+// kernels may address directly (its own allocations; managed memory), or another device's
+// memory, which kernels here must not touch (no peer mapping is assumed) -- such blocks
+// travel by hipMemcpyDefault, which the runtime routes as a peer copy.
+enum PtrKind { kHostPtr, kLocalPtr, kRemotePtr };
+static PtrKind pointer_kind(const void *p, int device) {
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
         (void)hipGetLastError();
-        return false;
+        return kHostPtr;
     }
-    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+    if (attr.type == hipMemoryTypeManaged) return kLocalPtr;
+    if (attr.type != hipMemoryTypeDevice) return kHostPtr;
+    return attr.device == device ? kLocalPtr : kRemotePtr;
 }
 
 // ----------------------------------------------------------- host-batch pipeline
@@ -1097,13 +1091,25 @@ static bool want_host(long long work) {
     return pol == kDispatchHost || (pol == kDispatchAuto && work <= g_host_max_work.load(std::memory_order_relaxed));
 }
 
-// 1 if every pointer is host memory, 0 if every one is device memory, -1 if mixed.
-static int classify(const void *const *ptrs, int n, const void *extra) {
-    int dev = 0;
-    for (int i = 0; i < n; ++i) dev += is_device_pointer(ptrs[i]) ? 1 : 0;
+// 1 if every pointer is host memory, 0 if every one is memory of `device` itself (the
+// pointer-table form reads and writes it in place), -1 otherwise (mixed, or any block on
+// another device: per-block hipMemcpyDefault staging).
+static int classify(const void *const *ptrs, int n, const void *extra, int device) {
+    int host = 0, local = 0;
     const int tot = n + (extra ? 1 : 0);
-    if (extra) dev += is_device_pointer(extra) ? 1 : 0;
-    return dev == 0 ? 1 : dev == tot ? 0 : -1;
+    for (int i = 0; i < tot; ++i) {
+        const PtrKind kd = pointer_kind(i < n ? ptrs[i] : extra, device);
+        host += kd == kHostPtr;
+        local += kd == kLocalPtr;
+    }
+    return host == tot ? 1 : local == tot ? 0 : -1;
+}
+
+// Drop-in calls in a process without a HIP device (cauchy_256.cpp:390-399 initialises on any
+// CPU): under the AUTO and HOST policies every call runs on the host SIMD engine; under GPU
+// the call fails with -2.  Batch calls always need a device.
+static bool host_only(int rc) {
+    return rc == kNoDevice && g_dispatch.load(std::memory_order_relaxed) != kDispatchGpu;
 }
 
 // A free drop-in slot (the first whose lock is free), else the slot this thread hashes to,
@@ -1129,9 +1135,10 @@ static int dropin_slot(Device *d, std::unique_lock<std::mutex> *lk, Device::Drop
 static int dropin_encode(int k, int m, const unsigned char *data_ptrs[], void *recovery, int bytes) {
     if (k < 1 || m < 1 || bytes <= 0 || k > 256 || m > 256) return fail(kInvalid, "invalid k, m or block_bytes");
     Device *d = nullptr;
-    if (int rc = current_device(&d)) return rc;
-    const int where = classify((const void *const *)data_ptrs, k, recovery);
-    if (where == 1 && want_host(k > 1 && m > 1 && k + m <= 256 && bytes % 8 == 0 ? host_work(k, m, 0, bytes, false) : 0)) {
+    const int drc = current_device(&d);
+    if (drc && !host_only(drc)) return drc;
+    const int where = drc ? 1 : classify((const void *const *)data_ptrs, k, recovery, d->id);
+    if (drc || (where == 1 && want_host(k > 1 && m > 1 && k + m <= 256 && bytes % 8 == 0 ? host_work(k, m, 0, bytes, false) : 0))) {
         const int rc = host::encode(k, m, (const uint8_t *const *)data_ptrs, (uint8_t *)recovery, bytes);
         return rc == 0 ? kOk : fail(kInvalid, "k + m > 256 or block_bytes % 8 != 0");
     }
@@ -1194,11 +1201,12 @@ static int dropin_decode(int k, int m, Block *blocks, int bytes) {
         if (k + m > 256 || bytes % 8 != 0) return fail(kInvalid, "k + m > 256 or block_bytes % 8 != 0");
     }
     Device *d = nullptr;
-    if (int rc = current_device(&d)) return rc;
+    const int drc = current_device(&d);
+    if (drc && !host_only(drc)) return drc;
     const void *ptrs[256];
     for (int i = 0; i < k; ++i) ptrs[i] = blocks[i].data;
-    const int where = classify(ptrs, k, nullptr);
-    if (where == 1 && want_host(m == 1 ? (long long)k * bytes : host_work(k, m, n_rcv, bytes, true))) {
+    const int where = drc ? 1 : classify(ptrs, k, nullptr, d->id);
+    if (drc || (where == 1 && want_host(m == 1 ? (long long)k * bytes : host_work(k, m, n_rcv, bytes, true)))) {
         if (m == 1) {
             host::decode_m1(k, blocks, bytes);
             return kOk;
@@ -1285,119 +1293,157 @@ static int dropin_decode(int k, int m, Block *blocks, int bytes) {
 
 #define LH_API __attribute__((visibility("default")))
 
+// No C++ exception crosses the C ABI: every int-returning entry point runs
+// inside LH_TRY / LH_CATCH, which turns any exception (std::bad_alloc from a vector or string,
+// std::system_error from a background-compile thread, a runtime_error) into -3 with
+// cauchy_256_last_error() naming it.
+#define LH_TRY try { lh::test_hook();
+#define LH_CATCH } catch (...) { return lh::internal_error(); }
+
 extern "C" {
 
 LH_API int _cauchy_256_init(int expected_version) {
-    if (expected_version != CAUCHY_256_VERSION) return -1;  // cauchy_256.cpp:392-394
-    (void)lh::Field::get();
-    lh::Device *d = nullptr;
-    return lh::current_device(&d);
+    LH_TRY
+        if (expected_version != CAUCHY_256_VERSION) return -1;  // cauchy_256.cpp:392-394
+        (void)lh::Field::get();
+        lh::Device *d = nullptr;
+        const int rc = lh::current_device(&d);
+        // No HIP device: the drop-in calls still work on the host engine unless the policy is
+        // GPU (lh::host_only); cauchy_256_last_error() says which.
+        if (lh::host_only(rc)) {
+            lh::g_last_error = "longhair_amd: no HIP device; drop-in calls run on the host engine, batch calls return -2";
+            return 0;
+        }
+        return rc;
+    LH_CATCH
 }
 
 LH_API int cauchy_256_encode(int k, int m, const unsigned char *data_ptrs[], void *recovery_blocks, int block_bytes) {
-    lh::LaunchTrace trace;
-    return lh::dropin_encode(k, m, data_ptrs, recovery_blocks, block_bytes);
+    LH_TRY
+        lh::LaunchTrace trace;
+        return lh::dropin_encode(k, m, data_ptrs, recovery_blocks, block_bytes);
+    LH_CATCH
 }
 
 LH_API int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes) {
-    lh::LaunchTrace trace;
-    return lh::dropin_decode(k, m, blocks, block_bytes);
+    LH_TRY
+        lh::LaunchTrace trace;
+        return lh::dropin_decode(k, m, blocks, block_bytes);
+    LH_CATCH
 }
 
 LH_API int cauchy_256_encode_batch(int k, int m, int block_bytes, int stripes, const void *d_data, long long data_stride,
                             void *d_recovery, long long recovery_stride, void *stream) {
-    lh::LaunchTrace trace;
-    return lh::encode_batch(k, m, block_bytes, stripes, (const uint8_t *)d_data, data_stride, (uint8_t *)d_recovery,
-                            recovery_stride, (hipStream_t)stream, true);
+    LH_TRY
+        lh::LaunchTrace trace;
+        return lh::encode_batch(k, m, block_bytes, stripes, (const uint8_t *)d_data, data_stride, (uint8_t *)d_recovery,
+                                recovery_stride, (hipStream_t)stream, true);
+    LH_CATCH
 }
 
 LH_API int cauchy_256_decode_batch(int k, int m, int block_bytes, int stripes, void *d_blocks, long long stripe_stride,
                             unsigned char *d_rows, signed char *d_status, void *stream) {
-    lh::LaunchTrace trace;
-    return lh::decode_batch(k, m, block_bytes, stripes, (uint8_t *)d_blocks, stripe_stride, d_rows,
-                            (int8_t *)d_status, (hipStream_t)stream, true);
+    LH_TRY
+        lh::LaunchTrace trace;
+        return lh::decode_batch(k, m, block_bytes, stripes, (uint8_t *)d_blocks, stripe_stride, d_rows,
+                                (int8_t *)d_status, (hipStream_t)stream, true);
+    LH_CATCH
 }
 
 LH_API int cauchy_256_encode_batch_ptrs(int k, int m, int block_bytes, int stripes, const void *const *d_data_ptrs,
                                         void *const *d_recovery_ptrs, void *stream) {
-    lh::LaunchTrace trace;
-    return lh::encode_batch_ptrs(k, m, block_bytes, stripes, (uint8_t *const *)d_data_ptrs,
-                                 (uint8_t *const *)d_recovery_ptrs, (hipStream_t)stream);
+    LH_TRY
+        lh::LaunchTrace trace;
+        return lh::encode_batch_ptrs(k, m, block_bytes, stripes, (uint8_t *const *)d_data_ptrs,
+                                     (uint8_t *const *)d_recovery_ptrs, (hipStream_t)stream);
+    LH_CATCH
 }
 
 LH_API int cauchy_256_decode_batch_ptrs(int k, int m, int block_bytes, int stripes, void *const *d_block_ptrs,
                                         unsigned char *d_rows, signed char *d_status, void *stream) {
-    lh::LaunchTrace trace;
-    return lh::decode_batch_ptrs(k, m, block_bytes, stripes, (uint8_t *const *)d_block_ptrs, d_rows,
-                                 (int8_t *)d_status, (hipStream_t)stream);
+    LH_TRY
+        lh::LaunchTrace trace;
+        return lh::decode_batch_ptrs(k, m, block_bytes, stripes, (uint8_t *const *)d_block_ptrs, d_rows,
+                                     (int8_t *)d_status, (hipStream_t)stream);
+    LH_CATCH
 }
 
 LH_API int cauchy_256_encode_host_batch(int k, int m, int block_bytes, int stripes, const void *h_data,
                                         long long data_stride, void *h_recovery, long long recovery_stride,
                                         int chunk_stripes) {
-    lh::LaunchTrace trace;
-    return lh::host_encode_batch(k, m, block_bytes, stripes, (const uint8_t *)h_data, data_stride,
-                                 (uint8_t *)h_recovery, recovery_stride, chunk_stripes);
+    LH_TRY
+        lh::LaunchTrace trace;
+        return lh::host_encode_batch(k, m, block_bytes, stripes, (const uint8_t *)h_data, data_stride,
+                                     (uint8_t *)h_recovery, recovery_stride, chunk_stripes);
+    LH_CATCH
 }
 
 LH_API int cauchy_256_decode_host_batch(int k, int m, int block_bytes, int stripes, void *h_blocks,
                                         long long stripe_stride, unsigned char *h_rows, signed char *h_status,
                                         int chunk_stripes) {
-    lh::LaunchTrace trace;
-    return lh::host_decode_batch(k, m, block_bytes, stripes, (uint8_t *)h_blocks, stripe_stride, h_rows,
-                                 (int8_t *)h_status, chunk_stripes);
+    LH_TRY
+        lh::LaunchTrace trace;
+        return lh::host_decode_batch(k, m, block_bytes, stripes, (uint8_t *)h_blocks, stripe_stride, h_rows,
+                                     (int8_t *)h_status, chunk_stripes);
+    LH_CATCH
 }
 
 LH_API int cauchy_256_batch_prepare_stream(int k, int m, int block_bytes, int max_stripes, void *stream) {
-    lh::Device *d = nullptr;
-    if (int rc = lh::current_device(&d)) return rc;
-    std::string err;
-    for (int dec = 0; dec < 2; ++dec) {
-        lh::JitConfig cfg;
-        if (lh::jit_config_for(k, m, block_bytes, dec == 1, &cfg) && !d->jit.get(cfg, &err))
-            return lh::fail(lh::kHipError, err);
-    }
-    {
-        lh::JitConfig cfg;
-        if (!lh::jit_config_for(k, m, block_bytes, false, &cfg) && lh::jit_win_config_for(k, m, block_bytes, &cfg) &&
-            !d->jit.get(cfg, &err))
-            return lh::fail(lh::kHipError, err);
-        if (!lh::jit_config_for(k, m, block_bytes, true, &cfg) && lh::jit_win_config_for(k, m, block_bytes, &cfg, true) &&
-            !d->jit.get(cfg, &err))
-            return lh::fail(lh::kHipError, err);
-    }
-    if (max_stripes > 0 && k > 1 && m > 1) {
-        const int e_max = k < m ? k : m;
-        lh::JitConfig cfg;
-        const bool generic = !lh::jit_config_for(k, m, block_bytes, true, &cfg);
-        lh::Workspace *w = nullptr;
-        hipStream_t st = (hipStream_t)stream;
-        if (int rc = lh::workspace(d, st, (size_t)max_stripes * lh::PlanView::bytes(k, m, e_max),
-                                   generic ? (size_t)max_stripes * e_max * block_bytes : 0, &w))
-            return rc;
-        const uint8_t *G = nullptr, *z = nullptr;
-        if (int rc = lh::zero_page(d, (size_t)block_bytes, &z, st)) return rc;
-        if (int rc = lh::device_generator(d, k, m, &G, nullptr, st)) return rc;
-    }
-    return 0;
+    LH_TRY
+        lh::Device *d = nullptr;
+        if (int rc = lh::current_device(&d)) return rc;
+        std::string err;
+        for (int dec = 0; dec < 2; ++dec) {
+            lh::JitConfig cfg;
+            if (lh::jit_config_for(k, m, block_bytes, dec == 1, &cfg) && !d->jit.get(cfg, &err))
+                return lh::fail(lh::kHipError, err);
+        }
+        {
+            lh::JitConfig cfg;
+            if (!lh::jit_config_for(k, m, block_bytes, false, &cfg) && lh::jit_win_config_for(k, m, block_bytes, &cfg) &&
+                !d->jit.get(cfg, &err))
+                return lh::fail(lh::kHipError, err);
+            if (!lh::jit_config_for(k, m, block_bytes, true, &cfg) && lh::jit_win_config_for(k, m, block_bytes, &cfg, true) &&
+                !d->jit.get(cfg, &err))
+                return lh::fail(lh::kHipError, err);
+        }
+        if (max_stripes > 0 && k > 1 && m > 1) {
+            const int e_max = k < m ? k : m;
+            lh::JitConfig cfg;
+            const bool generic = !lh::jit_config_for(k, m, block_bytes, true, &cfg);
+            lh::Workspace *w = nullptr;
+            hipStream_t st = (hipStream_t)stream;
+            if (int rc = lh::workspace(d, st, (size_t)max_stripes * lh::PlanView::bytes(k, m, e_max),
+                                       generic ? (size_t)max_stripes * e_max * block_bytes : 0, &w))
+                return rc;
+            const uint8_t *G = nullptr, *z = nullptr;
+            if (int rc = lh::zero_page(d, (size_t)block_bytes, &z, st)) return rc;
+            if (int rc = lh::device_generator(d, k, m, &G, nullptr, st)) return rc;
+        }
+        return 0;
+    LH_CATCH
 }
 
 LH_API int cauchy_256_batch_prepare_ptrs(int k, int m, int block_bytes) {
-    lh::Device *d = nullptr;
-    if (int rc = lh::current_device(&d)) return rc;
-    std::string err;
-    for (int dec = 0; dec < 2; ++dec) {
-        lh::JitConfig cfg;
-        const bool reg = lh::jit_config_for(k, m, block_bytes, dec == 1, &cfg);
-        if (reg ? lh::jit_ptr_config_for(k, m, block_bytes, dec == 1, &cfg)
-                : lh::jit_win_ptr_config_for(k, m, block_bytes, &cfg, dec == 1))
-            if (!d->jit.get(cfg, &err)) return lh::fail(lh::kHipError, err);
-    }
-    return 0;
+    LH_TRY
+        lh::Device *d = nullptr;
+        if (int rc = lh::current_device(&d)) return rc;
+        std::string err;
+        for (int dec = 0; dec < 2; ++dec) {
+            lh::JitConfig cfg;
+            const bool reg = lh::jit_config_for(k, m, block_bytes, dec == 1, &cfg);
+            if (reg ? lh::jit_ptr_config_for(k, m, block_bytes, dec == 1, &cfg)
+                    : lh::jit_win_ptr_config_for(k, m, block_bytes, &cfg, dec == 1))
+                if (!d->jit.get(cfg, &err)) return lh::fail(lh::kHipError, err);
+        }
+        return 0;
+    LH_CATCH
 }
 
 LH_API int cauchy_256_batch_prepare(int k, int m, int block_bytes, int max_stripes) {
-    return cauchy_256_batch_prepare_stream(k, m, block_bytes, max_stripes, nullptr);
+    LH_TRY
+        return cauchy_256_batch_prepare_stream(k, m, block_bytes, max_stripes, nullptr);
+    LH_CATCH
 }
 
 LH_API const char *cauchy_256_last_launch(void) { return lh::g_last_launch.c_str(); }
@@ -1407,105 +1453,123 @@ LH_API const char *cauchy_256_last_launch(void) { return lh::g_last_launch.c_str
 // LONGHAIR_AMD_PRECOMPILE_PART=enc|dec restricts it to the encode or decode modules, so
 // a build can compile the two large-m modules of a shape in parallel processes.
 LH_API int cauchy_256_jit_precompile(int k, int m, int block_bytes) {
-    std::string err;
-    std::vector<char> code;
-    lh::JitConfig cfg;
-    const char *part = std::getenv("LONGHAIR_AMD_PRECOMPILE_PART");
-    for (int dec = 0; dec < 2; ++dec) {
-        if (part && std::string(part) != (dec ? "dec" : "enc")) continue;
-        if (lh::jit_config_for(k, m, block_bytes, dec == 1, &cfg)) {
-            if (!lh::compile_code_object(cfg, &code, &err)) return lh::fail(lh::kHipError, err);
-            // the pointer-table form (cauchy_256_*_batch_ptrs) as well, with LONGHAIR_AMD_PRECOMPILE_PTR=1
-            const char *ptr = std::getenv("LONGHAIR_AMD_PRECOMPILE_PTR");
-            if (ptr && std::string(ptr) == "1" && lh::jit_ptr_config_for(k, m, block_bytes, dec == 1, &cfg) &&
-                !lh::compile_code_object(cfg, &code, &err))
-                return lh::fail(lh::kHipError, err);
-        } else if (lh::jit_win_config_for(k, m, block_bytes, &cfg, dec == 1)) {
-            if (!lh::compile_code_object(cfg, &code, &err)) return lh::fail(lh::kHipError, err);
-            const char *ptr = std::getenv("LONGHAIR_AMD_PRECOMPILE_PTR");
-            if (ptr && std::string(ptr) == "1" && lh::jit_win_ptr_config_for(k, m, block_bytes, &cfg, dec == 1) &&
-                !lh::compile_code_object(cfg, &code, &err))
-                return lh::fail(lh::kHipError, err);
+    LH_TRY
+        std::string err;
+        std::vector<char> code;
+        lh::JitConfig cfg;
+        const char *part = std::getenv("LONGHAIR_AMD_PRECOMPILE_PART");
+        for (int dec = 0; dec < 2; ++dec) {
+            if (part && std::string(part) != (dec ? "dec" : "enc")) continue;
+            if (lh::jit_config_for(k, m, block_bytes, dec == 1, &cfg)) {
+                if (!lh::compile_code_object(cfg, &code, &err)) return lh::fail(lh::kHipError, err);
+                // the pointer-table form (cauchy_256_*_batch_ptrs) as well, with LONGHAIR_AMD_PRECOMPILE_PTR=1
+                const char *ptr = std::getenv("LONGHAIR_AMD_PRECOMPILE_PTR");
+                if (ptr && std::string(ptr) == "1" && lh::jit_ptr_config_for(k, m, block_bytes, dec == 1, &cfg) &&
+                    !lh::compile_code_object(cfg, &code, &err))
+                    return lh::fail(lh::kHipError, err);
+            } else if (lh::jit_win_config_for(k, m, block_bytes, &cfg, dec == 1)) {
+                if (!lh::compile_code_object(cfg, &code, &err)) return lh::fail(lh::kHipError, err);
+                const char *ptr = std::getenv("LONGHAIR_AMD_PRECOMPILE_PTR");
+                if (ptr && std::string(ptr) == "1" && lh::jit_win_ptr_config_for(k, m, block_bytes, &cfg, dec == 1) &&
+                    !lh::compile_code_object(cfg, &code, &err))
+                    return lh::fail(lh::kHipError, err);
+            }
         }
-    }
-    return 0;
+        return 0;
+    LH_CATCH
 }
 
 LH_API int cauchy_256_batch_path(int k, int m, int block_bytes, int what) {
-    lh::JitConfig cfg;
-    if (!lh::jit_config_for(k, m, block_bytes, what == 1, &cfg)) {
-        if (what == 0) return lh::jit_win_config_for(k, m, block_bytes, &cfg) ? 3 : 0;
-        return lh::jit_win_config_for(k, m, block_bytes, &cfg, true) ? 4 : 0;
-    }
-    // Decode: 2 when the plan is computed inside the specialised kernel (jit_codec.hip,
-    // LH_FUSED: e_max <= 4, one stripe per <= 64 lanes, k <= 64).
-    const int e_max = k < m ? k : m;
-    if (what == 1 && e_max <= 4 && cfg.nch <= 64 && k <= 64 && std::getenv("LONGHAIR_AMD_NO_FUSED_PLAN") == nullptr)
-        return 2;
-    return 1;
+    LH_TRY
+        lh::JitConfig cfg;
+        if (!lh::jit_config_for(k, m, block_bytes, what == 1, &cfg)) {
+            if (what == 0) return lh::jit_win_config_for(k, m, block_bytes, &cfg) ? 3 : 0;
+            return lh::jit_win_config_for(k, m, block_bytes, &cfg, true) ? 4 : 0;
+        }
+        // Decode: 2 when the plan is computed inside the specialised kernel (jit_codec.hip,
+        // LH_FUSED: e_max <= 4, one stripe per <= 64 lanes, k <= 64).
+        const int e_max = k < m ? k : m;
+        if (what == 1 && e_max <= 4 && cfg.nch <= 64 && k <= 64 && std::getenv("LONGHAIR_AMD_NO_FUSED_PLAN") == nullptr)
+            return 2;
+        return 1;
+    LH_CATCH
 }
 
 LH_API int cauchy_256_frame_batch(int k, int m, int block_bytes, int stripes, const void *d_data,
                                   long long data_stride, const void *d_recovery, long long recovery_stride,
                                   void *d_packets, long long packet_stride, void *stream) {
-    if (k < 1 || m < 0 || k + m > 256 || block_bytes <= 0 || stripes < 0 ||
-        data_stride < (long long)k * block_bytes || (m > 0 && recovery_stride < (long long)m * block_bytes) ||
-        packet_stride < (long long)(k + m) * (block_bytes + 1))
-        return lh::fail(lh::kInvalid, "invalid framing parameters");
-    lh::Device *d = nullptr;
-    if (int rc = lh::current_device(&d)) return rc;
-    lh::FrameArgs a{};
-    a.data = (const uint8_t *)d_data;
-    a.data_stride = data_stride;
-    a.rec = (const uint8_t *)d_recovery;
-    a.rec_stride = recovery_stride;
-    a.packets = (uint8_t *)d_packets;
-    a.packet_stride = packet_stride;
-    a.k = k;
-    a.m = m;
-    a.bytes = block_bytes;
-    a.stripes = stripes;
-    a.npk = k + m;
-    a.unframe = 0;
-    if (hipError_t e = lh::launch_frame(a, (hipStream_t)stream))
-        return lh::fail(lh::kHipError, std::string("frame: ") + hipGetErrorString(e));
-    return 0;
+    LH_TRY
+        if (k < 1 || m < 0 || k + m > 256 || block_bytes <= 0 || stripes < 0 ||
+            data_stride < (long long)k * block_bytes || (m > 0 && recovery_stride < (long long)m * block_bytes) ||
+            packet_stride < (long long)(k + m) * (block_bytes + 1))
+            return lh::fail(lh::kInvalid, "invalid framing parameters");
+        lh::Device *d = nullptr;
+        if (int rc = lh::current_device(&d)) return rc;
+        lh::FrameArgs a{};
+        a.data = (const uint8_t *)d_data;
+        a.data_stride = data_stride;
+        a.rec = (const uint8_t *)d_recovery;
+        a.rec_stride = recovery_stride;
+        a.packets = (uint8_t *)d_packets;
+        a.packet_stride = packet_stride;
+        a.k = k;
+        a.m = m;
+        a.bytes = block_bytes;
+        a.stripes = stripes;
+        a.npk = k + m;
+        a.unframe = 0;
+        if (hipError_t e = lh::launch_frame(a, (hipStream_t)stream))
+            return lh::fail(lh::kHipError, std::string("frame: ") + hipGetErrorString(e));
+        return 0;
+    LH_CATCH
 }
 
 LH_API int cauchy_256_unframe_batch(int k, int block_bytes, int stripes, const void *d_packets,
                                     long long packet_stride, void *d_blocks, long long stripe_stride,
                                     unsigned char *d_rows, void *stream) {
-    if (k < 1 || k > 256 || block_bytes <= 0 || stripes < 0 || packet_stride < (long long)k * (block_bytes + 1) ||
-        stripe_stride < (long long)k * block_bytes)
-        return lh::fail(lh::kInvalid, "invalid framing parameters");
-    lh::Device *d = nullptr;
-    if (int rc = lh::current_device(&d)) return rc;
-    lh::FrameArgs a{};
-    a.packets = (uint8_t *)d_packets;
-    a.packet_stride = packet_stride;
-    a.blocks = (uint8_t *)d_blocks;
-    a.blocks_stride = stripe_stride;
-    a.rows = d_rows;
-    a.k = k;
-    a.bytes = block_bytes;
-    a.stripes = stripes;
-    a.npk = k;
-    a.unframe = 1;
-    if (hipError_t e = lh::launch_frame(a, (hipStream_t)stream))
-        return lh::fail(lh::kHipError, std::string("unframe: ") + hipGetErrorString(e));
-    return 0;
+    LH_TRY
+        if (k < 1 || k > 256 || block_bytes <= 0 || stripes < 0 || packet_stride < (long long)k * (block_bytes + 1) ||
+            stripe_stride < (long long)k * block_bytes)
+            return lh::fail(lh::kInvalid, "invalid framing parameters");
+        lh::Device *d = nullptr;
+        if (int rc = lh::current_device(&d)) return rc;
+        lh::FrameArgs a{};
+        a.packets = (uint8_t *)d_packets;
+        a.packet_stride = packet_stride;
+        a.blocks = (uint8_t *)d_blocks;
+        a.blocks_stride = stripe_stride;
+        a.rows = d_rows;
+        a.k = k;
+        a.bytes = block_bytes;
+        a.stripes = stripes;
+        a.npk = k;
+        a.unframe = 1;
+        if (hipError_t e = lh::launch_frame(a, (hipStream_t)stream))
+            return lh::fail(lh::kHipError, std::string("unframe: ") + hipGetErrorString(e));
+        return 0;
+    LH_CATCH
 }
 
 LH_API const char *cauchy_256_last_error(void) { return lh::g_last_error.c_str(); }
 
 LH_API int cauchy_256_set_dispatch(int policy, long long host_max_work) {
-    if (policy < lh::kDispatchGpu || policy > lh::kDispatchHost) return lh::fail(lh::kInvalid, "unknown dispatch policy");
-    if (host_max_work >= 0) lh::g_host_max_work.store(host_max_work);
-    return lh::g_dispatch.exchange(policy);
+    LH_TRY
+        if (policy < lh::kDispatchGpu || policy > lh::kDispatchHost) return lh::fail(lh::kInvalid, "unknown dispatch policy");
+        if (host_max_work >= 0) lh::g_host_max_work.store(host_max_work);
+        return lh::g_dispatch.exchange(policy);
+    LH_CATCH
 }
 
-LH_API int cauchy_256_get_dispatch(void) { return lh::g_dispatch.load(); }
+LH_API int cauchy_256_get_dispatch(void) {
+    LH_TRY
+        return lh::g_dispatch.load();
+    LH_CATCH
+}
 
 LH_API const char *cauchy_256_host_isa(void) { return lh::host::isa_name(); }
+
+// Test-only (include/cauchy_256_test.h): the calling thread's next guarded entry point
+// throws inside its exception barrier, which must turn it into -3.
+LH_API void cauchy_256_debug_throw_next(void) { lh::g_throw_next = 1; }
 
 }  // extern "C"

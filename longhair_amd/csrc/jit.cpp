@@ -10,6 +10,8 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <deque>
+#include <functional>
 #include <sstream>
 #include <thread>
 
@@ -67,14 +69,6 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
             best_nch = nch;
         }
     }
-    if (const char *fw = std::getenv("LONGHAIR_AMD_JIT_W")) {  // tuning override
-        const int W = std::atoi(fw);
-        if ((W == 1 || W == 2 || W == 4 || W == 8 || W == 12 || W == 16) && W <= sub &&
-            rows * 8 * ((W + 3) / 4) <= 2 * kMaxAccDwords) {
-            const int nch = (sub + W - 1) / W;
-            if (!(nch > 64 && decode && sub % W != 0)) { best_w = W; best_nch = nch; }
-        }
-    }
     if (!best_w) return false;
     const int W = best_w, nch2 = best_nch;
     if (nch2 <= 64) spw = 64 / nch2;
@@ -88,26 +82,6 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     cfg->nch = nch2;
     cfg->spw = spw;
     cfg->wps = wps;
-    // 8-byte lanes over whole stripes whose sub-blocks start off an 8-byte boundary (sub % 8
-    // != 0), when the last chunk's valid bytes plus any sub-block's offset fit one word
-    // (jit_codec.hip LH_VLAST + S_b <= 8: sub % 8 in {1, 2, 4}, e.g. 1296-byte blocks):
-    //  al = 2 (LONGHAIR_AMD_JIT_ALS=1): the outputs stored as aligned words (LH_ALS);
-    //  al = 1 (LONGHAIR_AMD_JIT_AL=1): aligned column loads realigned across lanes by DPP (LH_AL).
-    // Both off by default: measured slower on k29/m4 (profiles/r4d_tune_k29m4.txt: encode 0.591
-    // with aligned stores -- 132 VGPRs, 3 waves/SIMD -- against 0.563 ms; the aligned loads'
-    // access pattern 0.554 against 0.530 ms, profiles/r4c_ubench_floor_enc.txt).
-    cfg->al = 0;
-    if (W == 8 && nch2 <= 64 && sub % 8 != 0) {
-        const int vlast = sub - 8 * (nch2 - 1);
-        int smax = 0;
-        for (int b = 0; b < 8; ++b) smax = std::max(smax, (b * sub) % 8);
-        if (vlast + smax <= 8) {
-            const char *al = std::getenv("LONGHAIR_AMD_JIT_AL");
-            const char *als = std::getenv("LONGHAIR_AMD_JIT_ALS");
-            if (al && std::string(al) == "1") cfg->al = 1;
-            else if (als && std::string(als) == "1") cfg->al = 2;
-        }
-    }
     cfg->defines.clear();
     if (const char *d = std::getenv("LONGHAIR_AMD_JIT_DEFINES")) cfg->defines = d;
     return true;
@@ -117,15 +91,12 @@ bool jit_ptr_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     if (!jit_config_for(k, m, bytes, decode, cfg)) return false;
     if ((long long)(cfg->spw ? cfg->spw : 1) * k > 1024) return false;  // LDS: 4 waves x 8 B x spw x (k + 1) <= 35 KiB
     cfg->ptr = 1;
-    cfg->al = 0;  // (the aligned forms address through buffer resources)
     return true;
 }
 
 bool jit_win_ptr_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
     if (!jit_win_config_for(k, m, bytes, cfg, decode)) return false;
     cfg->ptr = 1;
-    cfg->win_lds = 1;                 // (the pointer form stages columns by LDS-DMA)
-    cfg->win_split = decode ? 1 : 0;  // (and writes V back for lh_inverse_gt_kernel)
     return true;
 }
 
@@ -145,17 +116,14 @@ bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
     cfg->spw = 0;
     cfg->wps = (cfg->nch + 63) / 64;
     cfg->win = decode ? 2 : 1;
+    // Decode: phase A writes V_r in place of R_r and lh_inverse_gt_kernel (kernels.hip) does
+    // phase B.  (Round 4 built two fused forms, V kept in the registers of the wave that
+    // computed it: both slower, k128/m32 5.55 / 4.03 ms against 3.44 ms, and removed in round 5;
+    // DESIGN.md 5.3.)
+    cfg->win_split = decode ? 1 : 0;
     // Rows per wave: 16 (half the redundant column loads and nibble tables of 8: k128/m32
     // encode 4.21 -> 3.00 ms; split decode phase A: k128/m32 decode 4.24 -> 4.14 ms,
-    // k200/m56 0.87 -> 0.79), for the fused decode too (its V rows stay in the registers of
-    // the wave that computed them).
-    cfg->win_split = decode ? 1 : 0;
-    // LONGHAIR_AMD_WIN_SPLIT: 1 split (default), 0 fused with the in-asm jump table, 2 fused
-    // with the table once per code object (as lh_inverse_gt_kernel)
-    if (const char *sp = std::getenv("LONGHAIR_AMD_WIN_SPLIT")) {
-        const int v = std::atoi(sp);
-        cfg->win_split = decode ? (v == 1 ? 1 : v == 2 ? 2 : 0) : 0;
-    }
+    // k200/m56 0.87 -> 0.79; 11 or 12 measured slower, profiles/r4i_tune_*_rows.txt).
     // At most 16 rows per wave, spread evenly over the ceil(m / 16) waves: the waves meet
     // at a barrier every column, so the fullest one sets the pace (k200/m56: 14-row groups
     // instead of 16 + 16 + 16 + 8, encode 0.414 -> 0.396 ms, decode 0.810 -> 0.788 ms).
@@ -163,14 +131,10 @@ bool jit_win_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
         const int cap = 16, ng = (m + cap - 1) / cap;
         cfg->rows_per_wave = (m + ng - 1) / ng;
     }
-    if (const char *r = std::getenv("LONGHAIR_AMD_WIN_ROWS")) cfg->rows_per_wave = std::atoi(r);
-    if (!decode)  // tuning knob for the encode alone (the decode's phase A keeps its rows)
-        if (const char *r = std::getenv("LONGHAIR_AMD_WIN_ROWS_ENC")) cfg->rows_per_wave = std::atoi(r);
-    cfg->rows_per_wave = std::max(1, std::min(16, cfg->rows_per_wave));
     cfg->win_pf = 3;
-    if (const char *f = std::getenv("LONGHAIR_AMD_WIN_PF")) cfg->win_pf = std::max(1, std::atoi(f));
+    // Column tiles staged once per workgroup by LDS-DMA (round 3: per-wave global loads and a
+    // private LDS ring per wave measured slower, profiles/r3t_win_private_ring.txt).
     cfg->win_lds = 1;
-    if (const char *l = std::getenv("LONGHAIR_AMD_WIN_LDS")) cfg->win_lds = std::min(2, std::max(0, std::atoi(l)));
     if ((m + cfg->rows_per_wave - 1) / cfg->rows_per_wave > 16) return false;  // <= 1024 threads
     if (decode && m > 64) return false;  // the plan's used-row mask is one 64-lane ballot
     cfg->defines.clear();
@@ -187,12 +151,6 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
     const int R = c.rows_per_wave, k = c.k, m = c.m, PF = c.win_pf;
     const int r0 = g * R, r1 = std::min(m, r0 + R);
     const bool elim = c.win == 2;  // decode phase A: slot-mapped columns + recovery rows
-    auto col = [&](int x) {
-        std::ostringstream e;
-        if (elim) e << "lh_slot(slv, " << x << ", base, zero)";
-        else e << "(base + " << (long long)x * c.bytes << "LL)";
-        return e.str();
-    };
     // LDS staging (c.win_lds): the workgroup's 8 x 256-byte column tile is fetched once by
     // LDS-DMA (global_load_lds_dwordx4, 16 B per lane; waves 0 and 1 each move one 1-KiB
     // half, or wave 0 both when the group has one wave) into a ring of D = PF + 1 tiles,
@@ -201,16 +159,8 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
     // x - 1 (read by every wave before the barrier) and reads its 8 dwords from LDS.  Each
     // column crosses HBM once per workgroup, at 16 B per lane, instead of once per wave at
     // 4 B per lane (a 4-byte-lane stream reads at 4.1 TB/s against 6.3 for 16-byte lanes).
-    const bool lds = c.win_lds != 0;
-    // c.win_lds == 2: every wave stages the whole column tile into a ring of its own (2 DMA
-    // instructions per column) and waits only for its own DMA: no workgroup barrier per
-    // column, twice the L2 -> LDS traffic and LDS.
-    const bool priv = c.win_lds == 2;
     const int NG = (m + R - 1) / R, D = PF + 1;
-    const int ndma = (NG == 1 || priv) ? 2 : (g < 2 ? 1 : 0);  // DMA instructions per column, this wave
-    const std::string toff = priv ? " + " + std::to_string(g * 2048) : "";  // this wave's ring slot
-    const bool split = elim && c.win_split == 1;  // V_r goes back in place of R_r (lh_inverse_gt_kernel follows)
-    const bool fgt = elim && c.win_split == 2;     // fused, multiply through the per-code-object table
+    const int ndma = NG == 1 ? 2 : (g < 2 ? 1 : 0);  // DMA instructions per column, this wave
     // c.ptr (pointer-table batches; LDS staging and the split decode only): the stripe's
     // block pointers ride in VGPR lanes (ptl: k slots / columns, otl: m recovery blocks) and
     // lh_pp reads one as a wave-uniform pointer; coff = the workgroup's byte offset in every
@@ -227,12 +177,9 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
            << ", const int coff, const int loff) {\n";
     else
     os << "__device__ __forceinline__ void lh_wg" << g << "(" << (elim ? "" : "const ") << "unsigned char *__restrict__ base, "
-       << (elim ? "const unsigned char *__restrict__ zero, const unsigned int (&slv)[LH_NQ], unsigned int *__restrict__ lv, "
-                  "const unsigned char *__restrict__ pl"
+       << (elim ? "const unsigned int (&slv)[LH_NQ], const unsigned char *__restrict__ pl"
                 : "unsigned char *__restrict__ o")
-       << (lds ? ", const unsigned char *__restrict__ sb, const unsigned char *__restrict__ zb" : "")
-       << (fgt ? ", const unsigned glo, const unsigned ghi" : "")
-       << ") {\n";
+       << ", const unsigned char *__restrict__ sb, const unsigned char *__restrict__ zb) {\n";
     {  // (Starting the accumulators at R_r, loaded before the column loop, measured equal:
        // k128/m32 decode 4.12 / 4.11 ms, k200/m56 0.83 / 0.81 ms.)
         for (int r = r0; r < r1; ++r)
@@ -248,45 +195,31 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
     };
     auto dma = [&](int x, const char *ind) {
         for (int h = 0; h < 2; ++h) {
-            if (!(NG == 1 || priv || g == h)) continue;
-            os << ind << "lh_dma(" << dcol(x) << " + dof" << h << ", tile" << x % D << toff << " + " << h * 1024 << ");\n";
+            if (!(NG == 1 || g == h)) continue;
+            os << ind << "lh_dma(" << dcol(x) << " + dof" << h << ", tile" << x % D << " + " << h * 1024 << ");\n";
         }
     };
-    if (lds) {
-        os << "  const int lane = threadIdx.x & 63;\n";
-        for (int h = 0; h < 2; ++h)
-            if (NG == 1 || priv || g == h)
-                os << "  const unsigned int dof" << h << " = ((" << 64 * h << " + lane) >> 4) * " << c.sub
-                   << "u + ((lane & 15) << 4);\n";
-        for (int q = 0; q < PF && q < k; ++q) dma(q, "  ");
-    } else {
-        for (int q = 0; q < PF && q < k; ++q) {
-            os << "  const unsigned char *c" << q << " = " << col(q) << ";\n";
-            for (int b = 0; b < 8; ++b)
-                os << "  unsigned int d" << q << "_" << b << " = lh_ld(c" << q << " + " << b * c.sub << ");\n";
-        }
-    }
+    os << "  const int lane = threadIdx.x & 63;\n";
+    for (int h = 0; h < 2; ++h)
+        if (NG == 1 || g == h)
+            os << "  const unsigned int dof" << h << " = ((" << 64 * h << " + lane) >> 4) * " << c.sub
+               << "u + ((lane & 15) << 4);\n";
+    for (int q = 0; q < PF && q < k; ++q) dma(q, "  ");
     for (int x = 0; x < k; ++x) {
-        const int slot = lds ? 0 : x % PF;
         os << "  {\n";
-        if (lds) {
+        {
             const int ahead = std::min(PF - 1, k - 1 - x);  // this wave's DMAs issued after column x
             if (ndma) os << "    lh_wait_vm(" << ndma * ahead << ");\n";
-            if (!priv) os << "    __builtin_amdgcn_s_barrier();\n";
+            os << "    __builtin_amdgcn_s_barrier();\n";
             if (x + PF < k) dma(x + PF, "    ");
-        } else if (x + PF < k) {
-            os << "    const unsigned char *cn = " << col(x + PF) << ";\n";
-            for (int b = 0; b < 8; ++b)
-                os << "    const unsigned int n" << b << " = lh_ld(cn + " << b * c.sub << ");\n";
         }
         // Decode: an erased original contributes nothing -- skip its tables and XORs (a
         // wave-uniform branch; the column's DMA / ring slot bookkeeping above still runs).
         if (elim)
             os << "    if (__builtin_amdgcn_readlane((int)slv[" << x / 64 << "], " << x % 64 << ") != 0xFF) {\n";
-        if (lds)
-            for (int b = 0; b < 8; ++b)
-                os << "    const unsigned int d0_" << b << " = ((const unsigned int *)(tile" << x % D << toff << " + " << b * 256
-                   << "))[lane];\n";
+        for (int b = 0; b < 8; ++b)
+            os << "    const unsigned int d0_" << b << " = ((const unsigned int *)(tile" << x % D << " + " << b * 256
+               << "))[lane];\n";
         // Which nibble-table entries (lo: sub-blocks 0..3, hi: 4..7) this group needs.
         bool need[2][16] = {};
         for (int r = r0; r < r1; ++r) {
@@ -305,7 +238,7 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
                 const int low = __builtin_ctz(n), pre = n & (n - 1);
                 os << "    const unsigned int t" << h << "_" << n << " = ";
                 if (pre) os << "t" << h << "_" << pre << " ^ ";
-                os << "d" << slot << "_" << (4 * h + low) << ";\n";
+                os << "d0_" << (4 * h + low) << ";\n";
             }
         }
         for (int r = r0; r < r1; ++r) {
@@ -323,11 +256,9 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
         }
         os << "    LH_PIN" << (r1 - r0) << ";\n";
         if (elim) os << "    }\n";
-        if (!lds && x + PF < k)
-            for (int b = 0; b < 8; ++b) os << "    d" << slot << "_" << b << " = n" << b << ";\n";
         os << "  }\n";
     }
-    if (split) {  // V_r = R_r + sum_x ...: read R_r, store V_r over it (absent rows: nothing)
+    if (elim) {  // V_r = R_r + sum_x ...: read R_r, store V_r over it (absent rows: nothing)
         for (int r = r0; r < r1; ++r) {
             os << "  {\n    const unsigned int s = (unsigned int)__builtin_amdgcn_readlane((int)slv[" << (k + r) / 64
                << "], " << (k + r) % 64 << ");\n    if (s != 0xFFu) {\n";
@@ -341,66 +272,6 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
                 os << "      lh_st(rp + " << y * c.sub << ", a" << (r - r0) << "_" << y << " ^ r" << y << ");\n";
             os << "    }\n  }\n";
         }
-    } else if (elim) {  // fused: V_r = R_r + sum_x ... stays in this wave's registers
-        for (int r = r0; r < r1; ++r) {
-            os << "  {\n    const unsigned char *rp = lh_slot(slv, " << k + r << ", base, zero);\n";
-            for (int y = 0; y < 8; ++y)
-                os << "    a" << (r - r0) << "_" << y << " ^= lh_ld(rp + " << y * c.sub << ");\n";
-            os << "  }\n";
-        }
-        // Phase B, 8 outputs at a time: this wave's share sum_{r in its rows} B(coef[i][r]) V_r
-        // of outputs i = ob .. ob + 7 (the computed-jump multiply of inv_jump.inc, one table
-        // build per row), XORed into the workgroup's LDS tile lv[8 outputs][8 sub-rows][64
-        // lanes]; after a barrier each wave stores and clears outputs ob + g, ob + g + NG, ...
-        const int NGt = (m + R - 1) / R, coef_off = 16 + std::min(k, m) + k + m;
-        os << "  const int lnb = threadIdx.x & 63;\n"
-           << "  const int e = pl[0];\n"
-           << "  for (int ob = 0; ob < e; ob += 8) {  // workgroup-uniform\n"
-           << "    unsigned cpk0 = 0, cpk1 = 0;  // lane r: coefficients of outputs ob .. ob + 7 for row r\n"
-           << "    if (lnb < " << m << ") {\n"
-           << "#pragma unroll\n      for (int i = 0; i < 8; ++i)\n"
-           << "        if (ob + i < e) {\n"
-           << "          const unsigned cb = (unsigned)pl[" << coef_off << " + (ob + i) * " << m << " + lnb] << (8 * (i & 3));\n"
-           << "          if (i < 4) cpk0 |= cb; else cpk1 |= cb;\n"
-           << "        }\n    }\n"
-           << "    unsigned acc[8][8];\n"
-           << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n#pragma unroll\n      for (int y = 0; y < 8; ++y) acc[i][y] = 0;\n";
-        if (fgt)  // lane r: the body address of output ob + i for row r (coefficient 0 past e: body 0)
-            os << "    unsigned tg[8];\n"
-               << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n"
-               << "      tg[i] = glo + (((i < 4 ? cpk0 : cpk1) >> (8 * (i & 3))) & 0xFFu) * 68u;\n";
-        for (int r = r0; r < r1; ++r) {
-            const std::string a = "a" + std::to_string(r - r0) + "_";
-            // the pin orders this row's table build after the previous row's multiply (both
-            // volatile): otherwise the scheduler hoists every row's tables and they all live at once
-            os << "    if (__builtin_amdgcn_readlane((int)slv[" << (k + r) / 64 << "], " << (k + r) % 64 << ") != 0xFF) {\n"
-               << "      asm volatile(\"\" :";
-            for (int y = 0; y < 8; ++y) os << (y ? ", " : " ") << "\"+v\"(" << a << y << ")";
-            os << ");\n"
-               << "      unsigned tl[16], th[16];\n      tl[0] = th[0] = 0;\n";
-            for (int q = 1; q < 16; ++q) {
-                const int low = __builtin_ctz(q), pre = q & (q - 1);
-                os << "      tl[" << q << "] = " << (pre ? "tl[" + std::to_string(pre) + "] ^ " : "") << a << low << ";\n"
-                   << "      th[" << q << "] = " << (pre ? "th[" + std::to_string(pre) + "] ^ " : "") << a << 4 + low << ";\n";
-            }
-            if (fgt)
-                os << "      lh_mul8g<" << r << ">(acc, tl, th, tg, ghi);\n    }\n";
-            else
-                os << "      lh_mul8((unsigned)__builtin_amdgcn_readlane((int)cpk0, " << r << "), "
-                   << "(unsigned)__builtin_amdgcn_readlane((int)cpk1, " << r << "), acc, tl, th);\n    }\n";
-        }
-        os << "#pragma unroll\n    for (int i = 0; i < 8; ++i)\n"
-           << "      if (ob + i < e)\n"
-           << "#pragma unroll\n        for (int y = 0; y < 8; ++y) __hip_atomic_fetch_xor(&lv[(i * 8 + y) * 64 + lnb], acc[i][y],\n"
-           << "                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
-           << "    __syncthreads();  // every wave's share of this batch is in the tile\n"
-           << "    for (int i = " << g << "; i < 8 && ob + i < e; i += " << NGt << ") {\n"
-           << "      unsigned char *dst = base + (long long)pl[16 + ob + i] * " << c.bytes << ";\n"
-           << "#pragma unroll\n      for (int y = 0; y < 8; ++y) {\n"
-           << "        lh_st(dst + " << "y * " << c.sub << ", lv[(i * 8 + y) * 64 + lnb]);\n"
-           << "        lv[(i * 8 + y) * 64 + lnb] = 0u;\n      }\n    }\n"
-           << "    __syncthreads();  // the tile is clear for the next batch\n"
-           << "  }\n";
     } else if (c.ptr) {
         for (int r = r0; r < r1; ++r) {
             os << "  {\n    unsigned char *op = lh_pp(otl, " << r << ") + loff;\n";
@@ -419,11 +290,7 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
 // Large-m decode modules (m <= 64, one workgroup per (stripe, 64 * W-byte column chunk)):
 // phase A (V_r = R_r + sum_{x present} B(G[r][x]) D_x, windowed network above, slot maps
 // from the stripe's plan held in VGPR lanes and read with v_readlane).
-//  split (default): V_r written back in place of R_r; phase B is lh_inverse_gt_kernel.
-//  fused (LONGHAIR_AMD_WIN_SPLIT=0, round 4): V stays in the registers of the wave that
-//   computed it and every wave adds its rows' share of each output into an LDS tile of 8
-//   outputs (emit_win_group): no V round trip through HBM and a 16 KiB tile instead of
-//   round 3's m x 2 KiB V tile.
+// V_r is written back in place of R_r; phase B is lh_inverse_gt_kernel (kernels.hip).
 static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::vector<uint8_t> &G) {
     const int R = c.rows_per_wave, NG = (c.m + R - 1) / R, CPS = c.sub / (64 * c.W);
     const int e_max = std::min(c.k, c.m), km = c.k + c.m;
@@ -432,28 +299,6 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
        << "    const unsigned char *base, const unsigned char *zero) {\n"
        << "  const unsigned int s = (unsigned int)__builtin_amdgcn_readlane((int)slv[i / 64], i % 64);\n"
        << "  return s == 0xFFu ? zero : base + (long long)s * " << c.bytes << ";\n}\n";
-    if (c.win_split != 1) {
-        // The computed-jump multiply (inv_jump.inc, the in-asm table reached by GPR indexing,
-        // the 8 accumulators of each output pinned to v[40 + 8i ..]).
-        os << lh_inv_jump_source;
-        os << "__device__ __forceinline__ void lh_mul8(unsigned c0, unsigned c1, unsigned (&a)[8][8],\n"
-           << "    const unsigned (&tl)[16], const unsigned (&th)[16]) {\n"
-           << "  asm volatile(LH_INV_JUMPI8_ASM : LH_INV_JUMPI8_OUTS(a) : [c0] \"s\"(c0), [c1] \"s\"(c1),\n"
-           << "               LH_INV_JUMPI_INS(tl, th) : \"s88\", \"s89\", \"s90\", \"s91\", \"s92\", \"s93\", \"s94\",\n"
-           << "               \"s95\", \"s96\", \"s97\", \"scc\");\n}\n";
-    }
-    if (c.win_split == 2) {
-        // The 256 bodies once in this code object (never-launched holder kernel, hidden symbol
-        // lh_inv_gtab), entered per output by v_readlane + s_set_gpr_idx_idx + s_swappc
-        // (kernels.hip lh_inverse_gt_kernel; tables pinned to v8..v38, accumulators v40..v103).
-        // (the row is a literal lane select here: an inline constant of v_readlane)
-        os << "__global__ void lh_inv_gtab_holder() { asm volatile(LH_INV_GTAB_TEXT); }\n"
-           << "template <int R>\n"
-           << "__device__ __forceinline__ void lh_mul8g(unsigned (&acc)[8][8], const unsigned (&tl)[16],\n"
-           << "    const unsigned (&th)[16], const unsigned (&t)[8], unsigned hi) {\n"
-           << "  asm volatile(LH_INV_JUMPG8_ASM : LH_INV_JUMPG8_OUTS(acc) : LH_INV_JUMPG_INS(tl, th, t), [r] \"n\"(R),\n"
-           << "               [hi] \"s\"(hi) : \"s92\", \"s93\", \"s94\", \"s95\", \"s97\", \"scc\");\n}\n";
-    }
     for (int g = 0; g < NG; ++g) emit_win_group(os, c, G, g);
     if (c.ptr) {
         // blocks: the pointer table, k slot pointers per stripe (row stride `stride` bytes)
@@ -487,7 +332,6 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
        << "lh_jit_decode_wide(unsigned char *__restrict__ blocks, long long stride,\n"
        << "                   const unsigned char *__restrict__ plan, long long plan_stride,\n"
        << "                   const unsigned char *__restrict__ zero_page, int stripes) {\n";
-    if (c.win_split != 1) os << "  __shared__ unsigned int lv[8 * 8 * 64];  // phase B: 8 outputs x 8 sub-rows x 64 lanes\n";
     os << "  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
        << "  const int lane = threadIdx.x & 63;\n"
        << "  const long long stripe = blockIdx.x / " << CPS << ";\n"
@@ -500,31 +344,10 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
        << "    slv[q] = i < " << km << " ? (unsigned int)pl[" << 16 + e_max << " + i] : 0xFFu;\n"
        << "  }\n"
        << "  const int chunk = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << ";\n"
-       << "  unsigned char *b = blocks + stripe * stride + chunk + lane * " << c.W << ";\n"
-       << "  const unsigned char *z = zero_page + chunk + lane * " << c.W << ";\n";
-    if (c.win_split != 1)
-        os << "  for (int i = threadIdx.x; i < 8 * 8 * 64; i += blockDim.x) lv[i] = 0u;\n"
-           << "  __syncthreads();\n";
-    std::string gargs;
-    if (c.win_split == 2) {
-        // the table's address (PC-relative); a table straddling a 4 GiB boundary cannot be
-        // reached with one high word: then the in-asm table (LONGHAIR_AMD_WIN_SPLIT=0) is the way
-        os << "  unsigned glo, ghi;\n"
-           << "  asm volatile(\"s_getpc_b64 s[92:93]\\n\"\n"
-           << "               \"s_add_u32 s92, s92, lh_inv_gtab@rel32@lo+4\\n\"\n"
-           << "               \"s_addc_u32 s93, s93, lh_inv_gtab@rel32@hi+12\\n\"\n"
-           << "               \"s_mov_b32 %0, s92\\n\"\n"
-           << "               \"s_mov_b32 %1, s93\\n\" : \"=s\"(glo), \"=s\"(ghi) : : \"s92\", \"s93\", \"scc\");\n"
-           << "  if (glo > 0xFFFFFFFFu - 256u * 68u) __builtin_trap();\n";
-        gargs = ", glo, ghi";
-    }
-    const std::string lvarg = c.win_split == 1 ? "nullptr" : "lv";
-    std::string dargs = "(b, z, slv, " + lvarg + ", pl" + gargs + ")";
-    if (c.win_lds) {
-        os << "  const unsigned char *sb = blocks + stripe * stride + chunk;\n"
-           << "  const unsigned char *zb = zero_page + chunk;\n";
-        dargs = "(b, z, slv, " + lvarg + ", pl, sb, zb" + gargs + ")";
-    }
+       << "  unsigned char *b = blocks + stripe * stride + chunk + lane * " << c.W << ";\n";
+    os << "  const unsigned char *sb = blocks + stripe * stride + chunk;\n"
+       << "  const unsigned char *zb = zero_page + chunk;\n";
+    const std::string dargs = "(b, slv, pl, sb, zb)";
     for (int g = 0; g < NG; ++g) os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << dargs << ";\n";
     os << "}\n";
 }
@@ -570,10 +393,8 @@ static std::string win_source_for(const JitConfig &c) {
            << "#pragma unroll\n  for (int q = 0; q < N; ++q) t[q] = q * 64 + lane < n ? row[q * 64 + lane] : 0ull;\n}\n";
     // One __shared__ object per LDS ring slot: the compiler's LDS-DMA wait tracking tells
     // distinct objects apart, so reading tile x % D does not wait for the DMA into another.
-    if (c.win_lds)
-        for (int q = 0; q <= c.win_pf; ++q)
-            os << "__shared__ __attribute__((aligned(16))) unsigned char tile" << q << "["
-               << (c.win_lds == 2 ? 2048 * NG : 2048) << "];\n";
+    for (int q = 0; q <= c.win_pf; ++q)
+        os << "__shared__ __attribute__((aligned(16))) unsigned char tile" << q << "[2048];\n";
     // LH_PINn: keep the accumulators in registers between columns (no re-association).
     // One asm statement per row (8 operands): every volatile asm is a memory side effect
     // to LLVM, and the IR sinking pass's cost grows with their number times the loads of
@@ -621,12 +442,9 @@ static std::string win_source_for(const JitConfig &c) {
        << c.W << ";\n"
        << "  const unsigned char *b = in + stripe * in_stride + p;\n"
        << "  unsigned char *o = out + stripe * out_stride + p;\n";
-    const char *eargs = "(b, o)";
-    if (c.win_lds) {
-        os << "  const unsigned char *sb = in + stripe * in_stride + (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W
-           << ";\n";
-        eargs = "(b, o, sb, nullptr)";
-    }
+    os << "  const unsigned char *sb = in + stripe * in_stride + (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W
+       << ";\n";
+    const char *eargs = "(b, o, sb, nullptr)";
     for (int g = 0; g < NG; ++g) os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << eargs << ";\n";
     os << "}\n";
     return os.str();
@@ -665,8 +483,6 @@ std::string jit_source_for(const JitConfig &c) {
        << "\n#define LH_SUB " << c.sub << "\n#define LH_W " << c.W << "\n#define LH_NCH " << c.nch
        << "\n#define LH_SPW " << (c.spw ? c.spw : 1) << "\n#define LH_WPS " << (c.wps ? c.wps : 1) << "\n";
     if (c.ptr) os << "#define LH_PTR 1\n#define LH_BUF 0\n";
-    if (c.al == 1) os << "#define LH_AL 1\n";
-    if (c.al == 2) os << "#define LH_ALS 1\n";
     const std::vector<uint8_t> g = generator_matrix(c.k, c.m);
     os << "static constexpr unsigned char LH_BM[" << c.m << "][" << c.k << "][8] = {";
     for (int r = 0; r < c.m; ++r) {
@@ -693,7 +509,7 @@ std::string jit_source_for(const JitConfig &c) {
 
 JitCache::Key JitCache::key_of(const JitConfig &cfg) {
     return Key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines,
-               cfg.ptr * 100000000 + cfg.al * 10000000 + cfg.win_split * 1000000 + cfg.win * 100000 + cfg.win_lds * 10000 +
+               cfg.ptr * 100000000 + cfg.win_split * 1000000 + cfg.win * 100000 + cfg.win_lds * 10000 +
                    cfg.rows_per_wave * 100 + cfg.win_pf);
 }
 
@@ -775,44 +591,87 @@ JitMode batch_jit_mode() {
     return (s && std::string(s) == "1") ? JitMode::kBlocking : JitMode::kAsync;
 }
 
-// Background compilations: joined by jit_join_background(), and at process exit by the
-// registry's destructor (a function-local static, constructed after hiprtc's own state and
-// so destroyed before it: no compile thread outlives the library it calls).
+// Background compilations run on ONE long-lived worker thread fed by a queue (round 5,
+// a thread per compilation stayed mapped until process exit, so a process meeting
+// many shapes grew without bound).  The worker is started by the first background request.
+// Exit: the worker registers a drain handler with atexit() right after its first hiprtc
+// compilation returns, i.e. after hiprtc has created its own lazily constructed state, so at
+// exit the handler (run in reverse order of registration) drops the queued requests and waits
+// for the one in flight while hiprtc is still intact.  (A compilation still in flight when
+// the process exits before the first one ever finished is the one case the handler cannot
+// cover: then the worker is detached by the registry's destructor.)
 namespace {
-struct CompileThreads {
+struct CompileWorker {
     std::mutex mu;
-    std::vector<std::thread> threads;
-    ~CompileThreads() { join(); }
-    void join() {
-        std::vector<std::thread> t;
+    std::condition_variable cv, idle_cv;
+    std::deque<std::function<void()>> q;
+    std::thread th;
+    bool busy = false, stop = false, drain_registered = false;
+    void post(std::function<void()> f) {
+        std::lock_guard<std::mutex> g(mu);
+        if (stop) return;  // exiting: the request stays pending, its shape on the generic kernels
+        q.push_back(std::move(f));
+        if (!th.joinable()) th = std::thread([this] { run(); });
+        cv.notify_one();
+    }
+    void run() {
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> l(mu);
+                cv.wait(l, [&] { return stop || !q.empty(); });
+                if (q.empty()) return;  // stop requested and nothing left
+                f = std::move(q.front());
+                q.pop_front();
+                busy = true;
+            }
+            f();
+            bool reg = false;
+            {
+                std::lock_guard<std::mutex> g(mu);
+                busy = false;
+                if (!drain_registered) reg = drain_registered = true;
+            }
+            if (reg) std::atexit(drain_at_exit);
+            idle_cv.notify_all();
+        }
+    }
+    // Wait until every queued request has run (jit_join_background).
+    void wait_idle() {
+        std::unique_lock<std::mutex> l(mu);
+        idle_cv.wait(l, [&] { return q.empty() && !busy; });
+    }
+    // Drop queued requests, let the one in flight finish, end the worker.
+    void shutdown() {
         {
             std::lock_guard<std::mutex> g(mu);
-            t.swap(threads);
+            stop = true;
+            q.clear();
         }
-        for (auto &th : t)
-            if (th.joinable()) th.join();
+        cv.notify_all();
+        if (th.joinable() && th.get_id() != std::this_thread::get_id()) th.join();
+    }
+    static void drain_at_exit();
+    ~CompileWorker() {
+        std::lock_guard<std::mutex> g(mu);
+        stop = true;
+        q.clear();
+        if (th.joinable()) th.detach();  // (see above: only reached with a first compile in flight)
     }
 };
-CompileThreads &compile_threads() {
-    static CompileThreads r;
-    return r;
+CompileWorker &compile_worker() {
+    static CompileWorker w;
+    return w;
 }
+void CompileWorker::drain_at_exit() { compile_worker().shutdown(); }
 }  // namespace
 
-void jit_join_background() { compile_threads().join(); }
+void jit_join_background() { compile_worker().wait_idle(); }
 
 bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::string *err, bool fresh, bool compile) {
     const std::string src = jit_source_for(cfg);
     const std::string path = cache_path(src);
     if (fresh && !path.empty()) unlink(path.c_str());  // a cached object the loader rejected
-    if (const char *dump = std::getenv("LONGHAIR_AMD_DUMP_SRC")) {  // tuning aid: the generated source
-        const std::string p = std::string(dump) + "/lh_" + std::to_string(cfg.k) + "_" + std::to_string(cfg.m) + "_" +
-                              std::to_string(cfg.bytes) + "_w" + std::to_string(cfg.win) + ".hip";
-        if (FILE *f = fopen(p.c_str(), "w")) {
-            fwrite(src.data(), 1, src.size(), f);
-            fclose(f);
-        }
-    }
     if (!path.empty()) {
         if (FILE *f = fopen(path.c_str(), "rb")) {
             fseek(f, 0, SEEK_END);
@@ -952,8 +811,7 @@ const JitKernels *JitCache::get(const JitConfig &cfg, std::string *err, JitMode 
             if (mode == JitMode::kAsync) {
                 // hiprtc only (no device calls) on the worker; the module is loaded by the
                 // first lookup after it finishes.
-                std::lock_guard<std::mutex> tg(compile_threads().mu);
-                compile_threads().threads.emplace_back([p, cfg] {
+                compile_worker().post([p, cfg] {
                     std::vector<char> code;
                     std::string e;
                     const bool ok = compile_code_object(cfg, &code, &e, false, true);

@@ -24,10 +24,9 @@ struct JitConfig {
     int win = 0;          // 1: windowed encode module, 2: windowed decode phase-A module
     int rows_per_wave = 8;
     int win_pf = 3;       // windowed modules: columns in flight ahead of the one combined
-    int win_lds = 1;      // windowed modules: stage column tiles in LDS by LDS-DMA (0: per-wave loads)
+    int win_lds = 1;      // windowed modules: column tiles staged in LDS by LDS-DMA (the only form since round 5)
     int win_split = 1;    // windowed decode: phase A writes V in place, lh_inverse_gt_kernel does phase B
                           // (0: the fused kernel, phase B from an LDS tile of V)
-    int al = 0;           // register networks: 2 aligned output stores (LH_ALS), 1 aligned column loads (LH_AL)
     int ptr = 0;          // register networks: blocks addressed through a pointer table (LH_PTR,
                           // cauchy_256_*_batch_ptrs)
     int lanes_per_launch_unit() const { return 64; }

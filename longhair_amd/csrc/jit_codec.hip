@@ -205,140 +205,14 @@ struct lh_col_net {
         }
     }
 };
-#ifndef LH_NET_PROBE
-#define LH_NET_PROBE 0  // timing probe only (tools/tune.py): one XOR per sub-block instead of the network
-#endif
 template <int X>
 __device__ __forceinline__ void lh_column(lh_word (&acc)[LH_M][8], const lh_word (&d)[8]) {
-#if LH_NET_PROBE
-#pragma unroll
-    for (int y = 0; y < 8; ++y) lh_xor(acc[X % LH_M][y], d[y]);
-#else
     lh_col_net<X>::run(acc, d);
-#endif
 }
-
-// LH_AL = 1 (a knob, jit.cpp: W = 8, whole stripes per wave, sub % 8 in {1, 2, 4}):
-// aligned column loads.  Sub-block b of a block starts (b * sub) % 8 = S_b bytes past an
-// 8-byte boundary, so a lane's 8 bytes [p, p + 8) of it straddle two aligned words: every
-// lane loads the aligned word at p - S_b and takes the bytes it lacks from the next lane's
-// word (DPP wave_shl:1, one v_mov per dword, then v_alignbyte; S_b is a compile-time
-// constant per b).  Lanes own p = 8c; the last lane of a stripe (c = nch - 1) holds only
-// LH_VLAST valid bytes, which its own word supplies (the host checks LH_VLAST + S_b <= 8), and
-// stores [sub - 8, sub) assembled with the previous lane's word (DPP wave_shr:1).  The same
-// bytes as 2-byte-aligned 8-byte loads (LH_AL = 0), with 8-byte-aligned load addresses.
-// Off by default: the realignment costs more than the misaligned loads (the k29/m4 access
-// pattern 0.554 against 0.530 ms, tools/ubench_floor.hip, profiles/r4c_ubench_floor_enc.txt).
-#ifndef LH_AL
-#define LH_AL 0
-#endif
-// LH_ALS = 1 (with LH_AL = 0; jit.cpp, a knob): the outputs are stored as
-// 8-byte-aligned words.  Lanes own p = 8c, the last lane of a stripe p = sub - 8 (its chunk
-// overlaps the previous one).  In store instruction y, lane c stores the aligned word at
-// y * sub - S_y + 8c of the block (S_y = (y * sub) % 8): bytes 8 - S_y .. 7 of lane c - 1's
-// chunk, then bytes 0 .. 7 - S_y of its own, gathered with ds_bpermute; lane 0 takes the
-// previous sub-block's last S_y bytes from its stripe's last lane, which shares its chunk of
-// that sub-block (exactly its last 8 bytes).  The last lane stores its own chunk when it is
-// the aligned word (S_y = 8 - LH_VLAST) and otherwise nothing: the next instruction's lane 0
-// covers that word (an out-of-range buffer offset drops the store).  Every aligned word of
-// the block is stored once when LH_VLAST + max S_y <= 8, which the host checks.  Off by
-// default (LONGHAIR_AMD_JIT_ALS=1): k29/m4 encode 0.591 against 0.563 ms, decode equal
-// (profiles/r4d_tune_k29m4.txt; the gathers cost the encode a wave per SIMD).
-#ifndef LH_ALS
-#define LH_ALS 0
-#endif
-#if LH_AL || LH_ALS
-#if LH_W != 8 || LH_NCH > 64
-#error "LH_AL / LH_ALS need 8-byte lanes and whole stripes per wave"
-#endif
-#define LH_VLAST (LH_SUB - 8 * (LH_NCH - 1))  // valid bytes of the last chunk of a stripe
-// Bytes [S, S + 8) of the 16 bytes d[0..3] (little endian), S a compile-time constant.
-template <int S>
-__device__ __forceinline__ lh_word lh_funnel(unsigned int d0, unsigned int d1, unsigned int d2, unsigned int d3) {
-    const unsigned int d[4] = {d0, d1, d2, d3};
-    constexpr int a = S / 4, r = S % 4;
-    lh_word w;
-    if constexpr (r == 0) {
-        w.v[0] = d[a];
-        w.v[1] = d[a + 1];
-    } else {
-        w.v[0] = __builtin_amdgcn_alignbyte(d[a + 1], d[a], r);
-        w.v[1] = __builtin_amdgcn_alignbyte(d[a + 2], d[a + 1], r);
-    }
-    return w;
-}
-#endif
-#if LH_AL && LH_ALS
-#error "LH_ALS assumes the 2-byte-aligned load mapping (LH_AL = 0)"
-#endif
-#if LH_AL
-__device__ __forceinline__ unsigned int lh_dpp_next(unsigned int v) {  // lane i <- lane i + 1
-    return (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
-}
-__device__ __forceinline__ unsigned int lh_dpp_prev(unsigned int v) {  // lane i <- lane i - 1
-    return (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
-}
-// Sub-block B's word loaded from its aligned floor -> the lane's bytes [p, p + 8).
-template <int B>
-__device__ __forceinline__ lh_word lh_realign(const lh_word &w) {
-    constexpr int S = (B * LH_SUB) % 8;
-    if constexpr (S == 0) {
-        return w;
-    } else {
-        // only the next lane's dwords the funnel reads are moved
-        const unsigned int n0 = lh_dpp_next(w.v[0]);
-        const unsigned int n1 = (S > 4) ? lh_dpp_next(w.v[1]) : 0u;
-        return lh_funnel<S>(w.v[0], w.v[1], n0, n1);
-    }
-}
-// The word a lane stores: its own, or for the last lane of a stripe the 8 bytes ending at
-// the sub-block's end (the previous lane's bytes LH_VLAST..7, then its own 0..LH_VLAST-1).
-__device__ __forceinline__ lh_word lh_store_word(const lh_word &w, bool last) {
-    const unsigned int p0 = lh_dpp_prev(w.v[0]), p1 = lh_dpp_prev(w.v[1]);
-    const lh_word f = lh_funnel<LH_VLAST>(p0, p1, w.v[0], w.v[1]);
-    lh_word o;
-    o.v[0] = last ? f.v[0] : w.v[0];
-    o.v[1] = last ? f.v[1] : w.v[1];
-    return o;
-}
-#endif
-#if LH_ALS
-#if !LH_BUF
-#error "LH_ALS stores through buffer resources"
-#endif
-template <int AUX>
-__device__ __forceinline__ void lh_store_buf(const lh_word &w, const __amdgpu_buffer_rsrc_t &rs, int off) {
-    const lh_u32x2 v = {w.v[0], w.v[1]};
-    __builtin_amdgcn_raw_buffer_store_b64(v, rs, off, 0, AUX);
-}
-// One block (8 sub-row words: the lane's chunk of each sub-block) at byte offset `blk` of
-// the resource.  c: the lane's chunk; src: lane c - 1, or for c = 0 its stripe's last lane.
-template <int AUX, int Y = 0>
-__device__ __forceinline__ void lh_store_block_al(const __amdgpu_buffer_rsrc_t &rs, int blk, int c, int src,
-                                                  const lh_word (&w)[8]) {
-    if constexpr (Y < 8) {
-        constexpr int S = (Y * LH_SUB) % 8;
-        const bool last = c == LH_NCH - 1;
-        lh_word word = w[Y];
-        if constexpr (S != 0) {
-            const lh_word &sh = last ? w[Y - 1] : w[Y];
-            const unsigned int p0 = (unsigned int)__builtin_amdgcn_ds_bpermute(src * 4, (int)sh.v[0]);
-            const unsigned int p1 = (unsigned int)__builtin_amdgcn_ds_bpermute(src * 4, (int)sh.v[1]);
-            const lh_word f = lh_funnel<8 - S>(p0, p1, w[Y].v[0], w[Y].v[1]);
-            word.v[0] = last ? w[Y].v[0] : f.v[0];
-            word.v[1] = last ? w[Y].v[1] : f.v[1];
-        }
-        const bool skip = last && S != 8 - LH_VLAST;
-        lh_store_buf<AUX>(word, rs, skip ? (int)0x80000000 : blk + Y * LH_SUB - S + 8 * c);
-        lh_store_block_al<AUX, Y + 1>(rs, blk, c, src, w);
-    }
-}
-#endif
 
 struct lh_lane {
     long long stripe;
-    int p;       // first byte of the lane's chunk in every sub-block (loads)
-    int ps;      // first byte the lane stores (LH_AL: the last lane stores [sub - 8, sub))
+    int p;       // first byte of the lane's chunk in every sub-block
     bool last;   // last chunk of its stripe
     bool active;
 };
@@ -371,13 +245,7 @@ __device__ __forceinline__ lh_lane lh_map_lane(int stripes, long long wave) {
     l.active = (c0 < LH_NCH) && (l.stripe < stripes);
 #endif
     l.last = c == LH_NCH - 1;
-#if LH_AL
-    l.p = c * LH_W;
-    l.ps = l.last ? LH_SUB - LH_W : l.p;
-#else
     l.p = l.last ? (LH_SUB - LH_W) : c * LH_W;
-    l.ps = l.p;
-#endif
     return l;
 }
 
@@ -512,21 +380,11 @@ struct lh_esrc {
     __device__ __forceinline__ lh_word load(int x, int b) const {
         return lh_load_buf<LH_NT ? 2 : 0>(rs, lbase + b * LH_SUB, x * LH_BYTES);
     }
-#if LH_AL
-    template <int B>
-    __device__ __forceinline__ lh_word load_al(int x) const {
-        return lh_realign<B>(lh_load_buf<LH_NT ? 2 : 0>(rs, lbase + B * LH_SUB - (B * LH_SUB) % 8, x * LH_BYTES));
-    }
-#endif
+
     // The 8 sub-block words of column x.
     __device__ __forceinline__ void load8(lh_word (&d)[8], int x) const {
-#if LH_AL
-        d[0] = load_al<0>(x); d[1] = load_al<1>(x); d[2] = load_al<2>(x); d[3] = load_al<3>(x);
-        d[4] = load_al<4>(x); d[5] = load_al<5>(x); d[6] = load_al<6>(x); d[7] = load_al<7>(x);
-#else
 #pragma unroll
         for (int b = 0; b < 8; ++b) d[b] = load(x, b);
-#endif
     }
 #elif LH_PTR
     const unsigned long long *pt;  // LDS: the lane's stripe's LH_K block pointers
@@ -550,9 +408,6 @@ struct lh_esrc {
     }
 #endif
 };
-#if LH_AL && !LH_BUF
-#error "LH_AL loads through buffer resources"
-#endif
 
 // Column loop, unrolled at compile time, with the next LH_PF columns' loads in flight
 // while column X is combined.
@@ -615,43 +470,22 @@ __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned ch
     for (int q = 0; q < LH_PF; ++q)
         if (q < LH_K) S.load8(ring[q], q);
     lh_unroll_encode<0>::run(acc, ring, S);
-#if LH_ALS
-    {
-        const long long s0o = (long long)__builtin_amdgcn_readfirstlane((int)wave) * LH_SPW;
-        const long long nso = (stripes - s0o) < LH_SPW ? (stripes - s0o) : LH_SPW;
-        if (nso * out_stride < (1ll << 31)) {  // wave-uniform: the outputs in one 32-bit range
-            const __amdgpu_buffer_rsrc_t ro =
-                __builtin_amdgcn_make_buffer_rsrc(out + s0o * out_stride, 0, (int)(nso * out_stride), 0x00020000);
-            const int lane = threadIdx.x & 63, c = lane % LH_NCH;
-            const int src = c == 0 ? lane + LH_NCH - 1 : lane - 1;
-            const int so = (int)((l.stripe - s0o) * out_stride);
-#pragma unroll
-            for (int r = 0; r < LH_M; ++r) lh_store_block_al<LH_NT_ST ? 2 : 0>(ro, so + r * LH_BYTES, c, src, acc[r]);
-            return;
-        }
-    }
-#endif
 #if LH_PTR
     // out: the recovery blocks' pointer table, LH_M per stripe (row stride out_stride bytes)
     const unsigned long long *ot = (const unsigned long long *)(out + l.stripe * out_stride);
 #pragma unroll
     for (int r = 0; r < LH_M; ++r) {
-        unsigned char *o = (unsigned char *)ot[r] + l.ps;
+        unsigned char *o = (unsigned char *)ot[r] + l.p;
 #pragma unroll
         for (int y = 0; y < 8; ++y) lh_store(o + y * LH_SUB, acc[r][y]);
     }
     return;
 #endif
-    unsigned char *o = out + l.stripe * out_stride + l.ps;
+    unsigned char *o = out + l.stripe * out_stride + l.p;
 #pragma unroll
     for (int r = 0; r < LH_M; ++r)
 #pragma unroll
-        for (int y = 0; y < 8; ++y)
-#if LH_AL
-            lh_store(o + (long long)r * LH_BYTES + y * LH_SUB, lh_store_word(acc[r][y], l.last));
-#else
-            lh_store(o + (long long)r * LH_BYTES + y * LH_SUB, acc[r][y]);
-#endif
+        for (int y = 0; y < 8; ++y) lh_store(o + (long long)r * LH_BYTES + y * LH_SUB, acc[r][y]);
 }
 
 #if 1
@@ -724,15 +558,8 @@ struct lh_dsrc {
 template <bool NT = (LH_NT_DEC == 1)>
 __device__ __forceinline__ void lh_load_col(lh_word (&d)[8], const lh_dsrc &S, unsigned int slot) {
     const int off = S.col(slot);
-#if LH_AL
-    // an absent column's offset is out of range: zeros, and so are its neighbours' words
-#define LH_ALD(B) d[B] = lh_realign<B>(lh_load_buf<NT ? 2 : 0>(S.rs, off + (B * LH_SUB - (B * LH_SUB) % 8)))
-    LH_ALD(0); LH_ALD(1); LH_ALD(2); LH_ALD(3); LH_ALD(4); LH_ALD(5); LH_ALD(6); LH_ALD(7);
-#undef LH_ALD
-#else
 #pragma unroll
     for (int b = 0; b < 8; ++b) d[b] = lh_load_buf<NT ? 2 : 0>(S.rs, off + b * LH_SUB);
-#endif
 }
 #else
 // Column source of a lane: its stripe's chunk pointer (LH_PTR: its stripe's block pointers
@@ -885,9 +712,6 @@ __device__ __forceinline__ void lh_dec_phase_a(lh_word (&v)[LH_M][8], lh_word (&
 // Phase B: D_{E_i} = sum_r B(coef[i][r]) V_r with the per-stripe inverse, by Horner over
 // the coefficient bits: B(c) v = B(2)(...B(2)(c_7 v)...) + c_0 v, one v_bitop3 masked XOR
 // per (row, bit, sub-row); the recovered blocks go to the plan's output slots.
-#ifndef LH_PB_PROBE
-#define LH_PB_PROBE 0  // timing probe only (tools/tune.py): V_i stored as output i, no phase-B XORs
-#endif
 struct lh_dsrc;
 __device__ __forceinline__ void lh_dec_phase_b(const lh_word (&v)[LH_M][8], const lh_plan_regs &pr,
                                                unsigned char *base, bool last, const lh_dsrc &S, int soff) {
@@ -895,14 +719,6 @@ __device__ __forceinline__ void lh_dec_phase_b(const lh_word (&v)[LH_M][8], cons
     (void)S;
     (void)soff;
     const int e = pr.e;
-#if LH_PB_PROBE
-#pragma unroll
-    for (int i = 0; i < LH_EMAX; ++i)
-        if (i < e)
-#pragma unroll
-            for (int y = 0; y < 8; ++y) lh_store(base + (long long)LH_BYTE(pr.outw, i) * LH_BYTES + y * LH_SUB, v[i][y]);
-    return;
-#endif
     const unsigned int(&coefw)[LH_NCOEF] = pr.coefw;
     const unsigned int(&outw)[LH_NOUT] = pr.outw;
 #pragma unroll
@@ -940,26 +756,13 @@ __device__ __forceinline__ void lh_dec_phase_b(const lh_word (&v)[LH_M][8], cons
                 lh_pin8(o);
 #endif
             }
-#if LH_ALS
-            {  // in place through the wave's buffer resource (S.rs), aligned words
-                const int lane = threadIdx.x & 63, c = lane % LH_NCH;
-                lh_store_block_al<LH_NT_ST ? 2 : 0>(S.rs, soff + (int)LH_BYTE(outw, i) * LH_BYTES, c,
-                                                    c == 0 ? lane + LH_NCH - 1 : lane - 1, o);
-            }
-#else
 #if LH_PTR
             unsigned char *dst = (unsigned char *)S.pt[LH_BYTE(outw, i)] + soff;  // soff: the lane's store offset
 #else
             unsigned char *dst = base + (long long)LH_BYTE(outw, i) * LH_BYTES;
 #endif
 #pragma unroll
-            for (int y = 0; y < 8; ++y)
-#if LH_AL
-                lh_store(dst + y * LH_SUB, lh_store_word(o[y], last));
-#else
-                lh_store(dst + y * LH_SUB, o[y]);
-#endif
-#endif
+            for (int y = 0; y < 8; ++y) lh_store(dst + y * LH_SUB, o[y]);
         }
     }
 }
@@ -1010,11 +813,11 @@ __device__ __forceinline__ void lh_decode_body(const lh_lane &l, long long wave,
         lh_dec_phase_a<PF>(v, ring, pr, S);
     }
 #if LH_BUF
-    lh_dec_phase_b(v, pr, blocks + l.stripe * stripe_stride + l.ps, l.last, S, S.lbase - l.p);
+    lh_dec_phase_b(v, pr, blocks + l.stripe * stripe_stride + l.p, l.last, S, S.lbase - l.p);
 #elif LH_PTR
-    lh_dec_phase_b(v, pr, nullptr, l.last, S, l.ps);
+    lh_dec_phase_b(v, pr, nullptr, l.last, S, l.p);
 #else
-    lh_dec_phase_b(v, pr, blocks + l.stripe * stripe_stride + l.ps, l.last, S, 0);
+    lh_dec_phase_b(v, pr, blocks + l.stripe * stripe_stride + l.p, l.last, S, 0);
 #endif
 }
 

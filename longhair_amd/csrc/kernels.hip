@@ -1004,7 +1004,17 @@ __global__ void __launch_bounds__(256) lh_ptr_copy_kernel(lh::PtrCopyArgs a) {
     const long long s = item / a.ncopy;
     const int j = (int)(item - s * a.ncopy);
     const long long t = s * a.n + j;  // table entry
-    if (a.scatter && a.sel && a.sel[t] < a.sel_min) return;
+    if (a.scatter) {  // wave-uniform tests: the wave copies one block
+        if (a.status && a.status[s] != 0) return;
+        if (a.sel && a.m1) {
+            int out = 0;
+            for (int i = 0; i < a.n; ++i)
+                if (a.sel[s * a.n + i] >= a.sel_min) out = i;
+            if (j != out) return;
+        } else if (a.sel && a.sel[t] < a.sel_min) {
+            return;
+        }
+    }
     uint8_t *blk = a.ptrs[t];
     uint8_t *lin = a.chunk + s * a.stride + (long long)j * a.bytes;
     const uint8_t *src = a.scatter ? lin : blk;
@@ -1082,23 +1092,18 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
     // lh_inverse_gt_kernel: 8 outputs per wave, packed (wave g: outputs 8g .. 8g + 7) for
     // e_max <= 32 and spread (g, g + nw, ...) above (profiles/r3m_phase_b_gtab.txt: k128/m32
-    // decode 3.56 -> 3.51 ms packed, k200/m56 0.583 -> 0.567 spread).  Knobs:
-    //   LONGHAIR_AMD_INV_PACK=0|1      override the output distribution
-    //   LONGHAIR_AMD_INV_FALLBACK=1    the in-asm table inside the same kernel (tests)
+    // decode 3.56 -> 3.51 ms packed, k200/m56 0.583 -> 0.567 spread).
+    // LONGHAIR_AMD_INV_FALLBACK=1: the in-asm table inside the same kernel (tests).
     InverseArgs g = a;
-    const char *pk = std::getenv("LONGHAIR_AMD_INV_PACK");
     const char *fb = std::getenv("LONGHAIR_AMD_INV_FALLBACK");
-    g.pack = pk ? (std::atoi(pk) ? 1 : 0) : (a.e_max <= 32 ? 1 : 0);
+    g.pack = a.e_max <= 32 ? 1 : 0;
     g.jump_fallback = fb && std::atoi(fb) ? 1 : 0;
-    // Chunks per workgroup (LONGHAIR_AMD_INV_CHUNKS, default 2): a workgroup runs its tile
-    // pipeline across that many consecutive 2 KiB chunks of its stripe, so the pipeline's
-    // start (plan, jump targets, first tile's DMA) is paid once per pair of chunks
-    // (profiles/r4k_tune_*_inv_chunks.txt: k200/m56 decode 0.665 -> 0.617 ms with 2, 0.635 with
-    // 4; k128/m32 3.634 ms with 1, 2 or 4).
+    // Two consecutive 2 KiB chunks of a stripe per workgroup, the tile pipeline carried across
+    // them, so the pipeline's start (plan, jump targets, first tile's DMA) is paid once per
+    // pair (profiles/r4k_tune_*_inv_chunks.txt: k200/m56 decode 0.665 -> 0.617 ms with 2, 0.635
+    // with 4; k128/m32 3.634 ms with 1, 2 or 4).
     const int cps = a.bytes / 2048;
-    int cpw = 2;
-    if (const char *c = std::getenv("LONGHAIR_AMD_INV_CHUNKS")) cpw = std::atoi(c);
-    cpw = cpw < 1 ? 1 : (cpw > cps ? cps : cpw);
+    const int cpw = cps < 2 ? cps : 2;
     g.chunks_per_wg = cpw;
     const long long wgs = (long long)a.stripes * ((cps + cpw - 1) / cpw);
     hipLaunchKernelGGL(lh_inverse_gt_kernel, dim3((unsigned)wgs), dim3(64u * (unsigned)((a.e_max + 7) / 8)), 0, st, g);
@@ -1163,10 +1168,6 @@ hipError_t launch_plan(const PlanArgs &a, hipStream_t st) {
     // waves per stripe split the elimination's columns; many stripes: one wave each.
     const size_t lds = (size_t)2 * a.e_max * (a.e_max > 64 ? 128 : 64);
     unsigned threads = (a.stripes <= 4096 && a.e_max > 8) ? 256u : 64u;
-    if (const char *t = std::getenv("LONGHAIR_AMD_PLAN_THREADS")) {  // tuning knob: 64, 128 or 256
-        const int v = std::atoi(t);
-        if (v == 64 || v == 128 || v == 256) threads = (unsigned)v;
-    }
     hipLaunchKernelGGL(lh_plan_kernel, dim3((unsigned)a.stripes), dim3(threads), lds, st, a);
     note_launch(a.points ? "lh_plan_kernel(closed form)" : "lh_plan_kernel");
     return hipGetLastError();

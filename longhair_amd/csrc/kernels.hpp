@@ -132,15 +132,19 @@ struct WritebackArgs {
 
 // Pointer-table batches (cauchy_256_*_batch_ptrs) on the paths without a pointer form:
 // block j of stripe s lives at ptrs[s * n + j].  gather: into a contiguous chunk (stripe s,
-// block j at chunk + s * stride + j * bytes); scatter: back from it, only the blocks with
-// sel[s * n + j] >= sel_min when sel is set (decode: the slots that held recovery rows).
-// Only the first ncopy blocks of each stripe are copied.
+// block j at chunk + s * stride + j * bytes); scatter: back from it, only the blocks the
+// decode may have changed when sel is set (sel = the chunk's rows before the decode):
+// the slots with sel[s * n + j] >= sel_min (k, m > 1: the slots that held recovery rows), or
+// with m1 the one output slot of cauchy_decode_m1 (the last slot with a row >= k, else slot 0,
+// cauchy_256.cpp:487-535); and never a stripe whose status (when given) is non-zero (invalid
+// rows: the decode left it untouched).  Only the first ncopy blocks of each stripe are copied.
 struct PtrCopyArgs {
     uint8_t *const *ptrs;         // [stripe][n]
     uint8_t *chunk;
     long long stride;
     const uint8_t *sel;           // [stripe][n] or NULL
-    int sel_min;
+    const int8_t *status;         // [stripe] or NULL (scatter)
+    int sel_min, m1;
     int n, ncopy, bytes, stripes, scatter;
 };
 

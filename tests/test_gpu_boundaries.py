@@ -33,9 +33,10 @@ BOUNDARIES = [
     # fused in-kernel plan <-> separate planner: k <= 64
     ("k64-fused", 64, 4, 1296, 48, {}, ["lh_jit_encode"], FUSED),
     ("k65-planned", 65, 4, 1296, 48, {}, ["lh_jit_encode"], SMALL4),
-    # ... and one stripe per <= 64 lanes (nch = 64 with 8-byte lanes; 65 with W pinned to 8)
+    # ... and one stripe per <= 64 lanes (nch = 64 with 8-byte lanes; the decode of m = 3 at
+    # 8128-byte blocks takes 8-byte lanes too, nch = 127: two waves per stripe)
     ("nch64-fused", 8, 4, 4096, 24, {}, ["lh_jit_encode"], FUSED),
-    ("nch65-planned", 8, 4, 4160, 24, {"LONGHAIR_AMD_JIT_W": "8"}, ["lh_jit_encode"], SMALL4),
+    ("nch127-planned", 8, 3, 8128, 24, {}, ["lh_jit_encode"], SMALL4),
     # ... and e_max <= 4 (both sides of e_max = min(k, m) = 4 / 5, from k and from m)
     ("emax4-k", 4, 8, 64, 64, {}, ["lh_jit_encode"], FUSED),
     ("emax5-k", 5, 8, 64, 64, {}, ["lh_jit_encode"], SMALL8),
@@ -67,14 +68,12 @@ BOUNDARIES = [
 ]
 
 # Phase-B kernel (kernels.hip launch_inverse): one kernel, lh_inverse_gt_kernel, with its
-# outputs packed 8 per wave (default for e_max <= 32) or spread (default above), and its
-# in-asm-table fallback.  (Round 3's other six forms were removed in round 4.)
+# outputs packed 8 per wave (e_max <= 32) or spread (above), and its in-asm-table fallback.
+# (Round 3's other six forms were removed in round 4; the packing override in round 5.)
 PHASE_B = [
     ({}, 32, "lh_inverse_gt_kernel"),
     ({}, 33, "lh_inverse_gt_kernel"),
-    ({"LONGHAIR_AMD_INV_PACK": "0"}, 32, "lh_inverse_gt_kernel"),
-    ({"LONGHAIR_AMD_INV_PACK": "1"}, 33, "lh_inverse_gt_kernel"),
-    ({"LONGHAIR_AMD_INV_PACK": "1"}, 64, "lh_inverse_gt_kernel"),
+    ({}, 64, "lh_inverse_gt_kernel"),
     ({"LONGHAIR_AMD_INV_FALLBACK": "1"}, 32, "lh_inverse_gt_kernel(fallback)"),
     ({"LONGHAIR_AMD_INV_FALLBACK": "1"}, 33, "lh_inverse_gt_kernel(fallback)"),
     ({"LONGHAIR_AMD_INV_FALLBACK": "1"}, 64, "lh_inverse_gt_kernel(fallback)"),
@@ -166,13 +165,11 @@ def test_phase_b_variant(lh, oracle, monkeypatch, env, m, kernel):
     assert dec == ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", kernel], dec
 
 
-@pytest.mark.parametrize("chunks", ["1", "2", "3"])
-def test_phase_b_chunks_per_workgroup(lh, oracle, monkeypatch, chunks):
-    """Phase-B workgroups over consecutive 2 KiB chunks of a stripe (LONGHAIR_AMD_INV_CHUNKS,
-    the tile pipeline carried across chunks): 6144-byte blocks = 3 chunks, so 2 per
-    workgroup leaves a one-chunk remainder; against the oracle."""
-    monkeypatch.setenv("LONGHAIR_AMD_INV_CHUNKS", chunks)
-    enc, dec = roundtrip(lh, oracle, 40, 20, 6144, 7, seed=int(chunks) * 7)
+def test_phase_b_chunks_per_workgroup(lh, oracle):
+    """Phase-B workgroups over two consecutive 2 KiB chunks of a stripe (the tile pipeline
+    carried across them): 6144-byte blocks = 3 chunks, so the second workgroup of a stripe has
+    a one-chunk remainder; against the oracle."""
+    enc, dec = roundtrip(lh, oracle, 40, 20, 6144, 7, seed=14)
     assert dec == ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_gt_kernel"], dec
 
 
@@ -305,18 +302,6 @@ def test_capture_never_allocates(lh):
     torch.cuda.synchronize()
     assert int((status != 0).sum()) == 0
     assert torch.equal(blocks, data) and torch.equal(rows[0].cpu(), torch.arange(k, dtype=torch.uint8))
-
-
-@pytest.mark.parametrize("overlap", ["0", "1"])
-def test_wide_decode_in_stripe_chunks(lh, oracle, monkeypatch, overlap):
-    """The split large-m decode in stripe chunks (phase A then phase B per chunk; with
-    LONGHAIR_AMD_WIDE_OVERLAP=1 phase B of one chunk on a side stream beside phase A of the
-    next): chunks of 3 stripes over 10, so chunk edges fall inside the batch."""
-    monkeypatch.setenv("LONGHAIR_AMD_WIDE_CHUNK", "3")
-    monkeypatch.setenv("LONGHAIR_AMD_WIDE_OVERLAP", overlap)
-    for k, m, nbytes in ((40, 20, 4096), (40, 33, 2048)):
-        enc, dec = roundtrip(lh, oracle, k, m, nbytes, 10, seed=k + m + int(overlap))
-        assert dec[:2] == ["lh_plan_kernel(closed form)", "lh_jit_decode_wide"], dec
 
 
 @pytest.mark.parametrize("align", [128, 64])

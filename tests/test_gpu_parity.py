@@ -343,24 +343,6 @@ def test_decode_batch_vs_oracle(lh, oracle, path, k, m, nbytes, stripes, e):
     _decode_batch_vs_oracle(lh, oracle, k, m, nbytes, stripes, e)
 
 
-@pytest.mark.parametrize("split", ["0", "2"])
-@pytest.mark.parametrize("k,m,nbytes,stripes", [(40, 20, 4096, 8), (100, 16, 2048, 6), (128, 32, 8192, 4),
-                                                (200, 56, 65536, 3), (250, 6, 2048, 8)])
-def test_wide_decode_fused_variant(lh, oracle, monkeypatch, split, k, m, nbytes, stripes):
-    """Large-m decode with the fused phase A + B kernel (LONGHAIR_AMD_WIN_SPLIT=0: V in the
-    registers of the wave that computed it, each wave's share of 8 outputs at a time reduced
-    in an LDS tile; =2: the same with the multiply through the per-code-object jump table): the
-    launch trace shows that kernel ran and no separate phase B; random e up to e_max (several
-    8-output batches at m = 32 and 56).  (The phase-B kernel of the split form is tested in
-    test_gpu_boundaries.py.)"""
-    monkeypatch.setenv("LONGHAIR_AMD_WIN_SPLIT", split)
-    assert lh.batch_path(k, m, nbytes, True) == "jit-wide"
-    _decode_batch_vs_oracle(lh, oracle, k, m, nbytes, stripes, None)
-    trace = lh.last_launch()
-    assert len(trace) == 2 and trace[0].startswith("lh_plan_")
-    assert trace[1] == "lh_jit_decode_wide(fused phase B)"
-
-
 def _decode_batch_vs_oracle(lh, oracle, k, m, nbytes, stripes, e):
     import torch
     data = lhutil.fill(k + m + nbytes, stripes * k * nbytes).reshape(stripes, k, nbytes)
@@ -673,3 +655,25 @@ def test_planner_closed_form_matches_elimination(lh, oracle, monkeypatch, k, m, 
         rc, exp_rows = oracle.decode(k, m, bufs, list(rows[s]), nbytes)
         assert rc == 0 and list(outs[0][1][s]) == exp_rows
         assert all(outs[0][0][s, i].tobytes() == bufs[i].tobytes() for i in range(k)), s
+
+
+# Every knob of INTEGRATION.md section 6 that selects other kernel code has a parity test.
+# These cover the separate planner of the e_max <= 4 decode and the JIT_DEFINES tuning hook
+# (tools/precompile.py KNOB_JOBS compiles the variant modules at build time).
+KNOB_VARIANTS = [
+    ("nofused", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1"}, ["lh_plan_small_kernel<4>", "lh_jit_decode"]),
+    ("defines-pf2-nt0-noxcd", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=2,LH_NT=0,LH_XCD=0"}, ["lh_jit_decode_fused"]),
+    ("defines-recfirst0-pfdec2", {"LONGHAIR_AMD_JIT_DEFINES": "LH_REC_FIRST=0,LH_PF_DEC=2"}, ["lh_jit_decode_fused"]),
+]
+
+
+@pytest.mark.parametrize("name,env,dec_trace", KNOB_VARIANTS, ids=[v[0] for v in KNOB_VARIANTS])
+def test_kernel_knob_variants(lh, oracle, monkeypatch, name, env, dec_trace):
+    """k29/m4/1296 encode + decode through each knob's kernels, bytes and rewritten rows
+    against the oracle (random e per stripe, the first at e = 4, shuffled slots)."""
+    import test_gpu_boundaries as tb
+    for key, v in env.items():
+        monkeypatch.setenv(key, v)
+    enc, dec = tb.roundtrip(lh, oracle, 29, 4, 1296, 96, seed=sum(map(ord, name)))
+    assert enc == ["lh_jit_encode"], enc
+    assert dec == dec_trace, dec

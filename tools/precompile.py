@@ -21,8 +21,9 @@ TESTS = [(29, 2, 1296), (29, 3, 1296), (29, 8, 1296), (4, 2, 16), (10, 6, 8), (1
 # (tests/test_gpu_ptrs.py; the north-star shape is benchmarked through them too).
 PTR_SHAPES = [(29, 4, 1296), (29, 8, 1296), (10, 6, 24), (64, 5, 4096), (64, 3, 4096), (40, 20, 4096),
               (128, 32, 8192), (200, 56, 65536)]
-# Shapes whose fused large-m decode (LONGHAIR_AMD_WIN_SPLIT=0 and 2) the GPU tests run.
-VARIANT_SHAPES = [(40, 20, 4096), (100, 16, 2048), (128, 32, 8192), (200, 56, 65536), (250, 6, 2048)]
+# Modules of the knob variants the GPU tests run (tests/test_gpu_parity.py KNOB_VARIANTS).
+KNOB_JOBS = [((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=2,LH_NT=0,LH_XCD=0"}),
+             ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_REC_FIRST=0,LH_PF_DEC=2"})]
 
 
 def boundary_jobs():
@@ -64,9 +65,8 @@ def main():
             # the large-m shapes' encode and decode modules compile in separate processes
             jobs_list = [(s, part) for s in slow[:2] for part in ("dec", "enc")]
             jobs_list += [(s, None) for s in slow[2:] + [s for s in DEFAULT + TESTS if s not in slow]]
-            # non-default kernels the GPU tests also run (test_wide_decode_fused_variant)
-            jobs_list += [(s, ("dec", {"LONGHAIR_AMD_WIN_SPLIT": v})) for v in ("0", "2") for s in VARIANT_SHAPES]
             ptr_jobs = [(s, (part, {"LONGHAIR_AMD_PRECOMPILE_PTR": "1"})) for s in PTR_SHAPES for part in ("dec", "enc")]
+            jobs_list += [(s, (None, env)) for s, env in KNOB_JOBS]
             jobs_list = ptr_jobs[-4:] + jobs_list + ptr_jobs[:-4]
             # kernel-selection boundaries and the reference-main sweep (test_gpu_boundaries.py)
             bj, tb = boundary_jobs()

@@ -12,9 +12,7 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 import longhair_amd as lh  # noqa: E402
 
-KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_WIN_ROWS", "LONGHAIR_AMD_WIN_PF", "LONGHAIR_AMD_WIN_LDS",
-         "LONGHAIR_AMD_NO_FUSED_PLAN", "LONGHAIR_AMD_GRID", "LONGHAIR_AMD_WIN_SPLIT",
-         "LONGHAIR_AMD_INV_PACK"]
+KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_NO_FUSED_PLAN"]
 
 
 def main():

@@ -2,7 +2,7 @@
 """Tuning sweep for the specialised kernels (one process, interleaved variants).
 
 For each variant (env knobs read by the library at JIT time: LONGHAIR_AMD_JIT_DEFINES,
-LONGHAIR_AMD_JIT_W, LONGHAIR_AMD_GRID) it times encode_batch and decode_batch on the
+LONGHAIR_AMD_NO_FUSED_PLAN) it times encode_batch and decode_batch on the
 bench workload with HIP events and checks the bytes against the default variant.
 Usage: python tools/tune.py [k m bytes stripes] > gpurun_out/tune.txt
 """
@@ -22,10 +22,7 @@ VARIANTS = [
     ("noxcd", {"LONGHAIR_AMD_JIT_DEFINES": "LH_XCD=0"}),
     ("nofused", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1"}),
 ]
-KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_JIT_W", "LONGHAIR_AMD_GRID", "LONGHAIR_AMD_NO_FUSED_PLAN",
-         "LONGHAIR_AMD_PLAN_THREADS",
-         "LONGHAIR_AMD_WIN_ROWS", "LONGHAIR_AMD_WIN_PF", "LONGHAIR_AMD_WIN_LDS",
-         "LONGHAIR_AMD_WIN_SPLIT", "LONGHAIR_AMD_INV_PACK", "LONGHAIR_AMD_INV_CHUNKS", "LONGHAIR_AMD_JIT_AL", "LONGHAIR_AMD_JIT_ALS"]
+KNOBS = ["LONGHAIR_AMD_JIT_DEFINES", "LONGHAIR_AMD_NO_FUSED_PLAN"]
 # Large-m (windowed) variants: rows per wave and columns in flight.
 VARIANTS_WIN = [
     ("base", {}),
