@@ -321,9 +321,14 @@ def batch_path(k, m, block_bytes, decode=False):
 
 def kernel_names(k, m, block_bytes):
     """Names of the kernels one encode_batch / decode_batch launches for this shape."""
-    enc = {"generic": ["lh_apply_generic_kernel"], "jit": ["lh_jit_encode"],
+    sub = block_bytes // 8
+    small = sub < 4  # the generic kernels below dword lanes
+    nch = (sub + 3) // 4  # decode in place: the overlapping last lane must share its neighbour's workgroup
+    old_dec = small or (sub % 4 != 0 and nch > 1 and (nch - 1) % 64 == 0)
+    enc = {"generic": ["lh_apply_generic_kernel" if small else "lh_apply_jump_kernel"], "jit": ["lh_jit_encode"],
            "jit-win": ["lh_jit_encode_win"]}[batch_path(k, m, block_bytes)]
-    dec = {"generic": ["lh_plan_kernel", "lh_apply_generic_kernel", "lh_scatter_kernel"],
+    dec = {"generic": ["lh_plan_kernel"] + (["lh_apply_generic_kernel", "lh_scatter_kernel"] if old_dec
+                                            else ["lh_apply_jump_kernel"]),
            "jit": ["lh_plan_small_kernel" if min(k, m) <= 8 else "lh_plan_kernel", "lh_jit_decode"],
            "jit-fused": ["lh_jit_decode_fused"],
            "jit-wide": ["lh_plan_kernel", "lh_jit_decode_wide", "lh_inverse_gt_kernel"],

@@ -395,6 +395,24 @@ static int encode_batch(int k, int m, int bytes, int stripes, const uint8_t *d_d
     }
     const uint8_t *G = nullptr;
     if (int rc = device_generator(d, k, m, &G, nullptr, st)) return rc;
+    if (bytes / 8 >= 4) {  // the jump-table apply (dword lanes)
+        JumpApplyArgs a{};
+        a.in = d_data;
+        a.in_stride = data_stride;
+        a.out = d_rec;
+        a.out_stride = rec_stride;
+        a.coef = G;
+        a.coef_stride = 0;
+        a.n_in = k;
+        a.n_out = m;
+        a.bytes = bytes;
+        a.sub = bytes / 8;
+        a.nch = (a.sub + 3) / 4;
+        a.stripes = stripes;
+        a.per_stripe = 0;
+        LH_HIP(launch_apply_jump(a, st));
+        return kOk;
+    }
     ApplyArgs a{};
     a.in = d_data;
     a.in_stride = data_stride;
@@ -498,7 +516,13 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         if (hard) return fail(kHipError, err);
         if (wk && !wk->decode_wide) wk = nullptr;
     }
-    const size_t work_bytes = (generic && !wk) ? (size_t)stripes * e_max * bytes : 0;
+    // The generic decode: the jump-table apply in place (dword lanes), unless the last dword
+    // lane of a sub-block -- shifted back over its neighbour's bytes when sub % 4 != 0 -- would
+    // sit alone in a workgroup of its own (sub = 256 t + 1..3): then the old apply into a
+    // workspace and a scatter.
+    const int sub = bytes / 8, jnch = (sub + 3) / 4;
+    const bool jump = generic && !wk && sub >= 4 && !(sub % 4 != 0 && jnch > 1 && (jnch - 1) % 64 == 0);
+    const size_t work_bytes = (generic && !wk && !jump) ? (size_t)stripes * e_max * bytes : 0;
     Workspace *w = nullptr;
     if (int rc = run_planner(d, st, k, m, e_max, stripes, d_rows, d_status, work_bytes, generic && !wk, &w)) return rc;
     if (k <= 1) return kOk;
@@ -566,7 +590,28 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         }
         return kOk;
     }
-    // Generic: recovered originals into the workspace, then into their slots.
+    if (jump) {
+        JumpApplyArgs a{};
+        a.in = d_blocks;
+        a.in_stride = stride;
+        a.out = d_blocks;
+        a.out_stride = stride;
+        a.coef = w->plan.ptr + PlanView::w_offset(k, m, e_max);
+        a.coef_stride = plan_stride;
+        a.plan = w->plan.ptr;
+        a.plan_stride = plan_stride;
+        a.n_in = k;
+        a.n_out = e_max;
+        a.bytes = bytes;
+        a.sub = sub;
+        a.nch = jnch;
+        a.stripes = stripes;
+        a.per_stripe = 1;
+        a.wps = (jnch + 63) / 64;
+        LH_HIP(launch_apply_jump(a, st));
+        return kOk;
+    }
+    // Generic, tiny blocks: recovered originals into the workspace, then into their slots.
     ApplyArgs a{};
     a.in = d_blocks;
     a.in_stride = stride;

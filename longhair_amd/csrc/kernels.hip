@@ -993,6 +993,168 @@ __global__ void __launch_bounds__(1024) lh_inverse_gt_kernel(lh::InverseArgs a) 
     lh_inverse_gt_body(a, lvA, lvB, tlo, thi);
 }
 
+// ------------------------------------------------------------ generic apply, jump table
+// lh_apply_jump_kernel (kernels.hpp JumpApplyArgs): every shape without a specialised module,
+// and every shape while its module compiles in the background.  Per input column a lane
+// builds the 16-entry XOR tables of its dword of sub-blocks 0..3 (tl) and 4..7 (th) -- the
+// win_encode idea of cauchy_256.cpp:1414-1493 with the tables in registers -- and a multiply
+// by a runtime coefficient c is a jump into body c of the phase-B table (lh_inv_gtab: one XOR3
+// per output sub-row, the nibble indices of c * 2^y compile-time constants of the body), the
+// body address of output i for column j held in lane j of t[i].  Column loads are unaligned
+// dword loads (a sub-block starts 2-byte aligned at 1296-byte blocks); the next column is in
+// flight while the current one is combined.
+namespace {
+typedef uint32_t lh_u32u __attribute__((aligned(1)));
+
+struct lh_ja_lane {
+    long long stripe;   // (clamped to a valid stripe for the loads of an inactive lane)
+    int p;              // the lane's byte offset in every sub-block
+    bool active;
+};
+
+// (an inactive lane -- past the last stripe, or past the chunk's sub-block bytes -- loads
+// nothing: exec-masked, no memory request)
+__device__ __forceinline__ void lh_ja_load(uint32_t (&d)[8], const uint8_t *col, int sub, bool active) {
+#pragma unroll
+    for (int b = 0; b < 8; ++b) d[b] = 0;
+    if (active) {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) d[b] = *(const lh_u32u *)(col + (long long)b * sub);
+    }
+}
+
+__device__ __forceinline__ void lh_ja_tables(const uint32_t (&d)[8], uint32_t (&tl)[16], uint32_t (&th)[16]) {
+    tl[0] = th[0] = 0;
+#pragma unroll
+    for (int q = 1; q < 16; ++q) {
+        const int low = __builtin_ctz(q), pre = q & (q - 1);
+        tl[q] = pre ? (tl[pre] ^ d[low]) : d[low];
+        th[q] = pre ? (th[pre] ^ d[4 + low]) : d[4 + low];
+    }
+}
+
+// One round: outputs i0 .. i0 + N - 1 of this wave over every input column.  GT: the table
+// once per code object (lh_mul_jump_g); else the in-asm table (lh_mul_jump_idx8, a table
+// straddling a 4 GiB boundary; coefficient 0 = body 0 leaves unused outputs unchanged).
+template <int N, bool GT>
+__device__ __forceinline__ void lh_ja_round(const lh::JumpApplyArgs &a, const lh_ja_lane &l, const uint8_t *coef,
+                                            int i0, uint32_t (&acc)[8][8], uint32_t tlo, uint32_t thi) {
+    const int lane = threadIdx.x & 63;
+    const uint8_t *in = a.in + l.stripe * a.in_stride + l.p;
+    for (int jq = 0; jq * 64 < a.n_in; ++jq) {  // 64 columns per block of body addresses
+        const int jc = jq * 64 + lane;
+        uint32_t t[8], cpk0 = 0, cpk1 = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t c = (i < N && jc < a.n_in) ? coef[(long long)(i0 + i) * a.n_in + jc] : 0u;
+            t[i] = tlo + c * 68u;
+            if (i < 4) cpk0 |= c << (8 * i);
+            else cpk1 |= c << (8 * (i - 4));
+        }
+        const int nj = a.n_in - jq * 64 < 64 ? a.n_in - jq * 64 : 64;
+        uint32_t cur[8];
+        lh_ja_load(cur, in + (long long)(jq * 64) * a.bytes, a.sub, l.active);
+        for (int jl = 0; jl < nj; ++jl) {  // wave-uniform
+            const int jn = jq * 64 + jl + 1 < a.n_in ? jq * 64 + jl + 1 : jq * 64 + jl;  // (the last reloads itself)
+            uint32_t nxt[8];
+            lh_ja_load(nxt, in + (long long)jn * a.bytes, a.sub, l.active);
+            uint32_t tl[16], th[16];
+            lh_ja_tables(cur, tl, th);
+            if constexpr (GT) {
+                (void)lh_mul_jump_g<N>(acc, tl, th, t, jl, tlo, thi);
+            } else {
+                lh_mul_jump_idx8((uint32_t)__builtin_amdgcn_readlane((int)cpk0, jl),
+                                 (uint32_t)__builtin_amdgcn_readlane((int)cpk1, jl), acc, tl, th);
+            }
+#pragma unroll
+            for (int b = 0; b < 8; ++b) cur[b] = nxt[b];
+        }
+    }
+}
+
+template <bool GT>
+__device__ __forceinline__ void lh_apply_jump_body(const lh::JumpApplyArgs &a, uint32_t tlo, uint32_t thi) {
+    const int lane = threadIdx.x & 63;
+    const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), ng = (int)(blockDim.x >> 6);
+    lh_ja_lane l;
+    int c;
+    if (a.per_stripe) {
+        l.stripe = blockIdx.x / a.wps;
+        if (l.stripe >= a.stripes) return;  // workgroup-uniform
+        c = (int)(blockIdx.x % a.wps) * 64 + lane;
+        l.active = c < a.nch;
+        c = l.active ? c : a.nch - 1;
+    } else {
+        const long long t = (long long)blockIdx.x * 64 + lane;
+        l.stripe = t / a.nch;
+        c = (int)(t - l.stripe * a.nch);
+        l.active = l.stripe < a.stripes;
+        if (!l.active) l.stripe = a.stripes - 1;
+    }
+    // The last chunk of a sub-block re-reads its final 4 bytes (overlapping its neighbour
+    // with identical results) instead of running past the sub-block.
+    l.p = c == a.nch - 1 ? a.sub - 4 : 4 * c;
+    const uint8_t *pl = a.plan ? a.plan + l.stripe * a.plan_stride : nullptr;
+    const int n_out = pl ? pl[0] : a.n_out;  // per_stripe: workgroup-uniform
+    if (pl && n_out == 0) return;           // workgroup-uniform: nothing erased
+    const uint8_t *coef = a.coef + l.stripe * a.coef_stride;
+    const int rounds = (a.n_out + 8 * ng - 1) / (8 * ng);  // the same for every wave (barriers)
+    for (int q = 0; q < rounds; ++q) {
+        const int i0 = 8 * (q * ng + g);
+        int nout = n_out - i0;
+        nout = nout < 0 ? 0 : (nout > 8 ? 8 : nout);  // wave-uniform
+        uint32_t acc[8][8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int y = 0; y < 8; ++y) acc[i][y] = 0;
+        switch (nout) {  // wave-uniform
+            case 0: break;
+            case 1: lh_ja_round<1, GT>(a, l, coef, i0, acc, tlo, thi); break;
+            case 2: lh_ja_round<2, GT>(a, l, coef, i0, acc, tlo, thi); break;
+            case 3: lh_ja_round<3, GT>(a, l, coef, i0, acc, tlo, thi); break;
+            case 4: lh_ja_round<4, GT>(a, l, coef, i0, acc, tlo, thi); break;
+            case 5: lh_ja_round<5, GT>(a, l, coef, i0, acc, tlo, thi); break;
+            case 6: lh_ja_round<6, GT>(a, l, coef, i0, acc, tlo, thi); break;
+            case 7: lh_ja_round<7, GT>(a, l, coef, i0, acc, tlo, thi); break;
+            default: lh_ja_round<8, GT>(a, l, coef, i0, acc, tlo, thi); break;
+        }
+        // In place (decode): every wave of the workgroup has read every slot of this chunk
+        // before any output overwrites one (the host runs a single round there).
+        if (pl && ng > 1) __syncthreads();
+        if (l.active) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if (i < nout) {
+                    uint8_t *dst = pl ? a.out + l.stripe * a.out_stride + (long long)pl[16 + i0 + i] * a.bytes
+                                      : a.out + l.stripe * a.out_stride + (long long)(i0 + i) * a.bytes;
+#pragma unroll
+                    for (int y = 0; y < 8; ++y) *(lh_u32u *)(dst + l.p + (long long)y * a.sub) = acc[i][y];
+                }
+            }
+        }
+    }
+}
+}  // namespace
+
+__global__ void __launch_bounds__(1024) lh_apply_jump_kernel(lh::JumpApplyArgs a) {
+    uint32_t tlo, thi;
+    asm volatile(
+        "s_getpc_b64 s[92:93]\n"
+        "s_add_u32 s92, s92, lh_inv_gtab@rel32@lo+4\n"
+        "s_addc_u32 s93, s93, lh_inv_gtab@rel32@hi+12\n"
+        "s_mov_b32 %0, s92\n"
+        "s_mov_b32 %1, s93\n"
+        : "=s"(tlo), "=s"(thi)
+        :
+        : "s92", "s93", "scc");
+    if (tlo > 0xFFFFFFFFu - 256u * 68u) {  // the table straddles a 4 GiB boundary (never seen)
+        lh_apply_jump_body<false>(a, tlo, thi);
+        return;
+    }
+    lh_apply_jump_body<true>(a, tlo, thi);
+}
+
 // ---------------------------------------------------------- pointer-table gather / scatter
 // One wave per (stripe, block): 16 B per lane when both addresses and the block size allow,
 // else 8 B, else single bytes (the caller's blocks may sit at any alignment).  Wave-uniform
@@ -1081,6 +1243,20 @@ hipError_t launch_apply_generic(const ApplyArgs &a, int W, hipStream_t st) {
         default: return hipErrorInvalidValue;
     }
     note_launch("lh_apply_generic_kernel");
+    return hipGetLastError();
+}
+
+hipError_t launch_apply_jump(const JumpApplyArgs &a, hipStream_t st) {
+    // sub >= 4 (dword lanes); at most 16 waves of 8 outputs per workgroup; in place a single
+    // round (e_max <= 128 always holds: e_max = min(k, m) and k + m <= 256).
+    if (a.sub < 4 || a.n_out < 1 || a.n_in < 1 || a.nch < 1) return hipErrorInvalidValue;
+    const int ng = (a.n_out + 7) / 8 < 16 ? (a.n_out + 7) / 8 : 16;
+    if (a.plan && a.n_out > 8 * ng) return hipErrorInvalidValue;
+    const long long wgs = a.per_stripe ? (long long)a.stripes * a.wps : ((long long)a.stripes * a.nch + 63) / 64;
+    if (wgs <= 0) return hipSuccess;
+    if (wgs > 0x7FFFFFFF) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(lh_apply_jump_kernel, dim3((unsigned)wgs), dim3(64u * (unsigned)ng), 0, st, a);
+    note_launch("lh_apply_jump_kernel");
     return hipGetLastError();
 }
 

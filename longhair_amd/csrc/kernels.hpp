@@ -54,6 +54,29 @@ struct ApplyArgs {
     int n_in, n_out, bytes, sub, stripes, nch;
 };
 
+// Generic apply through the phase-B jump table (lh_apply_jump_kernel): out_i = sum_j
+// B(W[i][j]) in_j for any coefficient matrix, at the nibble-table cost (22 XORs per input
+// column and lane, then one XOR3 per output sub-row) instead of lh_apply_generic_kernel's 64
+// masked XORs per output and column.  Dword lanes (sub >= 4), up to 8 outputs per wave and
+// ceil(n_out / 8) waves per workgroup (at most 16; more outputs take further rounds).
+//  per_stripe = 0 (encode: one coefficient matrix for every stripe): lanes run flat over
+//    (stripe, dword chunk), so small blocks fill whole waves;
+//  per_stripe = 1 (decode: the plan's per-stripe W over the k slots): a workgroup codes one
+//    stripe's 64-lane chunk; the outputs go in place to the plan's output slots (count e =
+//    plan[0]) after a workgroup barrier, so no wave still reads a slot another overwrites.
+struct JumpApplyArgs {
+    const uint8_t *in;            // stripe s, input j: in + s*in_stride + j*bytes
+    long long in_stride;
+    uint8_t *out;                 // per_stripe 0: stripe s, output i at out + s*out_stride + i*bytes
+    long long out_stride;
+    const uint8_t *coef;          // W[i][j] at coef + s*coef_stride + i*n_in + j (stride 0: shared)
+    long long coef_stride;
+    const uint8_t *plan;          // per_stripe 1: e and the output slots (PlanView), in place
+    long long plan_stride;
+    int n_in, n_out, bytes, sub, nch, stripes;
+    int per_stripe, wps;          // wps: workgroups per stripe (per_stripe 1) = ceil(nch / 64)
+};
+
 struct XorArgs {
     const uint8_t *in;            // stripe s, input j: in + s*in_stride + j*bytes
     long long in_stride;
@@ -154,6 +177,7 @@ void note_launch(const char *kernel);
 
 hipError_t launch_writeback(const WritebackArgs &a, hipStream_t st);
 hipError_t launch_apply_generic(const ApplyArgs &a, int W, hipStream_t st);
+hipError_t launch_apply_jump(const JumpApplyArgs &a, hipStream_t st);
 hipError_t launch_frame(const FrameArgs &a, hipStream_t st);
 hipError_t launch_xor_reduce(const XorArgs &a, hipStream_t st);
 hipError_t launch_scatter(const ScatterArgs &a, hipStream_t st);

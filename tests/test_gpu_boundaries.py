@@ -23,8 +23,12 @@ pytestmark = pytest.mark.gpu
 FUSED = ["lh_jit_decode_fused"]
 SMALL4 = ["lh_plan_small_kernel<4>", "lh_jit_decode"]
 SMALL8 = ["lh_plan_small_kernel<8>", "lh_jit_decode"]
-GENERIC_CF = ["lh_plan_kernel(closed form)", "lh_apply_generic_kernel", "lh_scatter_kernel"]
-GENERIC_S8 = ["lh_plan_small_kernel<8>", "lh_apply_generic_kernel", "lh_scatter_kernel"]
+GENERIC_CF = ["lh_plan_kernel(closed form)", "lh_apply_jump_kernel"]
+GENERIC_S8 = ["lh_plan_small_kernel<8>", "lh_apply_jump_kernel"]
+# the generic decode's fallback (sub < 4, or the overlapping last dword lane alone in its
+# workgroup: sub = 256 t + 1..3): apply into a workspace, then scatter
+OLD_CF = ["lh_plan_kernel(closed form)", "lh_apply_generic_kernel", "lh_scatter_kernel"]
+JUMP = ["lh_apply_jump_kernel"]
 WIDE16 = ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_gt_kernel"]
 WIDE64 = WIDE16  # (one phase-B kernel for every e_max since round 3)
 
@@ -50,18 +54,24 @@ BOUNDARIES = [
     # generator from the CAUCHY_MATRIX_2..6 tables (m <= 6) <-> from the X/Y points (m >= 7)
     ("m6-jit", 20, 6, 64, 64, {}, ["lh_jit_encode"], SMALL8),
     ("m7-jit", 20, 7, 64, 64, {}, ["lh_jit_encode"], SMALL8),
-    ("m6-generic", 20, 6, 64, 64, {"LONGHAIR_AMD_PATH": "generic"}, ["lh_apply_generic_kernel"], GENERIC_S8),
-    ("m7-generic", 20, 7, 64, 64, {"LONGHAIR_AMD_PATH": "generic"}, ["lh_apply_generic_kernel"], GENERIC_S8),
+    ("m6-generic", 20, 6, 64, 64, {"LONGHAIR_AMD_PATH": "generic"}, JUMP, GENERIC_S8),
+    ("m7-generic", 20, 7, 64, 64, {"LONGHAIR_AMD_PATH": "generic"}, JUMP, GENERIC_S8),
     # register-resident encode network: m <= 12 (96 accumulator dwords) <-> windowed / generic
     ("enc-m12", 40, 12, 2048, 8, {}, ["lh_jit_encode"], WIDE16),
     ("enc-m13", 40, 13, 2048, 8, {}, ["lh_jit_encode_win"], WIDE16),
     ("enc-m12-small", 10, 12, 64, 32, {}, ["lh_jit_encode"], GENERIC_CF),
-    ("enc-m13-small", 10, 13, 64, 32, {}, ["lh_apply_generic_kernel"], GENERIC_CF),
+    ("enc-m13-small", 10, 13, 64, 32, {}, JUMP, GENERIC_CF),
     # windowed decode: m <= 64 (the used-row ballot) and sub % 256 == 0
     ("wide-m64", 20, 64, 2048, 8, {}, ["lh_jit_encode_win"], WIDE16),
     ("generic-m65", 20, 65, 2048, 8, {}, ["lh_jit_encode_win"], GENERIC_CF),
     ("wide-sub512", 40, 20, 4096, 8, {}, ["lh_jit_encode_win"], WIDE16),
-    ("generic-sub513", 40, 20, 4104, 8, {}, ["lh_apply_generic_kernel"], GENERIC_CF),
+    ("generic-sub513", 40, 20, 4104, 8, {}, JUMP, OLD_CF),
+    # generic decode in place: every dword lane of a sub-block in one workgroup with its
+    # overlapped neighbour (sub 516: jump apply) <-> not (sub 513 above: workspace + scatter)
+    ("generic-sub516", 40, 20, 4128, 8, {}, JUMP, GENERIC_CF),
+    # generic kernels below dword lanes (sub < 4) <-> the jump apply (sub = 4)
+    ("generic-sub3", 30, 13, 24, 40, {}, ["lh_apply_generic_kernel"], OLD_CF),
+    ("generic-sub4", 30, 13, 32, 40, {}, JUMP, GENERIC_CF),
     # phase B: V rows staged 16 at a time for e_max <= 32, all at once above
     ("jump-emax32", 40, 32, 2048, 8, {}, ["lh_jit_encode_win"], WIDE16),
     ("jump-emax33", 40, 33, 2048, 8, {}, ["lh_jit_encode_win"], WIDE64),
@@ -198,7 +208,7 @@ def test_reference_main_sweep(lh, oracle, monkeypatch):
             seen.update(enc + dec)
             n += 1
     assert n > 2500
-    assert {"lh_jit_encode", "lh_jit_decode_fused", "lh_jit_decode", "lh_apply_generic_kernel",
+    assert {"lh_jit_encode", "lh_jit_decode_fused", "lh_jit_decode", "lh_apply_generic_kernel", "lh_apply_jump_kernel",
             "lh_xor_reduce_kernel"} <= seen, sorted(seen)
 
 
@@ -361,7 +371,7 @@ def test_jit_compiles_in_background(lh, oracle, monkeypatch, tmp_path):
     rec = lh.encode_batch(x, m)
     torch.cuda.synchronize()
     first = time.perf_counter() - t0
-    assert lh.last_launch() == ["lh_apply_generic_kernel"], lh.last_launch()
+    assert lh.last_launch() == ["lh_apply_jump_kernel"], lh.last_launch()
     assert first < 1.0, f"first call took {first:.2f} s"
     assert np.array_equal(rec.cpu().numpy(), expect)
     # another shape meanwhile: its (cached) module is not held up by the compilation
@@ -376,7 +386,7 @@ def test_jit_compiles_in_background(lh, oracle, monkeypatch, tmp_path):
         trace = lh.last_launch()
         if trace == ["lh_jit_encode"]:
             break
-        assert trace == ["lh_apply_generic_kernel"], trace
+        assert trace == ["lh_apply_jump_kernel"], trace
         assert time.time() < deadline, "the background compilation did not finish in 100 s"
         time.sleep(0.25)
     assert np.array_equal(rec.cpu().numpy(), expect)
