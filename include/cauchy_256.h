@@ -12,8 +12,11 @@
  *   Block                                  same layout as reference cauchy_256.h:52-55
  *
  * Behaviour follows the reference implementation (not its header comments):
- *   - init returns 0 on success, -1 on a version mismatch; here also -2 when no usable
- *     MI355X/HIP device is present (the codec has no CPU fallback).
+ *   - init returns 0 on success, -1 on a version mismatch.  Without a HIP device it still
+ *     returns 0 under the AUTO (default) and HOST dispatch policies (cauchy_256_dispatch.h):
+ *     the drop-in calls then run on the library's host SIMD engine; under the GPU policy
+ *     init and the drop-in calls return -2.  No C++ exception crosses this ABI: an internal
+ *     one returns -3 (cauchy_256_last_error() names it).
  *   - encode writes m * block_bytes bytes to recovery_blocks.  Recovery block 0 is the
  *     XOR of the k data blocks and is written before parameters are validated; with
  *     m > 1, k + m > 256 or block_bytes % 8 != 0 then returns -1.  k <= 1 copies data[0]

@@ -436,6 +436,162 @@ struct lh_unroll_encode<LH_K> {
     __device__ __forceinline__ static void run(lh_word (&)[LH_M][8], lh_word (&)[LH_PF][8], const lh_esrc &) {}
 };
 
+// ---------------------------------------------------------------- LDS-DMA column loads
+// LH_LDS = 1 (jit.cpp, whole stripes per wave with 8-byte lanes and 16-byte-multiple blocks,
+// e.g. k29/m4/1296): the column x of the wave's LH_SPW stripes is fetched as aligned 16-byte
+// chunks -- LH_LQ global_load_lds_dwordx4 per column, chunk j = 64 q + lane of the image
+// [stripe][bytes], per-lane source addresses -- into a per-wave LDS ring of LH_LD slots, and
+// every lane reads its 8 bytes of sub-block b back as two naturally aligned ds_read_b64
+// funnelled by v_alignbyte (sub-block b starts (b * sub) % 8 bytes past an 8-byte boundary in
+// both memory and the image, a compile-time constant; a misaligned ds_read_b64 would replay at
+// 64 cycles).  Versus 8 loads of 3 x 168-byte pieces per column, the wave issues LH_LQ = 4
+// loads of whole 1-KiB runs: the k29/m4 access pattern 0.546 against 0.563-0.594 ms on two
+// boxes (profiles/r5a/r5c_ubench_floor.txt, `ldsd`).  The last lane of a stripe reads its
+// chunk unshifted (only LH_VLAST bytes are its own) and stores [sub - 8, sub) assembled with
+// the previous lane's word (DPP row_shr:1; the host checks both lanes share a DPP row).
+#ifndef LH_LDS
+#define LH_LDS 0
+#endif
+#if LH_LDS
+#if LH_W != 8 || LH_NCH > 64 || LH_BYTES % 16 != 0 || LH_BUF == 0
+#error "LH_LDS: 8-byte lanes, whole stripes per wave, 16-byte-multiple blocks, strided batches"
+#endif
+#ifndef LH_LD
+#define LH_LD 4  // ring slots per wave (columns in flight + the one being read)
+#endif
+#define LH_LQ ((LH_SPW * LH_BYTES + 1023) / 1024)  // DMA instructions per column
+#define LH_VLAST (LH_SUB - 8 * (LH_NCH - 1))      // valid bytes of the last chunk of a sub-block
+typedef unsigned int lh_u32x2a __attribute__((ext_vector_type(2)));
+// Bytes [S, S + 8) of the 16 little-endian bytes (a, b).
+template <int S>
+__device__ __forceinline__ lh_word lh_funnel(unsigned a0, unsigned a1, unsigned b0, unsigned b1) {
+    lh_word w;
+    if constexpr (S == 0) {
+        w.v[0] = a0; w.v[1] = a1;
+    } else if constexpr (S == 4) {
+        w.v[0] = a1; w.v[1] = b0;
+    } else if constexpr (S < 4) {
+        w.v[0] = __builtin_amdgcn_alignbyte(a1, a0, S); w.v[1] = __builtin_amdgcn_alignbyte(b0, a1, S);
+    } else if constexpr (S == 8) {
+        w.v[0] = b0; w.v[1] = b1;
+    } else {
+        w.v[0] = __builtin_amdgcn_alignbyte(b0, a1, S - 4); w.v[1] = __builtin_amdgcn_alignbyte(b1, b0, S - 4);
+    }
+    return w;
+}
+// The lane's word of sub-block B from a ring slot: `lo` its chunk's offset in the image
+// (stripe * bytes + 8 c), `lo8` = lo + 8 hidden from the compiler so the pair stays two
+// ds_read_b64 (2 LDS cycles each) instead of one ds_read2_b64 (8).
+template <int B>
+__device__ __forceinline__ lh_word lh_slot_word(const unsigned char *slot, int lo, int lo8) {
+    constexpr int S = (B * LH_SUB) % 8, O = B * LH_SUB - S;
+    const lh_u32x2a a = *(const lh_u32x2a *)(slot + lo + O);
+    if constexpr (S == 0) {
+        lh_word w;
+        w.v[0] = a.x; w.v[1] = a.y;
+        return w;
+    } else {
+        const lh_u32x2a b = *(const lh_u32x2a *)(slot + lo8 + O);
+        return lh_funnel<S>(a.x, a.y, b.x, b.y);
+    }
+}
+template <int B = 0>
+__device__ __forceinline__ void lh_slot_col(lh_word (&d)[8], const unsigned char *slot, int lo, int lo8) {
+    if constexpr (B < 8) {
+        d[B] = lh_slot_word<B>(slot, lo, lo8);
+        lh_slot_col<B + 1>(d, slot, lo, lo8);
+    }
+}
+__device__ __forceinline__ unsigned lh_row_shr1(unsigned v) {  // lane i <- lane i - 1 within a DPP row of 16
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
+}
+struct lh_ldsrc {
+    const unsigned char *src[LH_LQ];  // this lane's chunk of DMA instruction q, column 0
+    unsigned char *ring;              // this wave's LH_LD slots of LH_LQ KiB
+    __device__ __forceinline__ void issue(int x, int slot) const {
+#pragma unroll
+        for (int q = 0; q < LH_LQ; ++q)
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src[q] + (long long)x * LH_BYTES),
+                                             (__attribute__((address_space(3))) void *)(ring + slot * (LH_LQ * 1024) + q * 1024),
+                                             16, 0, LH_NT ? 2 : 0);
+    }
+};
+// s_waitcnt vmcnt(N) (gfx9 encoding, expcnt / lgkmcnt left at their maxima); N a constant.
+template <int N>
+__device__ __forceinline__ void lh_wait_vmcnt() {
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+template <int X>
+struct lh_unroll_encode_lds {
+    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], const lh_ldsrc &S, int lo, int lo8) {
+        if constexpr (X < LH_K) {
+            // this column's DMAs landed: all but those of the columns issued after it
+            constexpr int ahead = (LH_LD - 1) < (LH_K - 1 - X) ? (LH_LD - 1) : (LH_K - 1 - X);
+            lh_wait_vmcnt<LH_LQ * ahead>();
+            asm volatile("" ::: "memory");  // no LDS read moves above the wait
+            lh_word d[8];
+            lh_slot_col(d, S.ring + (X % LH_LD) * (LH_LQ * 1024), lo, lo8);
+            lh_column<X>(acc, d);
+            lh_opaque(acc);
+            if constexpr (X + LH_LD < LH_K) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done
+                S.issue(X + LH_LD, X % LH_LD);
+            }
+            lh_unroll_encode_lds<X + 1>::run(acc, S, lo, lo8);
+        }
+    }
+};
+
+__device__ __forceinline__ void lh_encode_wave_lds(long long wave, const unsigned char *__restrict__ in,
+                                                   long long in_stride, unsigned char *__restrict__ out,
+                                                   long long out_stride, int stripes) {
+    __shared__ __attribute__((aligned(16))) unsigned char lh_lring[4][LH_LD * LH_LQ * 1024];
+    const int lane = threadIdx.x & 63;
+    const int sl = lane / LH_NCH, c = lane - sl * LH_NCH;
+    const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)wave) * LH_SPW;  // wave-uniform
+    if (s0 >= stripes) return;  // wave-uniform
+    const int nst = (int)((stripes - s0) < LH_SPW ? (stripes - s0) : LH_SPW);
+    lh_ldsrc S;
+    S.ring = lh_lring[threadIdx.x >> 6];
+#pragma unroll
+    for (int q = 0; q < LH_LQ; ++q) {  // every lane moves chunks, whatever its own stripe
+        int j = 64 * q + lane;
+        if (j >= nst * (LH_BYTES / 16)) j = nst * (LH_BYTES / 16) - 1;  // (lands past the image)
+        const int js = j / (LH_BYTES / 16);
+        S.src[q] = in + (s0 + js) * in_stride + (j - js * (LH_BYTES / 16)) * 16;
+    }
+#pragma unroll
+    for (int q = 0; q < LH_LD; ++q)
+        if (q < LH_K) S.issue(q, q);
+    lh_word acc[LH_M][8];
+#pragma unroll
+    for (int r = 0; r < LH_M; ++r)
+#pragma unroll
+        for (int y = 0; y < 8; ++y)
+#pragma unroll
+            for (int i = 0; i < LH_NW; ++i) acc[r][y].v[i] = 0;
+    const int lo = (sl < LH_SPW ? sl : LH_SPW - 1) * LH_BYTES + 8 * c;
+    int lo8 = lo + 8;
+    asm volatile("" : "+v"(lo8));
+    lh_unroll_encode_lds<0>::run(acc, S, lo, lo8);
+    const bool last = c == LH_NCH - 1;
+    if (sl >= nst) return;
+    unsigned char *o = out + (s0 + sl) * out_stride + (last ? LH_SUB - 8 : 8 * c);
+#pragma unroll
+    for (int r = 0; r < LH_M; ++r)
+#pragma unroll
+        for (int y = 0; y < 8; ++y) {
+            lh_word w = acc[r][y];
+            if constexpr (LH_VLAST != 8) {
+                const lh_word f = lh_funnel<LH_VLAST>(lh_row_shr1(w.v[0]), lh_row_shr1(w.v[1]), w.v[0], w.v[1]);
+                w.v[0] = last ? f.v[0] : w.v[0];
+                w.v[1] = last ? f.v[1] : w.v[1];
+            }
+            lh_store(o + (long long)r * LH_BYTES + y * LH_SUB, w);
+        }
+}
+#endif
+
 __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned char *__restrict__ in,
                                                long long in_stride, unsigned char *__restrict__ out,
                                                long long out_stride, int stripes) {
@@ -496,7 +652,11 @@ __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned ch
 extern "C" __global__ void __launch_bounds__(256, LH_ENC_LB)
 lh_jit_encode(const unsigned char *__restrict__ in, long long in_stride,
               unsigned char *__restrict__ out, long long out_stride, int stripes) {
+#if LH_LDS
+    LH_WAVE_LOOP(stripes) { lh_encode_wave_lds(lh_w, in, in_stride, out, out_stride, stripes); }
+#else
     LH_WAVE_LOOP(stripes) { lh_encode_wave(lh_w, in, in_stride, out, out_stride, stripes); }
+#endif
 }
 #endif
 

@@ -109,6 +109,53 @@ def render_global_call(n):
     return lines
 
 
+# Two-dword table (round 5): a lane owns 8 bytes of every sub-block, so one jump adds B(c) V
+# to 16 accumulator words -- half the jumps per byte of the one-dword table, whose cost is the
+# jump (s_swappc / s_setpc round trip, ~100 cycles per jump per SIMD in phase B) more than its 8
+# VALU.  Body c (132 bytes: 16 v_bitop3_b32 + the return) in lh_inv_gtab2; tl[q] in
+# v[W2_TL + 2q .. + 1], th[q] in v[W2_TH + 2q .. + 1] (q = 1..15), the 16 accumulators of output
+# i in v[W2_ACC + 16 i ..] (sub-row y, dword d at + 2y + d), reached by GPR indexing (16 i).
+W2_TL, W2_TH, W2_ACC = 8, 40, 72
+W2_MAX = 4
+
+
+def render_global_table2():
+    """Asm text of LH_INV_GTAB2_TEXT: s_endpgm, then the 256 two-dword bodies."""
+    body = ["s_endpgm", ".p2align 8", ".hidden lh_inv_gtab2", ".globl lh_inv_gtab2", "lh_inv_gtab2:"]
+    for c in range(256):
+        v = c
+        for y in range(8):
+            lo, hi = v & 15, v >> 4
+            for d in range(2):
+                a = f"v{W2_ACC + 2 * y + d}"
+                s1 = f"v{W2_TL + 2 * lo + d}" if lo else "0"
+                s2 = f"v{W2_TH + 2 * hi + d}" if hi else "0"
+                body.append(f"v_bitop3_b32 {a}, {s1}, {s2}, {a} bitop3:0x96")
+            v = xt(v)
+        body.append("s_setpc_b64 s[94:95]")
+    lines = ["#define LH_INV_GTAB2_TEXT \\"]
+    for i, b in enumerate(body):
+        lines.append(f'    "{b}\\n"' + (" \\" if i + 1 < len(body) else ""))
+    return lines
+
+
+def render_global_call2(n):
+    """Asm text of LH_INV_JUMPG2_<n>_ASM: outputs 0 .. n-1 of one row through lh_inv_gtab2
+    (operands as LH_INV_JUMPG<n>_ASM; the index steps by 16)."""
+    body = ["s_mov_b32 s97, m0", "s_mov_b32 s93, %[hi]"]
+    for i in range(n):
+        body.append(f"v_readlane_b32 s92, %[a{i}], %[r]")
+        body.append("s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)" if i == 0 else f"s_set_gpr_idx_idx {16 * i}")
+        body.append("s_swappc_b64 s[94:95], s[92:93]")
+    body += ["s_set_gpr_idx_off", "s_mov_b32 m0, s97"]
+    lines = [f"#define LH_INV_JUMPG2_{n}_ASM \\"]
+    for i, b in enumerate(body):
+        lines.append(f'    "{b}\\n"' + (" \\" if i + 1 < len(body) else ""))
+    outs = ", ".join(f'"+{{v{W2_ACC + 16 * i + j}}}"(acc[{i}][{j}])' for i in range(n) for j in range(16))
+    lines.append(f"#define LH_INV_JUMPG2_{n}_OUTS(acc) {outs}")
+    return lines
+
+
 def render():
     """The text of inv_jump.inc."""
     lines = ["// generated by tools/gen_inv_jump.py -- do not edit",
@@ -125,6 +172,14 @@ def render():
                      + [f'"{{v{GT_TH + q}}}"(th[{q}])' for q in range(1, 16)]
                      + [f'[a{i}] "v"(t[{i}])' for i in range(GT_MAX)])
     lines.append(f"#define LH_INV_JUMPG_INS(tl, th, t) {gins}")
+    lines.append(f"#define LH_INV_W2_ACC {W2_ACC}")
+    lines += render_global_table2()
+    for n in range(1, W2_MAX + 1):
+        lines += render_global_call2(n)
+    gins2 = ", ".join([f'"{{v{W2_TL + 2 * q + d}}}"(tl[{q}][{d}])' for q in range(1, 16) for d in range(2)]
+                      + [f'"{{v{W2_TH + 2 * q + d}}}"(th[{q}][{d}])' for q in range(1, 16) for d in range(2)]
+                      + [f'[a{i}] "v"(t[{i}])' for i in range(W2_MAX)])
+    lines.append(f"#define LH_INV_JUMPG2_INS(tl, th, t) {gins2}")
     return "\n".join(lines) + "\n"
 
 

@@ -503,6 +503,151 @@ __global__ void __launch_bounds__(256) geo(const uint8_t *__restrict__ in, uint8
   }
 }
 
+
+// ---------------------------------------------------------------- one stripe per wave, dword lanes
+// w4d: lane c < 41 owns bytes [4c, 4c + 4) of every sub-block of the wave's ONE stripe (the
+// last lane [158, 162)); 8 buffer_load_dword per column (2-byte aligned for odd sub-blocks),
+// PF columns in flight; 4 x 8 dword accumulators.  The wave streams one contiguous 37.6 KB
+// region (the geometry of flat1 / mixL U=1) at the price of 41 of 64 lanes.
+template <int PF>
+__global__ void __launch_bounds__(256) w4d(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, int stripes) {
+  const long long wave = (xcd_block() * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= stripes) return;
+  const bool act = lane < 41;
+  const int p = lane >= 40 ? SUB - 4 : 4 * lane;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(in + wave * STRIDE), 0, (int)STRIDE, 0x00020000);
+  const int lb = act ? p : (int)0x80000000;
+  uint32_t acc[M][8];
+#pragma unroll
+  for (int r = 0; r < M; ++r)
+#pragma unroll
+    for (int y = 0; y < 8; ++y) acc[r][y] = 0;
+  uint32_t ring[PF][8];
+#pragma unroll
+  for (int q = 0; q < PF; ++q)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) ring[q][b] = __builtin_amdgcn_raw_buffer_load_b32(rs, lb + b * SUB, q * BYTES, 2);
+#pragma unroll
+  for (int x = 0; x < K; ++x) {
+    uint32_t nxt[8];
+    if (x + PF < K)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) nxt[b] = __builtin_amdgcn_raw_buffer_load_b32(rs, lb + b * SUB, (x + PF) * BYTES, 2);
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+#pragma unroll
+      for (int y = 0; y < 8; ++y) acc[r][y] ^= ring[x % PF][(y + r + x) & 7];
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+#pragma unroll
+      for (int y = 0; y < 8; ++y) asm volatile("" : "+v"(acc[r][y]));
+    if (x + PF < K)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) ring[x % PF][b] = nxt[b];
+  }
+  if (!act) return;
+  uint8_t *o = out + wave * STRIDE + OUT_OFF + p;
+#pragma unroll
+  for (int r = 0; r < M; ++r)
+#pragma unroll
+    for (int y = 0; y < 8; ++y)
+      __builtin_nontemporal_store(acc[r][y] ^ ((uint32_t)r * 0x01010101u), (uint32_t *)(o + r * BYTES + y * SUB));
+}
+
+// w4l: the same lanes, each column landed in an LDS ring by 2 LDS-DMA instructions (81 x 16 B:
+// lanes 0..63, then 0..16) -- one contiguous 1296-B read per column -- and read back per lane:
+// even sub-blocks (4-byte aligned) one ds_read_b32, odd ones two dwords + v_alignbyte.
+template <int D>
+__global__ void __launch_bounds__(256) w4l(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, int stripes) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[4][D][1536];
+  const long long wave = (xcd_block() * 256 + threadIdx.x) >> 6;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (wave >= stripes) return;
+  const bool act = lane < 41;
+  const int p = lane >= 40 ? SUB - 4 : 4 * lane;
+  const uint8_t *src0 = in + wave * STRIDE + lane * 16;
+  const uint8_t *src1 = in + wave * STRIDE + (lane < 17 ? 64 + lane : 80) * 16;
+  auto issue = [&](int x, int sl) {
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src0 + x * BYTES),
+                                     (__attribute__((address_space(3))) void *)&ring[w][sl][0], 16, 0, 2);
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src1 + x * BYTES),
+                                     (__attribute__((address_space(3))) void *)&ring[w][sl][1024], 16, 0, 2);
+  };
+#pragma unroll
+  for (int q = 0; q < D; ++q) issue(q, q);
+  uint32_t acc[M][8];
+#pragma unroll
+  for (int r = 0; r < M; ++r)
+#pragma unroll
+    for (int y = 0; y < 8; ++y) acc[r][y] = 0;
+#pragma unroll
+  for (int x = 0; x < K; ++x) {
+    const int left = std::min(D - 1, K - 1 - x);  // columns issued after x (2 DMA each)
+    switch (left) {  // vmcnt(2 * left) (a constant per unrolled column)
+#define W4L_WAIT(L) case L: __builtin_amdgcn_s_waitcnt(((2 * L) & 15) | (((2 * L) >> 4) << 14) | (7 << 4) | (15 << 8)); break;
+      W4L_WAIT(0) W4L_WAIT(1) W4L_WAIT(2) W4L_WAIT(3) W4L_WAIT(4) W4L_WAIT(5) W4L_WAIT(6) W4L_WAIT(7)
+      W4L_WAIT(8) W4L_WAIT(9) W4L_WAIT(10) W4L_WAIT(11)
+#undef W4L_WAIT
+    }
+    asm volatile("" ::: "memory");
+    const uint8_t *t = ring[w][x % D];
+    uint32_t d[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int o = b * SUB + p;  // b odd: 2 mod 4
+      if (b % 2 == 0) {
+        d[b] = *(const uint32_t *)(t + o);
+      } else {
+        const uint32_t *q = (const uint32_t *)(t + o - 2);
+        d[b] = __builtin_amdgcn_alignbyte(q[1], q[0], 2);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+#pragma unroll
+      for (int y = 0; y < 8; ++y) acc[r][y] ^= d[(y + r + x) & 7];
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+#pragma unroll
+      for (int y = 0; y < 8; ++y) asm volatile("" : "+v"(acc[r][y]));
+    if (x + D < K) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      issue(x + D, x % D);
+    }
+  }
+  if (!act) return;
+  uint8_t *o = out + wave * STRIDE + OUT_OFF + p;
+#pragma unroll
+  for (int r = 0; r < M; ++r)
+#pragma unroll
+    for (int y = 0; y < 8; ++y)
+      __builtin_nontemporal_store(acc[r][y] ^ ((uint32_t)r * 0x01010101u), (uint32_t *)(o + r * BYTES + y * SUB));
+}
+
+
+// geop: geo S=1 G=37 on the stripe layout with the stores' cache-policy bits AUX (gfx950
+// buffer instructions: bit 0 sc0, bit 1 nt, bit 4 sc1) and the loads' LAUX.
+template <int SAUX, int LAUX>
+__global__ void __launch_bounds__(256) geop(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, int units,
+                                            long long OS, long long OO) {
+  constexpr int NC = 37;
+  const long long u = (xcd_block() * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (u >= units) return;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(in + u * STRIDE), 0, (int)STRIDE, 0x00020000);
+  u32x4 ring[NC], acc[4] = {};
+#pragma unroll
+  for (int j = 0; j < NC; ++j) ring[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, j * 1024, LAUX);
+#pragma unroll
+  for (int j = 0; j < NC; ++j) acc[j & 3] ^= ring[j];
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void *)(out + u * OS + OO), 0, M * BYTES, 0x00020000);
+#pragma unroll
+  for (int c = 0; c < 6; ++c)
+    if (c * 64 + lane < M * BYTES / 16)
+      __builtin_amdgcn_raw_buffer_store_b128(acc[c & 3] ^ u32x4{(uint32_t)c, 0, 0, 0}, ro, (c * 64 + lane) * 16, 0, SAUX);
+}
+
 // ---------------------------------------------------------------- driver
 static hipEvent_t e0, e1;
 template <class F>
@@ -697,6 +842,47 @@ int main(int argc, char **argv) {
     run("geo S=1 G=37 L=stripe US=stripe no output", geo<1, 37, 37>, 1, LS, LS, LS, 0, 0);
     run("geo S=1 G=4  L=stripe US=stripe no output", geo<1, 4, 37>, 1, LS, LS, LS, 0, 0);
     run("geo S=3 G=4  L=stripe US=stripe no output", geo<3, 4, 37>, 3, LS, LS, LS, 0, 0);
+  }
+
+  if (want(argc, argv, "w4")) {
+    const size_t ob = (size_t)(STRIPES * STRIDE);
+    std::vector<uint8_t> ref(ob), got(ob);
+    CK(hipMemset(dout, 0, ob));
+    enc_pat<3><<<g3, 256>>>(din, dout, (int)STRIPES);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(ref.data(), dout, ob, hipMemcpyDeviceToHost));
+    auto check = [&](const char *name) {
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(got.data(), dout, ob, hipMemcpyDeviceToHost));
+      size_t bad = 0;
+      for (long long s = 0; s < STRIPES; ++s)
+        for (long long i = 0; i < M * BYTES; ++i) bad += got[s * STRIDE + OUT_OFF + i] != ref[s * STRIDE + OUT_OFF + i];
+      printf("check %-34s %zu of %lld output bytes differ from enc\n", name, bad, (long long)OUT_BYTES);
+      fflush(stdout);
+    };
+    const int g1 = (int)((STRIPES + 3) / 4);
+#define W4(KER, P)                                                                                        \
+    {                                                                                                     \
+      char nm[64]; snprintf(nm, 64, #KER " %d (1 stripe per wave, dword lanes)", P);                        \
+      CK(hipMemset(dout, 0, ob));                                                                         \
+      KER<P><<<g1, 256>>>(din, dout, (int)STRIPES);                                                       \
+      check(nm);                                                                                          \
+      rep(nm, timeit([&] { KER<P><<<g1, 256>>>(din, dout, (int)STRIPES); }));                             \
+    }
+    W4(w4d, 3) W4(w4d, 6) W4(w4d, 10) W4(w4l, 4) W4(w4l, 8) W4(w4l, 12)
+  }
+
+  if (want(argc, argv, "pol")) {
+    auto run = [&](const char *nm, auto kern, long long OS, long long OO) {
+      const int units = (int)STRIPES;
+      const float ms = timeit([&] { kern<<<(units + 3) / 4, 256>>>(din, dout, units, OS, OO); });
+      printf("%-52s %8.4f ms %8.1f GB/s input\n", nm, ms, IN_BYTES / (ms * 1e-3) / 1e9);
+      fflush(stdout);
+    };
+#define POL(S, L)                                                                                       \
+    run("pol stores aux=" #S " loads aux=" #L " out bench", geop<S, L>, STRIDE, OUT_OFF);                \
+    run("pol stores aux=" #S " loads aux=" #L " out compact", geop<S, L>, M * BYTES, 0);
+    POL(2, 2) POL(0, 2) POL(1, 2) POL(3, 2) POL(16, 2) POL(17, 2) POL(18, 2) POL(19, 2) POL(2, 0) POL(0, 0)
   }
   CK(hipGetLastError());
   CK(hipDeviceSynchronize());
