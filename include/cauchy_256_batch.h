@@ -98,7 +98,9 @@ const char *cauchy_256_last_launch(void);
  * 1 = run-time specialised (JIT) network, 2 (decode only) = specialised network with the
  * erasure plan computed inside the same kernel, 3 (encode only) = run-time specialised
  * 4-bit-windowed network for large m, 4 (decode only) = per-stripe planner + fused
- * windowed decode for large m (m <= 64).  `what` = 0 for encode, 1 for decode. */
+ * windowed decode for large m (m <= 64).  `what` = 0 for encode, 1 for decode; `what` = 2:
+ * 1 when the shape's register networks (encode, and the decode with the in-kernel plan)
+ * stage their columns in LDS by LDS-DMA, else 0. */
 int cauchy_256_batch_path(int k, int m, int block_bytes, int what);
 
 /* Compile the specialised kernels of a shape into the on-disk code-object cache

@@ -319,16 +319,29 @@ def batch_path(k, m, block_bytes, decode=False):
     return {0: "generic", 1: "jit", 2: "jit-fused", 3: "jit-win", 4: "jit-wide"}[code]
 
 
+def lds_staged(k, m, block_bytes):
+    """True when the shape's register networks stage their columns by LDS-DMA (jit.cpp
+    jit_config_for, jit_codec.hip LH_LDS)."""
+    return lib().cauchy_256_batch_path(k, m, block_bytes, 2) == 1
+
+
 def kernel_names(k, m, block_bytes):
     """Names of the kernels one encode_batch / decode_batch launches for this shape."""
     sub = block_bytes // 8
     small = sub < 4  # the generic kernels below dword lanes
-    nch = (sub + 3) // 4  # decode in place: the overlapping last lane must share its neighbour's workgroup
-    old_dec = small or (sub % 4 != 0 and nch > 1 and (nch - 1) % 64 == 0)
-    enc = {"generic": ["lh_apply_generic_kernel" if small else "lh_apply_jump_kernel"], "jit": ["lh_jit_encode"],
+
+    def lone_tail(w):  # decode in place: the overlapping last lane must share its neighbour's workgroup
+        nch = (sub + w - 1) // w
+        return sub % w != 0 and nch > 1 and (nch - 1) % 64 == 0
+
+    old_dec = small or lone_tail(4)
+    two_dec = sub >= 512 and min(k, m) <= 4 and not lone_tail(8)  # codec.cpp jump_layout
+    two_enc = sub >= 8 and m <= 4
+    jump_enc = "lh_apply_generic_kernel" if small else ("lh_apply_jump2_kernel" if two_enc else "lh_apply_jump_kernel")
+    enc = {"generic": [jump_enc], "jit": ["lh_jit_encode"],
            "jit-win": ["lh_jit_encode_win"]}[batch_path(k, m, block_bytes)]
     dec = {"generic": ["lh_plan_kernel"] + (["lh_apply_generic_kernel", "lh_scatter_kernel"] if old_dec
-                                            else ["lh_apply_jump_kernel"]),
+                                            else ["lh_apply_jump2_kernel" if two_dec else "lh_apply_jump_kernel"]),
            "jit": ["lh_plan_small_kernel" if min(k, m) <= 8 else "lh_plan_kernel", "lh_jit_decode"],
            "jit-fused": ["lh_jit_decode_fused"],
            "jit-wide": ["lh_plan_kernel", "lh_jit_decode_wide", "lh_inverse_gt_kernel"],

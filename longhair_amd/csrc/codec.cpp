@@ -158,6 +158,7 @@ struct Workspace {
 struct Device {
     int id = 0;
     int cus = 0;                         // compute units
+    bool jump2 = false;                  // lh_apply_jump2_kernel may run (jump_table2_usable)
     std::mutex mu;                       // guards maps below and the drop-in staging
     uint8_t *gf_exp = nullptr;           // 512 B
     int16_t *gf_log = nullptr;           // 256 x int16
@@ -212,6 +213,7 @@ static int current_device(Device **out) {
         LH_HIP(hipMemcpy(d->gf_exp, F.exp, 512, hipMemcpyHostToDevice));
         LH_HIP(hipMemcpy(d->gf_log, F.log, 256 * sizeof(int16_t), hipMemcpyHostToDevice));
         LH_HIP(hipDeviceGetAttribute(&d->cus, hipDeviceAttributeMultiprocessorCount, id));
+        d->jump2 = jump_table2_usable(id);
         slot = std::move(d);
     }
     *out = slot.get();
@@ -322,6 +324,28 @@ static const JitKernels *jit_lookup(Device *d, const JitConfig &cfg, bool allow_
 }
 
 // ------------------------------------------------------------------------ encode
+// The jump-table apply's lane width (a.sub, a.n_out, a.per_stripe set): two-dword lanes
+// (lh_apply_jump2_kernel: a jump covers 8 bytes per lane) only where a one-dword wave would be
+// half empty -- at most 4 outputs -- and the lanes stay full: a flat (encode) launch with
+// sub >= 8, an in-place decode with sub >= 512.  With more outputs the one-dword form wins
+// (its wave carries 8 outputs per jump target fetch; profiles/r5f_jump_dw.txt: k128/m32
+// encode 5.31 ms one-dword, 8.27 two-dword; k29/m4 encode 0.700 / 0.665).  In place, the last
+// lane of a sub-block (shifted back over its neighbour when the width does not divide sub)
+// must share its neighbour's workgroup, whose barrier orders every read of a slot before its
+// overwrite.
+static void jump_layout(const Device *d, JumpApplyArgs &a, bool in_place) {
+    auto lone_tail = [&](int w) {
+        const int nch = (a.sub + w - 1) / w;
+        return a.sub % w != 0 && nch > 1 && (nch - 1) % 64 == 0;
+    };
+    bool two = a.n_out <= 4 && a.sub >= 8 && (!in_place || (a.sub >= 512 && !lone_tail(8)));
+    const char *fb = std::getenv("LONGHAIR_AMD_INV_FALLBACK");  // (tests: the in-asm table)
+    if (fb && std::atoi(fb)) two = false;
+    a.dw = two && d->jump2 ? 2 : 1;
+    a.nch = (a.sub + 4 * a.dw - 1) / (4 * a.dw);
+    a.wps = (a.nch + 63) / 64;
+}
+
 static int xor_rows(int k, int n_rep, int bytes, int stripes, const uint8_t *in, long long in_stride,
                     uint8_t *out, long long out_stride, hipStream_t st) {
     XorArgs a{};
@@ -407,9 +431,9 @@ static int encode_batch(int k, int m, int bytes, int stripes, const uint8_t *d_d
         a.n_out = m;
         a.bytes = bytes;
         a.sub = bytes / 8;
-        a.nch = (a.sub + 3) / 4;
         a.stripes = stripes;
         a.per_stripe = 0;
+        jump_layout(d, a, false);
         LH_HIP(launch_apply_jump(a, st));
         return kOk;
     }
@@ -604,10 +628,9 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         a.n_out = e_max;
         a.bytes = bytes;
         a.sub = sub;
-        a.nch = jnch;
         a.stripes = stripes;
         a.per_stripe = 1;
-        a.wps = (jnch + 63) / 64;
+        jump_layout(d, a, true);
         LH_HIP(launch_apply_jump(a, st));
         return kOk;
     }
@@ -1527,6 +1550,8 @@ LH_API int cauchy_256_jit_precompile(int k, int m, int block_bytes) {
 LH_API int cauchy_256_batch_path(int k, int m, int block_bytes, int what) {
     LH_TRY
         lh::JitConfig cfg;
+        if (what == 2)  // 1: the register networks stage their columns by LDS-DMA (LH_LDS)
+            return lh::jit_config_for(k, m, block_bytes, false, &cfg) && cfg.lds ? 1 : 0;
         if (!lh::jit_config_for(k, m, block_bytes, what == 1, &cfg)) {
             if (what == 0) return lh::jit_win_config_for(k, m, block_bytes, &cfg) ? 3 : 0;
             return lh::jit_win_config_for(k, m, block_bytes, &cfg, true) ? 4 : 0;

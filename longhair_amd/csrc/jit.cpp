@@ -82,6 +82,24 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     cfg->nch = nch2;
     cfg->spw = spw;
     cfg->wps = wps;
+    // LDS-DMA column staging (jit_codec.hip LH_LDS): 8-byte lanes, whole stripes per wave,
+    // 16-byte-multiple blocks (a DMA chunk never spans two blocks) and, when the last chunk
+    // of a sub-block is partial, every stripe's last lane in the same 16-lane DPP row as its
+    // neighbour (its stores funnel that lane's word through row_shr:1).
+    cfg->lds = 0;
+    if (W == 8 && nch2 <= 64 && bytes % 16 == 0) {
+        bool dpp_ok = true;
+        if (sub - 8 * (nch2 - 1) != 8)
+            for (int s = 0; s < spw; ++s) dpp_ok = dpp_ok && (s * nch2 + nch2 - 1) % 16 != 0;
+        cfg->lds = dpp_ok ? 1 : 0;
+    }
+    // One role per module: an encode module holds lh_jit_encode only, a decode module the one
+    // decode kernel its calls launch (the fused plan for e_max <= 4, one stripe per <= 64
+    // lanes, k <= 64, unless LONGHAIR_AMD_NO_FUSED_PLAN).  A module with all three compiled
+    // three copies of the network (six when encode and decode pick different lane widths,
+    // as m = 3 does), of which a call uses one.
+    cfg->role = decode ? 2 : 1;
+    cfg->plain = decode && !(emax <= 4 && nch2 <= 64 && k <= 64 && std::getenv("LONGHAIR_AMD_NO_FUSED_PLAN") == nullptr);
     cfg->defines.clear();
     if (const char *d = std::getenv("LONGHAIR_AMD_JIT_DEFINES")) cfg->defines = d;
     return true;
@@ -91,6 +109,7 @@ bool jit_ptr_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     if (!jit_config_for(k, m, bytes, decode, cfg)) return false;
     if ((long long)(cfg->spw ? cfg->spw : 1) * k > 1024) return false;  // LDS: 4 waves x 8 B x spw x (k + 1) <= 35 KiB
     cfg->ptr = 1;
+    cfg->lds = 0;
     return true;
 }
 
@@ -483,6 +502,8 @@ std::string jit_source_for(const JitConfig &c) {
        << "\n#define LH_SUB " << c.sub << "\n#define LH_W " << c.W << "\n#define LH_NCH " << c.nch
        << "\n#define LH_SPW " << (c.spw ? c.spw : 1) << "\n#define LH_WPS " << (c.wps ? c.wps : 1) << "\n";
     if (c.ptr) os << "#define LH_PTR 1\n#define LH_BUF 0\n";
+    if (c.lds) os << "#ifndef LH_LDS\n#define LH_LDS 1\n#endif\n";  // (a LONGHAIR_AMD_JIT_DEFINES value wins)
+    if (c.role) os << "#define LH_ROLE " << c.role << "\n#define LH_DEC_PLAIN " << c.plain << "\n";
     const std::vector<uint8_t> g = generator_matrix(c.k, c.m);
     os << "static constexpr unsigned char LH_BM[" << c.m << "][" << c.k << "][8] = {";
     for (int r = 0; r < c.m; ++r) {
@@ -509,7 +530,8 @@ std::string jit_source_for(const JitConfig &c) {
 
 JitCache::Key JitCache::key_of(const JitConfig &cfg) {
     return Key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines,
-               cfg.ptr * 100000000 + cfg.win_split * 1000000 + cfg.win * 100000 + cfg.win_lds * 10000 +
+               cfg.lds * 1000000000 + cfg.ptr * 100000000 + (cfg.role + 3 * cfg.plain) * 10000000 +
+                   cfg.win_split * 1000000 + cfg.win * 100000 + cfg.win_lds * 10000 +
                    cfg.rows_per_wave * 100 + cfg.win_pf);
 }
 
@@ -749,8 +771,9 @@ const JitKernels *JitCache::load_locked(const Key &key, const JitConfig &cfg, st
     kern.decode_fused = fn("lh_jit_decode_fused");
     kern.encode_win = fn("lh_jit_encode_win");
     kern.decode_wide = fn("lh_jit_decode_wide");
-    if (!kern.encode && !kern.encode_win && !kern.decode_wide) {
-        *err = "specialised module has no encode kernel";
+    // (one role per register-network module: the encode, or one of the two decodes)
+    if (!kern.encode && !kern.decode && !kern.decode_fused && !kern.encode_win && !kern.decode_wide) {
+        *err = "specialised module has no kernel";
         return nullptr;
     }
     not_cached_.erase(key);

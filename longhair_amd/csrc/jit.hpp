@@ -29,6 +29,11 @@ struct JitConfig {
                           // (0: the fused kernel, phase B from an LDS tile of V)
     int ptr = 0;          // register networks: blocks addressed through a pointer table (LH_PTR,
                           // cauchy_256_*_batch_ptrs)
+    int lds = 0;          // register networks: columns staged by LDS-DMA (LH_LDS, jit_codec.hip)
+    int role = 0;         // register networks: 1 = the encode module (lh_jit_encode only),
+                          // 2 = the decode module: lh_jit_decode_fused, or lh_jit_decode when
+                          // the fused plan does not apply or is switched off (plain = 1)
+    int plain = 0;
     int lanes_per_launch_unit() const { return 64; }
 };
 

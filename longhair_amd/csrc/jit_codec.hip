@@ -449,6 +449,8 @@ struct lh_unroll_encode<LH_K> {
 // boxes (profiles/r5a/r5c_ubench_floor.txt, `ldsd`).  The last lane of a stripe reads its
 // chunk unshifted (only LH_VLAST bytes are its own) and stores [sub - 8, sub) assembled with
 // the previous lane's word (DPP row_shr:1; the host checks both lanes share a DPP row).
+// That last lane's word pair may reach up to 16 bytes past its stripe's image (bytes that are
+// never its own): each ring carries 16 bytes of padding, so the read stays in the wave's ring.
 #ifndef LH_LDS
 #define LH_LDS 0
 #endif
@@ -505,6 +507,31 @@ __device__ __forceinline__ void lh_slot_col(lh_word (&d)[8], const unsigned char
 __device__ __forceinline__ unsigned lh_row_shr1(unsigned v) {  // lane i <- lane i - 1 within a DPP row of 16
     return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
 }
+typedef unsigned int lh_u32x4a __attribute__((ext_vector_type(4)));
+// An 8-byte word into LDS at an address A (mod 8) bytes past an 8-byte boundary, in naturally
+// aligned pieces (a misaligned ds_write_b64 would replay like the reads).
+template <int A>
+__device__ __forceinline__ void lh_lds_put(unsigned char *p, const lh_word &w) {
+    if constexpr (A == 0) {
+        lh_u32x2a v;
+        v.x = w.v[0]; v.y = w.v[1];
+        *(lh_u32x2a *)p = v;
+    } else if constexpr (A == 4) {
+        ((unsigned *)p)[0] = w.v[0];
+        ((unsigned *)p)[1] = w.v[1];
+    } else {
+        typedef unsigned short lh_u16a __attribute__((aligned(2)));
+        *(lh_u16a *)(p + 0) = (unsigned short)w.v[0];
+        *(lh_u16a *)(p + 2) = (unsigned short)(w.v[0] >> 16);
+        *(lh_u16a *)(p + 4) = (unsigned short)w.v[1];
+        *(lh_u16a *)(p + 6) = (unsigned short)(w.v[1] >> 16);
+    }
+}
+// LH_LDS_FLAT_ST: the encode's recovery blocks leave through the ring (below) when the
+// wave's output image fits it.
+#ifndef LH_LDS_FLAT_ST
+#define LH_LDS_FLAT_ST (LH_SPW * LH_M * LH_BYTES <= LH_LD * LH_LQ * 1024)
+#endif
 struct lh_ldsrc {
     const unsigned char *src[LH_LQ];  // this lane's chunk of DMA instruction q, column 0
     unsigned char *ring;              // this wave's LH_LD slots of LH_LQ KiB
@@ -542,10 +569,29 @@ struct lh_unroll_encode_lds {
     }
 };
 
+// Sub-rows Y.. of one output row into the ring image (LH_LDS_FLAT_ST): the last lane's
+// word funnelled as for a direct store and written at its own alignment.
+template <int Y>
+__device__ __forceinline__ void lh_img_row(unsigned char *row, const lh_word (&a)[8], bool last, bool on) {
+    if constexpr (Y < 8) {
+        lh_word w = a[Y];
+        if constexpr (LH_VLAST != 8) {
+            const lh_word f = lh_funnel<LH_VLAST>(lh_row_shr1(w.v[0]), lh_row_shr1(w.v[1]), w.v[0], w.v[1]);
+            w.v[0] = last ? f.v[0] : w.v[0];
+            w.v[1] = last ? f.v[1] : w.v[1];
+        }
+        if (on) {
+            if (last) lh_lds_put<((Y + 1) * LH_SUB) % 8>(row + Y * LH_SUB, w);
+            else lh_lds_put<(Y * LH_SUB) % 8>(row + Y * LH_SUB, w);
+        }
+        lh_img_row<Y + 1>(row, a, last, on);
+    }
+}
+
 __device__ __forceinline__ void lh_encode_wave_lds(long long wave, const unsigned char *__restrict__ in,
                                                    long long in_stride, unsigned char *__restrict__ out,
                                                    long long out_stride, int stripes) {
-    __shared__ __attribute__((aligned(16))) unsigned char lh_lring[4][LH_LD * LH_LQ * 1024];
+    __shared__ __attribute__((aligned(16))) unsigned char lh_lring[4][LH_LD * LH_LQ * 1024 + 16];
     const int lane = threadIdx.x & 63;
     const int sl = lane / LH_NCH, c = lane - sl * LH_NCH;
     const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)wave) * LH_SPW;  // wave-uniform
@@ -575,6 +621,41 @@ __device__ __forceinline__ void lh_encode_wave_lds(long long wave, const unsigne
     asm volatile("" : "+v"(lo8));
     lh_unroll_encode_lds<0>::run(acc, S, lo, lo8);
     const bool last = c == LH_NCH - 1;
+#if LH_LDS_FLAT_ST
+    // The wave's recovery blocks [stripe][row][bytes] assembled in its (now idle) ring, then
+    // stored as aligned 16-byte chunks, chunk j = 64 q + lane: half the store instructions of
+    // the per-lane 8-byte stores, each a contiguous 1 KiB run (profiles/r5c_ubench_floor.txt
+    // `flat`: 0.532 against 0.544 ms).  A lane writes its word of sub-row y at offset
+    // y * sub + 8 c of the row (the last lane its funnelled [sub - 8, sub)) in naturally
+    // aligned pieces, the alignment a compile-time constant per sub-row and lane kind.
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every ring read of the last column done
+    {
+        unsigned char *img = S.ring + (sl < LH_SPW ? sl : LH_SPW - 1) * (LH_M * LH_BYTES) + (last ? LH_SUB - 8 : 8 * c);
+        // (the last lane's word starts at y * sub + sub - 8: its own alignment, a second case)
+#pragma unroll
+        for (int r = 0; r < LH_M; ++r) lh_img_row<0>(img + r * LH_BYTES, acc[r], last, sl < nst);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the image is complete (one wave: in order)
+    {
+        constexpr int per = LH_M * LH_BYTES / 16;  // chunks per stripe
+        const int n = nst * per;
+#pragma unroll
+        for (int q = 0; q < (LH_SPW * per + 63) / 64; ++q) {
+            const int j = 64 * q + lane;
+            if (j < n) {
+                const int js = j / per, t = j - js * per;
+                const lh_u32x4a v = *(const lh_u32x4a *)(S.ring + js * (LH_M * LH_BYTES) + t * 16);
+                unsigned char *dst = out + (s0 + js) * out_stride + t * 16;
+#if LH_NT_ST
+                __builtin_nontemporal_store(v, (lh_u32x4a *)dst);
+#else
+                *(lh_u32x4a *)dst = v;
+#endif
+            }
+        }
+    }
+    return;
+#endif
     if (sl >= nst) return;
     unsigned char *o = out + (s0 + sl) * out_stride + (last ? LH_SUB - 8 : 8 * c);
 #pragma unroll
@@ -644,7 +725,13 @@ __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned ch
         for (int y = 0; y < 8; ++y) lh_store(o + (long long)r * LH_BYTES + y * LH_SUB, acc[r][y]);
 }
 
-#if 1
+// LH_ROLE (jit.cpp): 1 = the encode module, 2 = the decode module (LH_DEC_PLAIN: lh_jit_decode,
+// else lh_jit_decode_fused); undefined (the build-time syntax check) = every kernel.
+#ifndef LH_ROLE
+#define LH_ROLE 0
+#define LH_DEC_PLAIN 0
+#endif
+#if LH_ROLE != 2
 // recovery[s][r] = sum_x B(G[r][x]) data[s][x]   (cauchy_256_encode for m > 1, valid k, m)
 #ifndef LH_ENC_LB
 #define LH_ENC_LB 1  // min waves per SIMD the register allocator must allow (tools/tune.py)
@@ -770,10 +857,10 @@ __device__ __forceinline__ void lh_load_col(lh_word (&d)[8], const lh_dsrc &S, u
 #endif
 // Decode column X in stream order: data column x (the slot holding original x) or
 // recovery row r.
-template <int X>
+template <int X, int RF = LH_REC_FIRST>
 struct lh_dcol {
-    static constexpr bool rec = LH_REC_FIRST ? (X < LH_M) : (X >= LH_K);
-    static constexpr int idx = LH_REC_FIRST ? (X < LH_M ? X : X - LH_M) : (X < LH_K ? X : X - LH_K);
+    static constexpr bool rec = RF ? (X < LH_M) : (X >= LH_K);
+    static constexpr int idx = RF ? (X < LH_M ? X : X - LH_M) : (X < LH_K ? X : X - LH_K);
     static constexpr int x = rec ? 0 : (idx < LH_K ? idx : 0);
     static constexpr int r = rec ? (idx < LH_M ? idx : 0) : 0;
 };
@@ -784,13 +871,13 @@ __device__ __forceinline__ unsigned int lh_dcol_slot(const unsigned int (&srcw)[
     return LH_BYTE(srcw, lh_dcol<X>::x);
 }
 
-template <int X>
+template <int X, int RF = LH_REC_FIRST>
 __device__ __forceinline__ void lh_dcombine(lh_word (&acc)[LH_M][8], const lh_word (&d)[8]) {
-    if constexpr (lh_dcol<X>::rec) {
+    if constexpr (lh_dcol<X, RF>::rec) {
 #pragma unroll
-        for (int y = 0; y < 8; ++y) lh_xor(acc[lh_dcol<X>::r][y], d[y]);
+        for (int y = 0; y < 8; ++y) lh_xor(acc[lh_dcol<X, RF>::r][y], d[y]);
     } else {
-        lh_column<lh_dcol<X>::x>(acc, d);
+        lh_column<lh_dcol<X, RF>::x>(acc, d);
     }
 }
 
@@ -998,7 +1085,7 @@ __device__ __forceinline__ void lh_decode_wave(long long wave, unsigned char *__
     lh_decode_body<LH_PF_DEC>(l, wave, blocks, stripe_stride, pr, zero_page, stripes, lh_no_prep());
 }
 
-#if 1
+#if LH_ROLE == 0 || (LH_ROLE == 2 && (LH_DEC_PLAIN || !(LH_EMAX <= 4 && LH_NCH <= 64 && LH_K <= 64)))
 extern "C" __global__ void __launch_bounds__(256)
 lh_jit_decode(unsigned char *__restrict__ blocks, long long stripe_stride,
               const unsigned char *__restrict__ plan, long long plan_stride,
@@ -1275,6 +1362,181 @@ __device__ __forceinline__ void lh_fused_solve::operator()(lh_plan_regs &pr) con
     for (int q = 0; q < LH_NOUT; ++q) asm volatile("" : "+v"(pr.outw[q]));
 }
 
+#if LH_LDS
+// The fused decode with its columns staged like the encode's (LH_LDS = 1): the wave's
+// LH_SPW stripes of column X (stream order, lh_dcol) arrive as LH_LQ buffer_load_dwordx4
+// ... lds per column into the wave's ring, chunk j = 64 q + lane of the image
+// [stripe][bytes].  A DMA lane takes its stripe's slot for X from the plan's slot maps in
+// the wave's LDS scratch (lh_fused_plan); an absent column (erased original, missing
+// recovery row) or a stripe with nothing to do gets an out-of-range offset: zeros into the
+// ring, no memory request.  Compute lanes read their words as the encode's do and store
+// the recovered blocks as it stores recovery blocks (the last lane of a stripe funnels the
+// previous lane's word).
+// Column order and cache policy of this form (profiles/r5i_tune_k29m4_lds_dec.txt, k29/m4:
+// 0.611 ms register ring; 0.588 staged, recovery rows first, default policy; 0.577 recovery
+// rows last with non-temporal loads -- the slots the outputs overwrite are then no longer
+// L2-resident when the stores arrive, the pattern DESIGN.md 5.2 measured for the stores).
+#ifndef LH_LDS_REC_FIRST
+#define LH_LDS_REC_FIRST 0
+#endif
+#ifndef LH_LDS_NT_DEC
+#define LH_LDS_NT_DEC 1
+#endif
+#define LH_SR_SRC LH_P4(LH_K)        // scratch offsets of the src / rec slot maps
+#define LH_SR_REC (2 * LH_P4(LH_K))
+template <int X>
+struct lh_dmoff {  // scratch offset of column X's slot byte
+    using D = lh_dcol<X, LH_LDS_REC_FIRST>;
+    static constexpr int v = D::rec ? LH_SR_REC + D::r : LH_SR_SRC + D::x;
+};
+struct lh_dldsrc {
+    __amdgpu_buffer_rsrc_t rs;
+    int joff[LH_LQ];  // DMA chunk q: byte offset in the wave's stripes (block 0)
+    int jsc[LH_LQ];   // ... its stripe's scratch offset, or -1: nothing to do there
+    const unsigned char *scr;  // the wave's scratch (LDS)
+    unsigned char *ring;
+    template <int X>
+    __device__ __forceinline__ void slots(unsigned (&sv)[LH_LQ]) const {
+#pragma unroll
+        for (int q = 0; q < LH_LQ; ++q) {  // (unconditional read: no branch per chunk)
+            const unsigned b = scr[(jsc[q] & 0x7FFFFFFF) + lh_dmoff<X>::v];
+            sv[q] = jsc[q] < 0 ? 0xFFu : b;
+        }
+    }
+    __device__ __forceinline__ void issue(const unsigned (&sv)[LH_LQ], int slot) const {
+#pragma unroll
+        for (int q = 0; q < LH_LQ; ++q)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, (__attribute__((address_space(3))) void *)(ring + slot * (LH_LQ * 1024) + q * 1024), 16,
+                sv[q] == 0xFFu ? (int)0x80000000 : joff[q] + (int)sv[q] * LH_BYTES, 0, 0, LH_LDS_NT_DEC ? 2 : 0);
+    }
+};
+template <int X>
+struct lh_unroll_decode_lds {
+    __device__ __forceinline__ static void run(lh_word (&v)[LH_M][8], const lh_dldsrc &S, int lo, int lo8) {
+        if constexpr (X < LH_DCOLS) {
+            constexpr int ahead = (LH_LD - 1) < (LH_DCOLS - 1 - X) ? (LH_LD - 1) : (LH_DCOLS - 1 - X);
+            unsigned sv[LH_LQ];
+            if constexpr (X + LH_LD < LH_DCOLS) S.slots<(X + LH_LD < LH_DCOLS ? X + LH_LD : 0)>(sv);
+            lh_wait_vmcnt<LH_LQ * ahead>();
+            asm volatile("" ::: "memory");  // no LDS read moves above the wait
+            lh_word d[8];
+            lh_slot_col(d, S.ring + (X % LH_LD) * (LH_LQ * 1024), lo, lo8);
+            lh_dcombine<X, LH_LDS_REC_FIRST>(v, d);
+            lh_dopaque(v);
+            if constexpr (X + LH_LD < LH_DCOLS) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done
+                S.issue(sv, X % LH_LD);
+            }
+            lh_unroll_decode_lds<X + 1>::run(v, S, lo, lo8);
+        }
+    }
+};
+template <int X = 0>
+__device__ __forceinline__ void lh_decode_lds_prologue(const lh_dldsrc &S) {
+    if constexpr (X < LH_LD && X < LH_DCOLS) {
+        unsigned sv[LH_LQ];
+        S.slots<X>(sv);
+        S.issue(sv, X);
+        lh_decode_lds_prologue<X + 1>(S);
+    }
+}
+// One wave's stripe group; `work`: this lane's stripe has a plan (lh_fused_plan true).
+// Every lane of the wave runs this (the DMAs need them all); only working lanes solve and store.
+__device__ __forceinline__ void lh_fused_wave_lds(const lh_lane &l, long long wave, int c, int sl, bool work,
+                                                  const unsigned char *scr, unsigned char *__restrict__ blocks,
+                                                  long long stripe_stride, int stripes, const lh_fused_solve &sv,
+                                                  lh_plan_regs &pr) {
+    __shared__ __attribute__((aligned(16))) unsigned char lh_dring[4][LH_LD * LH_LQ * 1024 + 16];
+    const int lane = threadIdx.x & 63;
+    const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)wave) * LH_SPW;  // wave-uniform
+    if (s0 >= stripes) return;  // wave-uniform
+    const int nst = (int)((stripes - s0) < LH_SPW ? (stripes - s0) : LH_SPW);
+    const unsigned long long wm = __ballot(work);
+    if (wm == 0) return;  // wave-uniform
+    lh_dldsrc S;
+    S.rs = __builtin_amdgcn_make_buffer_rsrc(blocks + s0 * stripe_stride, 0, (int)(nst * stripe_stride), 0x00020000);
+    S.scr = scr;
+    S.ring = lh_dring[threadIdx.x >> 6];
+#pragma unroll
+    for (int q = 0; q < LH_LQ; ++q) {
+        int j = 64 * q + lane;
+        if (j >= nst * (LH_BYTES / 16)) j = nst * (LH_BYTES / 16) - 1;  // (lands past the image)
+        const int js = j / (LH_BYTES / 16);
+        S.joff[q] = js * (int)stripe_stride + (j - js * (LH_BYTES / 16)) * 16;
+        S.jsc[q] = js * LH_SR | (((wm >> (js * LH_NCH)) & 1ull) ? 0 : (int)0x80000000);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous group's ring reads are done
+    lh_decode_lds_prologue(S);
+    if (work) sv(pr);  // the solve, while the first columns land
+    lh_word v[LH_M][8];
+#pragma unroll
+    for (int r = 0; r < LH_M; ++r)
+#pragma unroll
+        for (int y = 0; y < 8; ++y)
+#pragma unroll
+            for (int i = 0; i < LH_NW; ++i) v[r][y].v[i] = 0;
+    const int lo = (sl < LH_SPW ? sl : LH_SPW - 1) * LH_BYTES + 8 * c;
+    int lo8 = lo + 8;
+    asm volatile("" : "+v"(lo8));
+    lh_unroll_decode_lds<0>::run(v, S, lo, lo8);
+    if (!work) return;
+    // Phase B as lh_dec_phase_b; the stores as the LDS encode's.  (Storing the recovered
+    // blocks through the ring as the encode does measured slower in place:
+    // profiles/r5l_tune_k29m4_flat_dec.txt, 0.604 against 0.574 ms.)
+    const int e = pr.e;
+    const bool last = l.last;
+    unsigned char *base = blocks + l.stripe * stripe_stride + (last ? LH_SUB - 8 : 8 * c);
+#pragma unroll
+    for (int i = 0; i < LH_EMAX; ++i) {
+        if (i < e) {  // stripe-uniform: the funnel's source lane is active too
+            lh_word o[8];
+#pragma unroll
+            for (int y = 0; y < 8; ++y)
+#pragma unroll
+                for (int q = 0; q < LH_NW; ++q) o[y].v[q] = 0;
+#pragma unroll
+            for (int t = 7; t >= 0; --t) {
+                if (t != 7) {
+                    lh_word t7;
+#pragma unroll
+                    for (int q = 0; q < LH_NW; ++q) t7.v[q] = lh_x3(o[0].v[q], o[1].v[q], o[2].v[q]) ^ o[7].v[q];
+#pragma unroll
+                    for (int y = 0; y < 7; ++y) o[y] = o[y + 1];
+                    o[7] = t7;
+                }
+#pragma unroll
+                for (int r = 0; r < LH_M; ++r) {
+                    const int idx = i * LH_M + r;
+                    const unsigned int mask =
+                        (unsigned int)((int)(pr.coefw[idx / 4] << (31 - (8 * (idx % 4) + t))) >> 31);
+#pragma unroll
+                    for (int y = 0; y < 8; ++y)
+#pragma unroll
+                        for (int q = 0; q < LH_NW; ++q) o[y].v[q] = lh_xand(o[y].v[q], v[r][y].v[q], mask);
+                }
+#if LH_PIN_WORDS & 2
+                lh_pin8w(o);
+#else
+                lh_pin8(o);
+#endif
+            }
+            unsigned char *dst = base + (long long)LH_BYTE(pr.outw, i) * LH_BYTES;
+#pragma unroll
+            for (int y = 0; y < 8; ++y) {
+                lh_word w = o[y];
+                if constexpr (LH_VLAST != 8) {
+                    const lh_word f = lh_funnel<LH_VLAST>(lh_row_shr1(w.v[0]), lh_row_shr1(w.v[1]), w.v[0], w.v[1]);
+                    w.v[0] = last ? f.v[0] : w.v[0];
+                    w.v[1] = last ? f.v[1] : w.v[1];
+                }
+                lh_store(dst + y * LH_SUB, w);
+            }
+        }
+    }
+}
+#endif  // LH_LDS
+
 #ifndef LH_DEC_LB
 #define LH_DEC_LB 1  // min waves per SIMD the register allocator must allow (tools/tune.py)
 #endif
@@ -1305,16 +1567,24 @@ __device__ __forceinline__ void lh_fused_body(unsigned char *__restrict__ blocks
         sv.glog = glog;
         unsigned int rowv[LH_NRW];
         lh_fused_rows(l, c, rows, rowv);
+#if LH_LDS
+        (void)zero_page;
+        const bool work = l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr);
+        lh_fused_wave_lds(l, lh_w, c, sl, work, &scratch[wid][0][0], blocks, stripe_stride, stripes, sv, pr);
+#else
         if (l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr))
             lh_decode_body<PF>(l, lh_w, blocks, stripe_stride, pr, zero_page, stripes, sv);
+#endif
     }
 }
 
+#if LH_ROLE == 0 || (LH_ROLE == 2 && !LH_DEC_PLAIN)
 extern "C" __global__ void __launch_bounds__(256, LH_DEC_LB)
 lh_jit_decode_fused(unsigned char *__restrict__ blocks, long long stripe_stride, unsigned char *__restrict__ rows,
                     signed char *__restrict__ status, const unsigned char *__restrict__ zero_page,
                     const unsigned char *__restrict__ gf_exp, const short *__restrict__ gf_log, int stripes) {
     lh_fused_body<LH_PF_DEC>(blocks, stripe_stride, rows, status, zero_page, gf_exp, gf_log, stripes);
 }
+#endif
 
 #endif  // LH_EMAX <= 4 && LH_NCH <= 64 && LH_K <= 64

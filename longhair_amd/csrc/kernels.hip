@@ -31,6 +31,8 @@
 #include <stdint.h>
 
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "kernels.hpp"
 
@@ -1103,6 +1105,10 @@ __device__ __forceinline__ void lh_apply_jump_body(const lh::JumpApplyArgs &a, u
         const int i0 = 8 * (q * ng + g);
         int nout = n_out - i0;
         nout = nout < 0 ? 0 : (nout > 8 ? 8 : nout);  // wave-uniform
+        // In place (a single round): a wave past its stripe's e neither reads nor writes, and
+        // an ended wave no longer counts at the workgroup barrier, so it leaves now and frees
+        // its slot (random e: k200/m56 keeps ~half of each workgroup's waves).
+        if (pl && nout == 0) return;
         uint32_t acc[8][8];
 #pragma unroll
         for (int i = 0; i < 8; ++i)
@@ -1153,6 +1159,200 @@ __global__ void __launch_bounds__(1024) lh_apply_jump_kernel(lh::JumpApplyArgs a
         return;
     }
     lh_apply_jump_body<true>(a, tlo, thi);
+}
+
+// ---- two-dword form (a.dw == 2): a lane owns 8 bytes of every sub-block and a jump enters
+// lh_inv_gtab2, whose body c adds B(c) V to 16 accumulator words (tools/gen_inv_jump.py
+// render_global_table2) -- half the jumps per byte, at twice the table registers (60) and 4
+// outputs per wave.  ~150 VGPRs: at most 12 waves per workgroup (3 per SIMD).
+__global__ void lh_inv_gtab2_holder() { asm volatile(LH_INV_GTAB2_TEXT); }
+
+template <int N>
+__device__ __forceinline__ bool lh_mul_jump_g2(uint32_t (&acc)[4][16], const uint32_t (&tl)[16][2],
+                                               const uint32_t (&th)[16][2], const uint32_t (&t)[4], int r,
+                                               uint32_t tlo, uint32_t hi) {
+#if LH_GT_CHECK
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)t[i], r) - tlo;
+        if (d >= 256u * 132u || d % 132u != 0u) return false;  // wave-uniform
+    }
+#else
+    (void)tlo;
+#endif
+#define LH_GT2_CASE(n)                                                                                       \
+    if constexpr (N == n)                                                                                    \
+        asm volatile(LH_INV_JUMPG2_##n##_ASM : LH_INV_JUMPG2_##n##_OUTS(acc) : LH_INV_JUMPG2_INS(tl, th, t),  \
+                     [r] "s"(r), [hi] "s"(hi) : "s92", "s93", "s94", "s95", "s97", "scc");
+    LH_GT2_CASE(1) LH_GT2_CASE(2) LH_GT2_CASE(3) LH_GT2_CASE(4)
+#undef LH_GT2_CASE
+#if LH_GT_CHECK
+    if (__builtin_amdgcn_s_getreg(1 | (27 << 6) | (0 << 11)) != 0) return false;
+#endif
+    return true;
+}
+
+namespace {
+typedef unsigned long long lh_u64u __attribute__((aligned(1)));
+
+__device__ __forceinline__ void lh_ja_load2(uint32_t (&d)[8][2], const uint8_t *col, int sub, bool active) {
+#pragma unroll
+    for (int b = 0; b < 8; ++b) d[b][0] = d[b][1] = 0;
+    if (active) {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const unsigned long long v = *(const lh_u64u *)(col + (long long)b * sub);
+            d[b][0] = (uint32_t)v;
+            d[b][1] = (uint32_t)(v >> 32);
+        }
+    }
+}
+
+__device__ __forceinline__ void lh_ja_tables2(const uint32_t (&d)[8][2], uint32_t (&tl)[16][2],
+                                              uint32_t (&th)[16][2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        tl[0][h] = th[0][h] = 0;
+#pragma unroll
+        for (int q = 1; q < 16; ++q) {
+            const int low = __builtin_ctz(q), pre = q & (q - 1);
+            tl[q][h] = pre ? (tl[pre][h] ^ d[low][h]) : d[low][h];
+            th[q][h] = pre ? (th[pre][h] ^ d[4 + low][h]) : d[4 + low][h];
+        }
+    }
+}
+
+template <int N>
+__device__ __forceinline__ bool lh_ja_round2(const lh::JumpApplyArgs &a, const lh_ja_lane &l, const uint8_t *coef,
+                                             int i0, uint32_t (&acc)[4][16], uint32_t tlo, uint32_t thi) {
+    const int lane = threadIdx.x & 63;
+    const uint8_t *in = a.in + l.stripe * a.in_stride + l.p;
+    bool ok = true;
+    for (int jq = 0; jq * 64 < a.n_in; ++jq) {
+        const int jc = jq * 64 + lane;
+        uint32_t t[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t c = (i < N && jc < a.n_in) ? coef[(long long)(i0 + i) * a.n_in + jc] : 0u;
+            t[i] = tlo + c * 132u;
+        }
+        const int nj = a.n_in - jq * 64 < 64 ? a.n_in - jq * 64 : 64;
+        uint32_t cur[8][2];
+        lh_ja_load2(cur, in + (long long)(jq * 64) * a.bytes, a.sub, l.active);
+        for (int jl = 0; jl < nj; ++jl) {  // wave-uniform
+            const int jn = jq * 64 + jl + 1 < a.n_in ? jq * 64 + jl + 1 : jq * 64 + jl;
+            uint32_t nxt[8][2];
+            lh_ja_load2(nxt, in + (long long)jn * a.bytes, a.sub, l.active);
+            uint32_t tl[16][2], th[16][2];
+            lh_ja_tables2(cur, tl, th);
+            if (ok) ok = lh_mul_jump_g2<N>(acc, tl, th, t, jl, tlo, thi);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) cur[b][0] = nxt[b][0], cur[b][1] = nxt[b][1];
+        }
+    }
+    return ok;
+}
+
+// gt: the table's address is usable.  The host launches this kernel only after
+// probe_jump_tables found lh_inv_gtab2 within one 4 GiB page; a failed check here (or in the
+// debug build's target check) poisons the outputs, so the parity tests fail loudly.
+__device__ __forceinline__ void lh_apply_jump2_body(const lh::JumpApplyArgs &a, bool gt, uint32_t tlo,
+                                                    uint32_t thi) {
+    const int lane = threadIdx.x & 63;
+    const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), ng = (int)(blockDim.x >> 6);
+    lh_ja_lane l;
+    int c;
+    if (a.per_stripe) {
+        l.stripe = blockIdx.x / a.wps;
+        if (l.stripe >= a.stripes) return;  // workgroup-uniform
+        c = (int)(blockIdx.x % a.wps) * 64 + lane;
+        l.active = c < a.nch;
+        c = l.active ? c : a.nch - 1;
+    } else {
+        const long long t = (long long)blockIdx.x * 64 + lane;
+        l.stripe = t / a.nch;
+        c = (int)(t - l.stripe * a.nch);
+        l.active = l.stripe < a.stripes;
+        if (!l.active) l.stripe = a.stripes - 1;
+    }
+    l.p = c == a.nch - 1 ? a.sub - 8 : 8 * c;  // (the last chunk overlaps its neighbour)
+    const uint8_t *pl = a.plan ? a.plan + l.stripe * a.plan_stride : nullptr;
+    const int n_out = pl ? pl[0] : a.n_out;
+    if (pl && n_out == 0) return;  // workgroup-uniform
+    const uint8_t *coef = a.coef + l.stripe * a.coef_stride;
+    const int rounds = (a.n_out + 4 * ng - 1) / (4 * ng);
+    for (int q = 0; q < rounds; ++q) {
+        const int i0 = 4 * (q * ng + g);
+        int nout = n_out - i0;
+        nout = nout < 0 ? 0 : (nout > 4 ? 4 : nout);  // wave-uniform
+        if (pl && nout == 0) return;  // (as lh_apply_jump_body)
+        uint32_t acc[4][16];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int y = 0; y < 16; ++y) acc[i][y] = 0;
+        bool ok = gt;
+        if (gt) {
+            switch (nout) {  // wave-uniform
+                case 0: break;
+                case 1: ok = lh_ja_round2<1>(a, l, coef, i0, acc, tlo, thi); break;
+                case 2: ok = lh_ja_round2<2>(a, l, coef, i0, acc, tlo, thi); break;
+                case 3: ok = lh_ja_round2<3>(a, l, coef, i0, acc, tlo, thi); break;
+                default: ok = lh_ja_round2<4>(a, l, coef, i0, acc, tlo, thi); break;
+            }
+        }
+        if (pl && ng > 1) __syncthreads();  // in place: every slot read before any is written
+        if (l.active) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (i < nout) {
+                    uint8_t *dst = pl ? a.out + l.stripe * a.out_stride + (long long)pl[16 + i0 + i] * a.bytes
+                                      : a.out + l.stripe * a.out_stride + (long long)(i0 + i) * a.bytes;
+#pragma unroll
+                    for (int y = 0; y < 8; ++y) {
+                        const unsigned long long v = ok ? ((unsigned long long)acc[i][2 * y + 1] << 32) | acc[i][2 * y]
+                                                        : 0xDEADBEEFDEADBEEFull;
+                        *(lh_u64u *)(dst + l.p + (long long)y * a.sub) = v;
+                    }
+                }
+            }
+        }
+    }
+}
+}  // namespace
+
+__global__ void __launch_bounds__(768) lh_apply_jump2_kernel(lh::JumpApplyArgs a) {
+    uint32_t tlo, thi;
+    asm volatile(
+        "s_getpc_b64 s[92:93]\n"
+        "s_add_u32 s92, s92, lh_inv_gtab2@rel32@lo+4\n"
+        "s_addc_u32 s93, s93, lh_inv_gtab2@rel32@hi+12\n"
+        "s_mov_b32 %0, s92\n"
+        "s_mov_b32 %1, s93\n"
+        : "=s"(tlo), "=s"(thi)
+        :
+        : "s92", "s93", "scc");
+    lh_apply_jump2_body(a, tlo <= 0xFFFFFFFFu - 256u * 132u, tlo, thi);
+}
+
+// The low words of the two jump tables' addresses (out[0]: lh_inv_gtab, out[1]: lh_inv_gtab2),
+// read once per device: a table whose bodies straddle a 4 GiB boundary is not entered.
+__global__ void lh_jump_probe_kernel(uint32_t *out) {
+    uint32_t t1, t2;
+    asm volatile(
+        "s_getpc_b64 s[92:93]\n"
+        "s_add_u32 s92, s92, lh_inv_gtab@rel32@lo+4\n"
+        "s_mov_b32 %0, s92\n"
+        "s_getpc_b64 s[92:93]\n"
+        "s_add_u32 s92, s92, lh_inv_gtab2@rel32@lo+4\n"
+        "s_mov_b32 %1, s92\n"
+        : "=s"(t1), "=s"(t2)
+        :
+        : "s92", "s93", "scc");
+    if (threadIdx.x == 0) {
+        out[0] = t1;
+        out[1] = t2;
+    }
 }
 
 // ---------------------------------------------------------- pointer-table gather / scatter
@@ -1250,6 +1450,17 @@ hipError_t launch_apply_jump(const JumpApplyArgs &a, hipStream_t st) {
     // sub >= 4 (dword lanes); at most 16 waves of 8 outputs per workgroup; in place a single
     // round (e_max <= 128 always holds: e_max = min(k, m) and k + m <= 256).
     if (a.sub < 4 || a.n_out < 1 || a.n_in < 1 || a.nch < 1) return hipErrorInvalidValue;
+    if (a.dw == 2) {  // 4 outputs per wave, at most 12 waves, the rounds balanced over them
+        const int groups = (a.n_out + 3) / 4, rounds = (groups + 11) / 12, ng = (groups + rounds - 1) / rounds;
+        if (a.sub < 8 || (a.plan && rounds > 1)) return hipErrorInvalidValue;
+        const long long wgs = a.per_stripe ? (long long)a.stripes * a.wps : ((long long)a.stripes * a.nch + 63) / 64;
+        if (wgs <= 0) return hipSuccess;
+        if (wgs > 0x7FFFFFFF) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(lh_apply_jump2_kernel, dim3((unsigned)wgs), dim3(64u * (unsigned)ng), 0, st, a);
+        note_launch("lh_apply_jump2_kernel");
+        return hipGetLastError();
+    }
+    if (a.dw != 1) return hipErrorInvalidValue;
     const int ng = (a.n_out + 7) / 8 < 16 ? (a.n_out + 7) / 8 : 16;
     if (a.plan && a.n_out > 8 * ng) return hipErrorInvalidValue;
     const long long wgs = a.per_stripe ? (long long)a.stripes * a.wps : ((long long)a.stripes * a.nch + 63) / 64;
@@ -1258,6 +1469,24 @@ hipError_t launch_apply_jump(const JumpApplyArgs &a, hipStream_t st) {
     hipLaunchKernelGGL(lh_apply_jump_kernel, dim3((unsigned)wgs), dim3(64u * (unsigned)ng), 0, st, a);
     note_launch("lh_apply_jump_kernel");
     return hipGetLastError();
+}
+
+bool jump_table2_usable(int device) {
+    static std::mutex mu;
+    static std::map<int, bool> known;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = known.find(device);
+    if (it != known.end()) return it->second;
+    bool ok = false;
+    uint32_t *d_out = nullptr, h[2] = {0, 0};
+    if (hipMalloc(&d_out, 8) == hipSuccess) {
+        hipLaunchKernelGGL(lh_jump_probe_kernel, dim3(1), dim3(64), 0, nullptr, d_out);
+        ok = hipGetLastError() == hipSuccess && hipMemcpy(h, d_out, 8, hipMemcpyDeviceToHost) == hipSuccess &&
+             h[1] <= 0xFFFFFFFFu - 256u * 132u;
+        (void)hipFree(d_out);
+    }
+    known[device] = ok;
+    return ok;
 }
 
 hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {

@@ -75,6 +75,8 @@ struct JumpApplyArgs {
     long long plan_stride;
     int n_in, n_out, bytes, sub, nch, stripes;
     int per_stripe, wps;          // wps: workgroups per stripe (per_stripe 1) = ceil(nch / 64)
+    int dw;                       // bytes per lane per sub-block / 4: 1 (nch = ceil(sub / 4)) or
+                                  // 2 (nch = ceil(sub / 8), the two-dword table, sub >= 8)
 };
 
 struct XorArgs {
@@ -178,6 +180,8 @@ void note_launch(const char *kernel);
 hipError_t launch_writeback(const WritebackArgs &a, hipStream_t st);
 hipError_t launch_apply_generic(const ApplyArgs &a, int W, hipStream_t st);
 hipError_t launch_apply_jump(const JumpApplyArgs &a, hipStream_t st);
+// lh_inv_gtab2 lies within one 4 GiB page on `device` (probed once; dw 2 only then)
+bool jump_table2_usable(int device);
 hipError_t launch_frame(const FrameArgs &a, hipStream_t st);
 hipError_t launch_xor_reduce(const XorArgs &a, hipStream_t st);
 hipError_t launch_scatter(const ScatterArgs &a, hipStream_t st);

@@ -58,6 +58,19 @@ def test_specialisation_policy():
     assert longhair_amd.batch_path(128, 32, 1000) == "generic"
 
 
+def test_lds_staging_policy():
+    """jit.cpp jit_config_for: the register networks stage their columns by LDS-DMA for 8-byte
+    lanes, whole stripes per wave and 16-byte-multiple blocks, unless a stripe's partial last
+    lane would open a 16-lane DPP row (its stores funnel the previous lane's word)."""
+    import longhair_amd
+    assert longhair_amd.lds_staged(29, 4, 1296)        # nch 21, spw 3: last lanes 20, 41, 62
+    assert longhair_amd.lds_staged(64, 4, 4096)        # nch 64: the last lane is whole
+    assert not longhair_amd.lds_staged(29, 4, 1304)    # 1304 % 16 = 8: a chunk would span blocks
+    assert not longhair_amd.lds_staged(29, 4, 1040)    # nch 17, spw 3: lane 16 is a last lane
+    assert not longhair_amd.lds_staged(29, 8, 1296)    # m = 8: 4-byte lanes
+    assert not longhair_amd.lds_staged(100, 12, 800)   # no register network
+
+
 def test_no_device_gpu_policy_fails_loudly():
     """Without a GPU: under the GPU dispatch policy every drop-in call fails with -2 and
     writes nothing; batch calls always need a device (test_launch_trace_empty_without_gpu)."""
@@ -222,11 +235,13 @@ def test_inv_jump_table_is_generated():
     spec.loader.exec_module(gen)
     committed = open(os.path.join(REPO, "longhair_amd", "csrc", "inv_jump.inc")).read()
     assert committed == gen.render()
-    # two tables (in-asm indexed for 8 outputs; once per code object) of 256 bodies of
-    # 8 v_bitop3_b32 + a return: the fixed 68-byte stride the jump assumes
-    assert committed.count("v_bitop3_b32") == 2 * 256 * 8
-    assert committed.count("s_setpc_b64 s[94:95]") == 2 * 256
-    # every call statement (1..8 outputs) turns GPR indexing on once and off once, and
-    # restores M0 (no path leaves the statement with indexing on)
-    assert committed.count("lh_inv_gtab:") == 1 and committed.count("s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)") == 8
-    assert committed.count("s_set_gpr_idx_off") == 8 + 1 and committed.count("s_mov_b32 m0, s97") == 8 + 1
+    # two one-dword tables (in-asm indexed for 8 outputs; once per code object) of 256 bodies
+    # of 8 v_bitop3_b32 + a return (the fixed 68-byte stride the jump assumes) and the
+    # two-dword table of 256 bodies of 16 (132 bytes)
+    assert committed.count("v_bitop3_b32") == 2 * 256 * 8 + 256 * 16
+    assert committed.count("s_setpc_b64 s[94:95]") == 3 * 256
+    # every call statement (1..8 outputs, two-dword 1..4) turns GPR indexing on once and off
+    # once, and restores M0 (no path leaves the statement with indexing on)
+    assert committed.count("lh_inv_gtab:") == 1 and committed.count("lh_inv_gtab2:") == 1
+    assert committed.count("s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)") == 8 + 4
+    assert committed.count("s_set_gpr_idx_off") == 8 + 4 + 1 and committed.count("s_mov_b32 m0, s97") == 8 + 4 + 1

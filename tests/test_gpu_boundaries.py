@@ -29,6 +29,11 @@ GENERIC_S8 = ["lh_plan_small_kernel<8>", "lh_apply_jump_kernel"]
 # workgroup: sub = 256 t + 1..3): apply into a workspace, then scatter
 OLD_CF = ["lh_plan_kernel(closed form)", "lh_apply_generic_kernel", "lh_scatter_kernel"]
 JUMP = ["lh_apply_jump_kernel"]
+JUMP2 = ["lh_apply_jump2_kernel"]  # two-dword lanes (codec.cpp jump_layout)
+GEN = {"LONGHAIR_AMD_PATH": "generic"}
+PS4_JUMP = ["lh_plan_small_kernel<4>", "lh_apply_jump_kernel"]
+PS4_JUMP2 = ["lh_plan_small_kernel<4>", "lh_apply_jump2_kernel"]
+PS8_JUMP = ["lh_plan_small_kernel<8>", "lh_apply_jump_kernel"]
 WIDE16 = ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_gt_kernel"]
 WIDE64 = WIDE16  # (one phase-B kernel for every e_max since round 3)
 
@@ -72,6 +77,17 @@ BOUNDARIES = [
     # generic kernels below dword lanes (sub < 4) <-> the jump apply (sub = 4)
     ("generic-sub3", 30, 13, 24, 40, {}, ["lh_apply_generic_kernel"], OLD_CF),
     ("generic-sub4", 30, 13, 32, 40, {}, JUMP, GENERIC_CF),
+    # two-dword lanes (codec.cpp jump_layout): at most 4 outputs, sub >= 8 (encode) and, in
+    # place, sub >= 512 with the last two-dword lane in its neighbour's workgroup
+    ("jump2-n4-sub7", 40, 4, 56, 64, GEN, JUMP, PS4_JUMP),
+    ("jump2-n4-sub8", 40, 4, 64, 64, GEN, JUMP2, PS4_JUMP),
+    ("jump2-n5-sub8", 40, 5, 64, 64, GEN, JUMP, PS8_JUMP),
+    ("jump2-n4-sub504", 40, 4, 4032, 8, GEN, JUMP2, PS4_JUMP),
+    ("jump2-n4-sub520", 40, 4, 4160, 8, GEN, JUMP2, PS4_JUMP2),
+    ("jump2-n5-sub520", 40, 5, 4160, 8, GEN, JUMP, PS8_JUMP),
+    ("jump2-n4-sub516", 40, 4, 4128, 8, GEN, JUMP2, PS4_JUMP),  # (sub % 8 = 4, nch 65: lone)
+    # the in-asm one-dword table (and the address-probe fallback) for every jump apply
+    ("jump2-n4-fallback", 40, 4, 4160, 8, dict(GEN, LONGHAIR_AMD_INV_FALLBACK="1"), JUMP, PS4_JUMP),
     # phase B: V rows staged 16 at a time for e_max <= 32, all at once above
     ("jump-emax32", 40, 32, 2048, 8, {}, ["lh_jit_encode_win"], WIDE16),
     ("jump-emax33", 40, 33, 2048, 8, {}, ["lh_jit_encode_win"], WIDE64),
@@ -209,7 +225,7 @@ def test_reference_main_sweep(lh, oracle, monkeypatch):
             n += 1
     assert n > 2500
     assert {"lh_jit_encode", "lh_jit_decode_fused", "lh_jit_decode", "lh_apply_generic_kernel", "lh_apply_jump_kernel",
-            "lh_xor_reduce_kernel"} <= seen, sorted(seen)
+            "lh_apply_jump2_kernel", "lh_xor_reduce_kernel"} <= seen, sorted(seen)
 
 
 def _jit_sample(n=24, seed=2024):
@@ -371,7 +387,7 @@ def test_jit_compiles_in_background(lh, oracle, monkeypatch, tmp_path):
     rec = lh.encode_batch(x, m)
     torch.cuda.synchronize()
     first = time.perf_counter() - t0
-    assert lh.last_launch() == ["lh_apply_jump_kernel"], lh.last_launch()
+    assert lh.last_launch() == ["lh_apply_jump2_kernel"], lh.last_launch()
     assert first < 1.0, f"first call took {first:.2f} s"
     assert np.array_equal(rec.cpu().numpy(), expect)
     # another shape meanwhile: its (cached) module is not held up by the compilation
@@ -386,7 +402,7 @@ def test_jit_compiles_in_background(lh, oracle, monkeypatch, tmp_path):
         trace = lh.last_launch()
         if trace == ["lh_jit_encode"]:
             break
-        assert trace == ["lh_apply_jump_kernel"], trace
+        assert trace == ["lh_apply_jump2_kernel"], trace
         assert time.time() < deadline, "the background compilation did not finish in 100 s"
         time.sleep(0.25)
     assert np.array_equal(rec.cpu().numpy(), expect)

@@ -662,8 +662,14 @@ def test_planner_closed_form_matches_elimination(lh, oracle, monkeypatch, k, m, 
 # (tools/precompile.py KNOB_JOBS compiles the variant modules at build time).
 KNOB_VARIANTS = [
     ("nofused", {"LONGHAIR_AMD_NO_FUSED_PLAN": "1"}, ["lh_plan_small_kernel<4>", "lh_jit_decode"]),
-    ("defines-pf2-nt0-noxcd", {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=2,LH_NT=0,LH_XCD=0"}, ["lh_jit_decode_fused"]),
-    ("defines-recfirst0-pfdec2", {"LONGHAIR_AMD_JIT_DEFINES": "LH_REC_FIRST=0,LH_PF_DEC=2"}, ["lh_jit_decode_fused"]),
+    # the register-ring forms (LH_LDS=0: every shape the LDS staging does not take, jit.cpp)
+    ("defines-lds0-pf2-nt0-noxcd", {"LONGHAIR_AMD_JIT_DEFINES": "LH_LDS=0,LH_PF=2,LH_NT=0,LH_XCD=0"},
+     ["lh_jit_decode_fused"]),
+    ("defines-lds0-recfirst0-pfdec2", {"LONGHAIR_AMD_JIT_DEFINES": "LH_LDS=0,LH_REC_FIRST=0,LH_PF_DEC=2"},
+     ["lh_jit_decode_fused"]),
+    # the LDS-staged forms' other ring depth, cache policy, column order and direct stores
+    ("defines-ld2-nt0-ldsrecfirst-direct", {"LONGHAIR_AMD_JIT_DEFINES": "LH_LD=2,LH_NT=0,LH_LDS_NT_DEC=0,LH_LDS_REC_FIRST=1,LH_LDS_FLAT_ST=0"},
+     ["lh_jit_decode_fused"]),
 ]
 
 

@@ -22,8 +22,9 @@ TESTS = [(29, 2, 1296), (29, 3, 1296), (29, 8, 1296), (4, 2, 16), (10, 6, 8), (1
 PTR_SHAPES = [(29, 4, 1296), (29, 8, 1296), (10, 6, 24), (64, 5, 4096), (64, 3, 4096), (40, 20, 4096),
               (128, 32, 8192), (200, 56, 65536)]
 # Modules of the knob variants the GPU tests run (tests/test_gpu_parity.py KNOB_VARIANTS).
-KNOB_JOBS = [((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_PF=2,LH_NT=0,LH_XCD=0"}),
-             ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_REC_FIRST=0,LH_PF_DEC=2"})]
+KNOB_JOBS = [((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_LDS=0,LH_PF=2,LH_NT=0,LH_XCD=0"}),
+             ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_LDS=0,LH_REC_FIRST=0,LH_PF_DEC=2"}),
+             ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_LD=2,LH_NT=0,LH_LDS_NT_DEC=0,LH_LDS_REC_FIRST=1,LH_LDS_FLAT_ST=0"})]
 
 
 def boundary_jobs():
@@ -55,16 +56,13 @@ def main():
                 print("pruned", f)
         return
     if sys.argv[1:] == ["--all"]:
-        # One child process per shape, largest first: hiprtc is single-threaded and the
-        # k200/m56 module alone takes minutes, so the rest compile beside it.
-        jobs = max(1, min(8, (os.cpu_count() or 2) - 1))
+        # One child process per (shape, part), largest network first (k * m): hiprtc is
+        # single-threaded and the big modules take minutes, so the rest compile beside them
+        # and none starts last.
+        jobs = max(1, min(8, os.cpu_count() or 2))
         cmd = [sys.executable, os.path.abspath(__file__)]
         with ThreadPoolExecutor(jobs) as pool:
-            # ~570, 130, 190, 110 s alone: start first (the GPU tests run k200/m56 too)
-            slow = [(200, 56, 65536), (128, 32, 8192), (64, 3, 4096), (64, 5, 4096)]
-            # the large-m shapes' encode and decode modules compile in separate processes
-            jobs_list = [(s, part) for s in slow[:2] for part in ("dec", "enc")]
-            jobs_list += [(s, None) for s in slow[2:] + [s for s in DEFAULT + TESTS if s not in slow]]
+            jobs_list = [(s, None) for s in dict.fromkeys(DEFAULT + TESTS)]
             ptr_jobs = [(s, (part, {"LONGHAIR_AMD_PRECOMPILE_PTR": "1"})) for s in PTR_SHAPES for part in ("dec", "enc")]
             jobs_list += [(s, (None, env)) for s, env in KNOB_JOBS]
             jobs_list = ptr_jobs[-4:] + jobs_list + ptr_jobs[:-4]
@@ -79,6 +77,14 @@ def main():
             have |= set(sweep_shapes(tb))
             # the specialised-kernel parity sample (test_specialised_sample), slowest first
             jobs_list += [(sh, None) for sh in sorted(tb.JIT_SAMPLE, key=lambda s: -s[0] * s[1]) if sh not in have]
+            # the encode and decode modules of a shape in separate processes
+            split = []
+            for sh, part in jobs_list:
+                p, env = part if isinstance(part, tuple) else (part, None)
+                for q in ((p,) if p else ("dec", "enc")):
+                    split.append((sh, (q, env) if env is not None else q))
+            jobs_list = split
+            jobs_list.sort(key=lambda j: -j[0][0] * j[0][1])  # (stable: parts keep their order)
 
             def run(job):
                 shape, part = job

@@ -555,76 +555,6 @@ __global__ void __launch_bounds__(256) w4d(const uint8_t *__restrict__ in, uint8
       __builtin_nontemporal_store(acc[r][y] ^ ((uint32_t)r * 0x01010101u), (uint32_t *)(o + r * BYTES + y * SUB));
 }
 
-// w4l: the same lanes, each column landed in an LDS ring by 2 LDS-DMA instructions (81 x 16 B:
-// lanes 0..63, then 0..16) -- one contiguous 1296-B read per column -- and read back per lane:
-// even sub-blocks (4-byte aligned) one ds_read_b32, odd ones two dwords + v_alignbyte.
-template <int D>
-__global__ void __launch_bounds__(256) w4l(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, int stripes) {
-  __shared__ __attribute__((aligned(16))) uint8_t ring[4][D][1536];
-  const long long wave = (xcd_block() * 256 + threadIdx.x) >> 6;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (wave >= stripes) return;
-  const bool act = lane < 41;
-  const int p = lane >= 40 ? SUB - 4 : 4 * lane;
-  const uint8_t *src0 = in + wave * STRIDE + lane * 16;
-  const uint8_t *src1 = in + wave * STRIDE + (lane < 17 ? 64 + lane : 80) * 16;
-  auto issue = [&](int x, int sl) {
-    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src0 + x * BYTES),
-                                     (__attribute__((address_space(3))) void *)&ring[w][sl][0], 16, 0, 2);
-    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src1 + x * BYTES),
-                                     (__attribute__((address_space(3))) void *)&ring[w][sl][1024], 16, 0, 2);
-  };
-#pragma unroll
-  for (int q = 0; q < D; ++q) issue(q, q);
-  uint32_t acc[M][8];
-#pragma unroll
-  for (int r = 0; r < M; ++r)
-#pragma unroll
-    for (int y = 0; y < 8; ++y) acc[r][y] = 0;
-#pragma unroll
-  for (int x = 0; x < K; ++x) {
-    const int left = std::min(D - 1, K - 1 - x);  // columns issued after x (2 DMA each)
-    switch (left) {  // vmcnt(2 * left) (a constant per unrolled column)
-#define W4L_WAIT(L) case L: __builtin_amdgcn_s_waitcnt(((2 * L) & 15) | (((2 * L) >> 4) << 14) | (7 << 4) | (15 << 8)); break;
-      W4L_WAIT(0) W4L_WAIT(1) W4L_WAIT(2) W4L_WAIT(3) W4L_WAIT(4) W4L_WAIT(5) W4L_WAIT(6) W4L_WAIT(7)
-      W4L_WAIT(8) W4L_WAIT(9) W4L_WAIT(10) W4L_WAIT(11)
-#undef W4L_WAIT
-    }
-    asm volatile("" ::: "memory");
-    const uint8_t *t = ring[w][x % D];
-    uint32_t d[8];
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const int o = b * SUB + p;  // b odd: 2 mod 4
-      if (b % 2 == 0) {
-        d[b] = *(const uint32_t *)(t + o);
-      } else {
-        const uint32_t *q = (const uint32_t *)(t + o - 2);
-        d[b] = __builtin_amdgcn_alignbyte(q[1], q[0], 2);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < M; ++r)
-#pragma unroll
-      for (int y = 0; y < 8; ++y) acc[r][y] ^= d[(y + r + x) & 7];
-#pragma unroll
-    for (int r = 0; r < M; ++r)
-#pragma unroll
-      for (int y = 0; y < 8; ++y) asm volatile("" : "+v"(acc[r][y]));
-    if (x + D < K) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      issue(x + D, x % D);
-    }
-  }
-  if (!act) return;
-  uint8_t *o = out + wave * STRIDE + OUT_OFF + p;
-#pragma unroll
-  for (int r = 0; r < M; ++r)
-#pragma unroll
-    for (int y = 0; y < 8; ++y)
-      __builtin_nontemporal_store(acc[r][y] ^ ((uint32_t)r * 0x01010101u), (uint32_t *)(o + r * BYTES + y * SUB));
-}
-
 
 // geop: geo S=1 G=37 on the stripe layout with the stores' cache-policy bits AUX (gfx950
 // buffer instructions: bit 0 sc0, bit 1 nt, bit 4 sc1) and the loads' LAUX.
@@ -869,7 +799,7 @@ int main(int argc, char **argv) {
       check(nm);                                                                                          \
       rep(nm, timeit([&] { KER<P><<<g1, 256>>>(din, dout, (int)STRIPES); }));                             \
     }
-    W4(w4d, 3) W4(w4d, 6) W4(w4d, 10) W4(w4l, 4) W4(w4l, 8) W4(w4l, 12)
+    W4(w4d, 3) W4(w4d, 6) W4(w4d, 10)
   }
 
   if (want(argc, argv, "pol")) {
