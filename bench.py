@@ -48,18 +48,18 @@ CONFIGS = {
     "k200m56": (200, 56, 65536, 64, "random"),   # BASELINE configs[4] (device-resident part)
 }
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
-# Calibrated ceilings of this chip (tools/ubench_floor.hip, profiles/r4a_ubench_floor.txt; the
-# same run reproduces the MI355X_MICROARCH.md float4 copy at 6.55 TB/s against the guide's
-# 6.29, so the floors below are tuned): one-shot grids (one chunk set per thread) beat every
-# persistent grid, non-temporal loads and stores beat default ones.
-HBM_CEILING_GBS = 7110.6   # read-only stream, dwordx4, non-temporal, one-shot grid
-HBM_CEILING_SRC = "profiles/r4a_ubench_floor.txt (read os U=8 nt=1: 2.46 GB read-only, dwordx4 non-temporal, one-shot grid)"
-# The encode's and decode's own byte mix (2.46 GB read + 0.34 GB written) as a flat stream with
-# the stores interleaved (each wave reads 29 KiB then writes 4 KiB, non-temporal): 0.4634 ms =
-# 6.05 TB/s of total traffic, 5.32 TB/s of input.  What a kernel moving these bytes can reach.
-MIX_CEILING_GBS = 6048.4
-FLAT_FLOOR_MS = 0.4634
-FLAT_FLOOR_SRC = "profiles/r4a_ubench_floor.txt (mix one-shot G=29 ntl=1 nts=1: 29:4 read:write flat stream)"
+# Calibrated ceilings of this chip (round 5: tools/ubench_r5.hip, profiles/r5b_ubench_floor.txt,
+# one box; the same run reproduces the MI355X_MICROARCH.md float4 copy at 6.60 TB/s against the
+# guide's 6.29): one-shot grids (one chunk set per thread), non-temporal loads and stores.
+HBM_CEILING_GBS = 7131.3   # read-only stream, dwordx4, non-temporal, one-shot grid
+HBM_CEILING_SRC = "profiles/r5b_ubench_floor.txt (read dwordx4 one-shot nt U=8: 2.46 GB read-only)"
+# The encode's and decode's own byte mix (2.463 GB read + 0.340 GB written) as a flat stream,
+# the fastest of the round-5 shapes (8 waves per block, 512-byte store segments): 0.4592 ms =
+# 6.10 TB/s of total traffic, 5.36 TB/s of input.  The fastest 29:4 stream built, not a proven
+# bound (its writes cost 2.9 TB/s against the copy's 6.1).
+MIX_CEILING_GBS = 6104.4
+FLAT_FLOOR_MS = 0.4592
+FLAT_FLOOR_SRC = "profiles/r5b_ubench_floor.txt (mix LB=8 SEG=512 BS=256: 29:4 read:write flat stream)"
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD
 # (SIMD-32, MI355X_MICROARCH.md 'Wave scheduling'), 2.4 GHz -> wave-instructions / s.
 VALU_PEAK_GINSTR = 256 * 4 * 2.4e9 / 2 / 1e9
