@@ -204,13 +204,9 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
         for (int r = r0; r < r1; ++r)
             for (int y = 0; y < 8; ++y) os << "  unsigned int a" << (r - r0) << "_" << y << " = 0;\n";
     }
-    // Decode: a recovery row the stripe did not receive (slot 0xFF) is never stored, so its
-    // XORs are skipped (LH_ROWSKIP, a wave-uniform branch per row and column: with random e
-    // about half of k200/m56's rows, and phase A is VALU-bound there).
-    if (elim)
-        for (int r = r0; r < r1; ++r)
-            os << "  const bool u" << (r - r0) << " = !LH_ROWSKIP || __builtin_amdgcn_readlane((int)slv[" << (k + r) / 64
-               << "], " << (k + r) % 64 << ") != 0xFF;\n";
+    // (Skipping the XORs of a recovery row the stripe did not receive, a wave-uniform branch
+    // per row and column, measured slower: k200/m56 random-e decode 0.629 against 0.591 ms,
+    // profiles/r5o_bench_k200m56.json / r5o_rs0_bench_k200m56.json.)
     auto dcol = [&](int x) {  // uniform base of column x for the DMA (stripe + chunk, or zero page)
         std::ostringstream e;
         if (c.ptr && elim) e << "(lh_pp(cpl, " << x << ") + coff)";
@@ -269,7 +265,6 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
         }
         for (int r = r0; r < r1; ++r) {
             const uint64_t bm = bitmatrix(G[(size_t)r * k + x]);
-            if (elim) os << "    if (u" << (r - r0) << ") {\n";
             for (int y = 0; y < 8; ++y) {
                 const int s = (int)((bm >> (8 * y)) & 0xFF), lo = s & 15, hi = s >> 4;
                 if (!lo && !hi) continue;
@@ -280,7 +275,6 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
                 else
                     os << "    " << a << " ^= " << (lo ? "t0_" + std::to_string(lo) : "t1_" + std::to_string(hi)) << ";\n";
             }
-            if (elim) os << "    }\n";
         }
         os << "    LH_PIN" << (r1 - r0) << ";\n";
         if (elim) os << "    }\n";
@@ -387,7 +381,6 @@ static std::string win_source_for(const JitConfig &c) {
     os << "// longhair_amd windowed " << (c.win == 2 ? "decode" : "encode") << ", k=" << c.k << " m=" << c.m
        << " bytes=" << c.bytes << "\n"
        << "#ifndef LH_NT\n#define LH_NT 1\n#endif\n"
-       << "#ifndef LH_ROWSKIP\n#define LH_ROWSKIP 1\n#endif\n"
        << "__device__ __forceinline__ unsigned int lh_ld(const unsigned char *p) {\n"
        << "#if LH_NT\n  return __builtin_nontemporal_load((const unsigned int *)p);\n#else\n"
        << "  unsigned int w; __builtin_memcpy(&w, p, 4); return w;\n#endif\n}\n"
