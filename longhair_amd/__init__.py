@@ -344,7 +344,7 @@ def kernel_names(k, m, block_bytes):
                                             else ["lh_apply_jump2_kernel" if two_dec else "lh_apply_jump_kernel"]),
            "jit": ["lh_plan_small_kernel" if min(k, m) <= 8 else "lh_plan_kernel", "lh_jit_decode"],
            "jit-fused": ["lh_jit_decode_fused"],
-           "jit-wide": ["lh_plan_kernel", "lh_jit_decode_wide", "lh_inverse_gt_kernel"],
+           "jit-wide": ["lh_plan_kernel", "lh_jit_decode_wide", "lh_order_kernel", "lh_inverse_gt_kernel"],
            }[batch_path(k, m, block_bytes, True)]
     if m == 1 or k == 1:
         enc, dec = ["lh_xor_reduce_kernel"], ["lh_plan_kernel", "lh_xor_reduce_kernel"]

@@ -459,11 +459,18 @@ static int encode_batch(int k, int m, int bytes, int stripes, const uint8_t *d_d
 // The per-stripe erasure planner (lh_plan_kernel / lh_plan_small_kernel) into the stream's
 // plan workspace (reserved with `work_bytes` of generic-path workspace beside it).
 // LONGHAIR_AMD_PLAN_GJ (knob): Gauss-Jordan even where the closed form applies.
+// The plan workspace holds the stripes' plans, then (16-byte aligned) one int per stripe:
+// phase B's launch order (InverseArgs::order).
+static size_t plan_order_offset(int stripes, long long plan_stride) {
+    return ((size_t)stripes * (size_t)plan_stride + 15) & ~(size_t)15;
+}
+
 static int run_planner(Device *d, hipStream_t st, int k, int m, int e_max, int stripes, uint8_t *d_rows,
                        int8_t *d_status, size_t work_bytes, bool want_w, Workspace **out) {
     const long long plan_stride = PlanView::bytes(k, m, e_max);
     Workspace *w = nullptr;
-    if (int rc = workspace(d, st, (size_t)stripes * plan_stride, work_bytes, &w)) return rc;
+    if (int rc = workspace(d, st, plan_order_offset(stripes, plan_stride) + (size_t)stripes * sizeof(int), work_bytes, &w))
+        return rc;
     const uint8_t *G = nullptr, *points = nullptr;
     if (int rc = device_generator(d, k, m, &G, &points, st)) return rc;
     PlanArgs pa{};
@@ -610,6 +617,7 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
             ia.e_max = e_max;
             ia.bytes = bytes;
             ia.stripes = stripes;
+            ia.order = (int *)(w->plan.ptr + plan_order_offset(stripes, plan_stride));
             LH_HIP(launch_inverse(ia, st));
         }
         return kOk;
@@ -854,6 +862,7 @@ static int decode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
             ia.e_max = e_max;
             ia.bytes = bytes;
             ia.stripes = stripes;
+            ia.order = (int *)(w->plan.ptr + plan_order_offset(stripes, plan_stride));
             LH_HIP(launch_inverse(ia, st));
             return kOk;
         }
@@ -1481,7 +1490,9 @@ LH_API int cauchy_256_batch_prepare_stream(int k, int m, int block_bytes, int ma
             const bool generic = !lh::jit_config_for(k, m, block_bytes, true, &cfg);
             lh::Workspace *w = nullptr;
             hipStream_t st = (hipStream_t)stream;
-            if (int rc = lh::workspace(d, st, (size_t)max_stripes * lh::PlanView::bytes(k, m, e_max),
+            if (int rc = lh::workspace(d, st,
+                                       lh::plan_order_offset(max_stripes, lh::PlanView::bytes(k, m, e_max)) +
+                                           (size_t)max_stripes * sizeof(int),
                                        generic ? (size_t)max_stripes * e_max * block_bytes : 0, &w))
                 return rc;
             const uint8_t *G = nullptr, *z = nullptr;

@@ -800,7 +800,8 @@ struct lh_pb_ctx {
     }
 };
 
-// The workgroup's stripe and chunks: a.chunks_per_wg consecutive 2 KiB chunks of one stripe.
+// The workgroup's stripe and chunks: a.chunks_per_wg consecutive 2 KiB chunks of one stripe,
+// the stripes taken in a.order (largest e first) when given.
 struct lh_pb_span {
     long long stripe;
     int c0, nch;
@@ -808,6 +809,7 @@ struct lh_pb_span {
         const int cps = a.bytes >> 11, cpw = a.chunks_per_wg > 0 ? a.chunks_per_wg : 1;
         const int wps = (cps + cpw - 1) / cpw;  // workgroups per stripe
         stripe = blockIdx.x / wps;
+        if (a.order && stripe < a.stripes) stripe = a.order[stripe];
         c0 = (int)(blockIdx.x % wps) * cpw;
         nch = cps - c0 < cpw ? cps - c0 : cpw;
     }
@@ -993,6 +995,30 @@ __global__ void __launch_bounds__(1024) lh_inverse_gt_kernel(lh::InverseArgs a) 
         return;
     }
     lh_inverse_gt_body(a, lvA, lvB, tlo, thi);
+}
+
+// Phase B's launch order: a stripe's phase-B work grows with e^2 (e outputs, each a sum over
+// e rows), so with random erasures (k200/m56: e uniform in [1, 56]) a few heavy stripes set
+// the kernel's tail.  One workgroup counting-sorts the stripes by e, largest first, and
+// lh_pb_span maps workgroup b to stripe order[b / wps].
+__global__ void __launch_bounds__(1024) lh_order_kernel(const uint8_t *__restrict__ plan, long long plan_stride,
+                                                        int stripes, int *__restrict__ order) {
+    __shared__ int cnt[256];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) cnt[i] = 0;
+    __syncthreads();
+    for (int s = threadIdx.x; s < stripes; s += blockDim.x) atomicAdd(&cnt[plan[(long long)s * plan_stride]], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {  // start of each e's run, descending e
+        int run = 0;
+        for (int e = 255; e >= 0; --e) {
+            const int c = cnt[e];
+            cnt[e] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    for (int s = threadIdx.x; s < stripes; s += blockDim.x)
+        order[atomicAdd(&cnt[plan[(long long)s * plan_stride]], 1)] = s;
 }
 
 // ------------------------------------------------------------ generic apply, jump table
@@ -1507,10 +1533,25 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     // them, so the pipeline's start (plan, jump targets, first tile's DMA) is paid once per
     // pair (profiles/r4k_tune_*_inv_chunks.txt: k200/m56 decode 0.665 -> 0.617 ms with 2, 0.635
     // with 4; k128/m32 3.634 ms with 1, 2 or 4).
+#ifndef LH_PB_CPW
+#define LH_PB_CPW 2  // (an A/B build may set another, make HIP_EXTRA=-DLH_PB_CPW=n)
+#endif
     const int cps = a.bytes / 2048;
-    const int cpw = cps < 2 ? cps : 2;
+    const int cpw = cps < LH_PB_CPW ? cps : LH_PB_CPW;
     g.chunks_per_wg = cpw;
     const long long wgs = (long long)a.stripes * ((cps + cpw - 1) / cpw);
+#ifndef LH_PB_ORDER
+#define LH_PB_ORDER 1  // (0: an A/B build of the launch order, make HIP_EXTRA=-DLH_PB_ORDER=0)
+#endif
+    if (!LH_PB_ORDER) g.order = nullptr;
+    if (g.order) {
+        if (a.stripes > 1) {
+            hipLaunchKernelGGL(lh_order_kernel, dim3(1), dim3(1024), 0, st, a.plan, a.plan_stride, a.stripes, g.order);
+            note_launch("lh_order_kernel");
+        } else {
+            g.order = nullptr;
+        }
+    }
     hipLaunchKernelGGL(lh_inverse_gt_kernel, dim3((unsigned)wgs), dim3(64u * (unsigned)((a.e_max + 7) / 8)), 0, st, g);
     note_launch(g.jump_fallback ? "lh_inverse_gt_kernel(fallback)" : "lh_inverse_gt_kernel");
     return hipGetLastError();

@@ -139,6 +139,8 @@ struct InverseArgs {
     int chunks_per_wg;            // lh_inverse_gt_kernel: consecutive 2 KiB chunks per workgroup (>= 1)
     uint8_t *const *ptrs;         // pointer-table batches: slot j of stripe s at ptrs[s*k + j]
                                   // (blocks and stride unused), else NULL
+    int *order;                   // scratch of `stripes` ints: the stripes by e, largest first
+                                  // (written by launch_inverse; NULL: launch order = stripe order)
 };
 
 hipError_t launch_inverse(const InverseArgs &a, hipStream_t st);

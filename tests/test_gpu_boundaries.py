@@ -34,7 +34,8 @@ GEN = {"LONGHAIR_AMD_PATH": "generic"}
 PS4_JUMP = ["lh_plan_small_kernel<4>", "lh_apply_jump_kernel"]
 PS4_JUMP2 = ["lh_plan_small_kernel<4>", "lh_apply_jump2_kernel"]
 PS8_JUMP = ["lh_plan_small_kernel<8>", "lh_apply_jump_kernel"]
-WIDE16 = ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_gt_kernel"]
+# (lh_order_kernel: phase B's stripes by e, largest first; kernels.hip launch_inverse)
+WIDE16 = ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_order_kernel", "lh_inverse_gt_kernel"]
 WIDE64 = WIDE16  # (one phase-B kernel for every e_max since round 3)
 
 # (id, k, m, bytes, stripes, env, encode kernels, decode kernels)
@@ -188,7 +189,7 @@ def test_phase_b_variant(lh, oracle, monkeypatch, env, m, kernel):
         monkeypatch.setenv(key, v)
     k, nbytes = 40, 2048
     enc, dec = roundtrip(lh, oracle, k, m, nbytes, 8, seed=m * 31)
-    assert dec == ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", kernel], dec
+    assert dec == ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_order_kernel", kernel], dec
 
 
 def test_phase_b_chunks_per_workgroup(lh, oracle):
@@ -196,7 +197,7 @@ def test_phase_b_chunks_per_workgroup(lh, oracle):
     carried across them): 6144-byte blocks = 3 chunks, so the second workgroup of a stripe has
     a one-chunk remainder; against the oracle."""
     enc, dec = roundtrip(lh, oracle, 40, 20, 6144, 7, seed=14)
-    assert dec == ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_inverse_gt_kernel"], dec
+    assert dec == ["lh_plan_kernel(closed form)", "lh_jit_decode_wide", "lh_order_kernel", "lh_inverse_gt_kernel"], dec
 
 
 def _sweep_ms(k):
