@@ -340,11 +340,12 @@ def kernel_names(k, m, block_bytes):
     jump_enc = "lh_apply_generic_kernel" if small else ("lh_apply_jump2_kernel" if two_enc else "lh_apply_jump_kernel")
     enc = {"generic": [jump_enc], "jit": ["lh_jit_encode"],
            "jit-win": ["lh_jit_encode_win"]}[batch_path(k, m, block_bytes)]
+    order = ["lh_order_kernel"] if min(k, m) > 8 else []  # kernels.hip order_stripes
     dec = {"generic": ["lh_plan_kernel"] + (["lh_apply_generic_kernel", "lh_scatter_kernel"] if old_dec
-                                            else ["lh_apply_jump2_kernel" if two_dec else "lh_apply_jump_kernel"]),
+                                            else order + ["lh_apply_jump2_kernel" if two_dec else "lh_apply_jump_kernel"]),
            "jit": ["lh_plan_small_kernel" if min(k, m) <= 8 else "lh_plan_kernel", "lh_jit_decode"],
            "jit-fused": ["lh_jit_decode_fused"],
-           "jit-wide": ["lh_plan_kernel", "lh_jit_decode_wide", "lh_order_kernel", "lh_inverse_gt_kernel"],
+           "jit-wide": ["lh_plan_kernel", "lh_jit_decode_wide"] + order + ["lh_inverse_gt_kernel"],
            }[batch_path(k, m, block_bytes, True)]
     if m == 1 or k == 1:
         enc, dec = ["lh_xor_reduce_kernel"], ["lh_plan_kernel", "lh_xor_reduce_kernel"]

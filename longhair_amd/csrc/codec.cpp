@@ -638,6 +638,7 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         a.sub = sub;
         a.stripes = stripes;
         a.per_stripe = 1;
+        a.order = (int *)(w->plan.ptr + plan_order_offset(stripes, plan_stride));  // by e, largest first
         jump_layout(d, a, true);
         LH_HIP(launch_apply_jump(a, st));
         return kOk;

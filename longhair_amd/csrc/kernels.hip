@@ -1109,6 +1109,7 @@ __device__ __forceinline__ void lh_apply_jump_body(const lh::JumpApplyArgs &a, u
     if (a.per_stripe) {
         l.stripe = blockIdx.x / a.wps;
         if (l.stripe >= a.stripes) return;  // workgroup-uniform
+        if (a.order) l.stripe = a.order[l.stripe];
         c = (int)(blockIdx.x % a.wps) * 64 + lane;
         l.active = c < a.nch;
         c = l.active ? c : a.nch - 1;
@@ -1291,6 +1292,7 @@ __device__ __forceinline__ void lh_apply_jump2_body(const lh::JumpApplyArgs &a, 
     if (a.per_stripe) {
         l.stripe = blockIdx.x / a.wps;
         if (l.stripe >= a.stripes) return;  // workgroup-uniform
+        if (a.order) l.stripe = a.order[l.stripe];
         c = (int)(blockIdx.x % a.wps) * 64 + lane;
         l.active = c < a.nch;
         c = l.active ? c : a.nch - 1;
@@ -1459,6 +1461,20 @@ __global__ void __launch_bounds__(256) lh_writeback_kernel(lh::WritebackArgs a) 
 // ------------------------------------------------------------------ host launchers
 namespace lh {
 
+// Writes `order` (the stripes by their plan's e, largest first: lh_order_kernel) when there is
+// a scratch, more than one stripe and more than one wave of outputs (e_max > 8: below that a
+// stripe's work varies too little to pay for the sort); false: launch in stripe order.
+#ifndef LH_PB_ORDER
+#define LH_PB_ORDER 1  // (0: an A/B build of the launch order, make HIP_EXTRA=-DLH_PB_ORDER=0)
+#endif
+static bool order_stripes(int *order, const uint8_t *plan, long long plan_stride, int stripes, int e_max,
+                          hipStream_t st) {
+    if (!LH_PB_ORDER || !order || !plan || stripes < 2 || e_max <= 8) return false;
+    hipLaunchKernelGGL(lh_order_kernel, dim3(1), dim3(1024), 0, st, plan, plan_stride, stripes, order);
+    note_launch("lh_order_kernel");
+    return true;
+}
+
 hipError_t launch_apply_generic(const ApplyArgs &a, int W, hipStream_t st) {
     const long long lanes = (long long)a.stripes * a.nch;
     dim3 grid((unsigned)((lanes + 255) / 256), (unsigned)((a.n_out + kGenericTileOut - 1) / kGenericTileOut));
@@ -1482,17 +1498,27 @@ hipError_t launch_apply_jump(const JumpApplyArgs &a, hipStream_t st) {
         const long long wgs = a.per_stripe ? (long long)a.stripes * a.wps : ((long long)a.stripes * a.nch + 63) / 64;
         if (wgs <= 0) return hipSuccess;
         if (wgs > 0x7FFFFFFF) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(lh_apply_jump2_kernel, dim3((unsigned)wgs), dim3(64u * (unsigned)ng), 0, st, a);
+        JumpApplyArgs g = a;
+        if (!order_stripes(g.order, a.plan, a.plan_stride, a.per_stripe ? a.stripes : 0, a.n_out, st)) g.order = nullptr;
+        hipLaunchKernelGGL(lh_apply_jump2_kernel, dim3((unsigned)wgs), dim3(64u * (unsigned)ng), 0, st, g);
         note_launch("lh_apply_jump2_kernel");
         return hipGetLastError();
     }
     if (a.dw != 1) return hipErrorInvalidValue;
-    const int ng = (a.n_out + 7) / 8 < 16 ? (a.n_out + 7) / 8 : 16;
+    // Flat (encode) launches: a power-of-two number of waves per workgroup, further rounds for
+    // the remaining outputs, so whole workgroups fill a CU's 16 wave slots (124 VGPRs: 4 per
+    // SIMD); 7 waves left 2 slots idle.  k200/m56 generic encode 1.20-1.23 -> 1.10-1.11 ms
+    // (profiles/r5v_generic_pow2.txt).  In place: one round, every output's wave present.
+    int ng = (a.n_out + 7) / 8 < 16 ? (a.n_out + 7) / 8 : 16;
+    if (!a.plan)
+        while (ng & (ng - 1)) ng &= ng - 1;
     if (a.plan && a.n_out > 8 * ng) return hipErrorInvalidValue;
     const long long wgs = a.per_stripe ? (long long)a.stripes * a.wps : ((long long)a.stripes * a.nch + 63) / 64;
     if (wgs <= 0) return hipSuccess;
     if (wgs > 0x7FFFFFFF) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(lh_apply_jump_kernel, dim3((unsigned)wgs), dim3(64u * (unsigned)ng), 0, st, a);
+    JumpApplyArgs g = a;
+    if (!order_stripes(g.order, a.plan, a.plan_stride, a.per_stripe ? a.stripes : 0, a.n_out, st)) g.order = nullptr;
+    hipLaunchKernelGGL(lh_apply_jump_kernel, dim3((unsigned)wgs), dim3(64u * (unsigned)ng), 0, st, g);
     note_launch("lh_apply_jump_kernel");
     return hipGetLastError();
 }
@@ -1540,18 +1566,7 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     const int cpw = cps < LH_PB_CPW ? cps : LH_PB_CPW;
     g.chunks_per_wg = cpw;
     const long long wgs = (long long)a.stripes * ((cps + cpw - 1) / cpw);
-#ifndef LH_PB_ORDER
-#define LH_PB_ORDER 1  // (0: an A/B build of the launch order, make HIP_EXTRA=-DLH_PB_ORDER=0)
-#endif
-    if (!LH_PB_ORDER) g.order = nullptr;
-    if (g.order) {
-        if (a.stripes > 1) {
-            hipLaunchKernelGGL(lh_order_kernel, dim3(1), dim3(1024), 0, st, a.plan, a.plan_stride, a.stripes, g.order);
-            note_launch("lh_order_kernel");
-        } else {
-            g.order = nullptr;
-        }
-    }
+    if (!order_stripes(g.order, a.plan, a.plan_stride, a.stripes, a.e_max, st)) g.order = nullptr;
     hipLaunchKernelGGL(lh_inverse_gt_kernel, dim3((unsigned)wgs), dim3(64u * (unsigned)((a.e_max + 7) / 8)), 0, st, g);
     note_launch(g.jump_fallback ? "lh_inverse_gt_kernel(fallback)" : "lh_inverse_gt_kernel");
     return hipGetLastError();

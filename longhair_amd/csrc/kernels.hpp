@@ -75,6 +75,8 @@ struct JumpApplyArgs {
     long long plan_stride;
     int n_in, n_out, bytes, sub, nch, stripes;
     int per_stripe, wps;          // wps: workgroups per stripe (per_stripe 1) = ceil(nch / 64)
+    int *order;                   // per_stripe 1: scratch of `stripes` ints, the stripes by e, largest
+                                  // first (written by launch_apply_jump), or NULL: stripe order
     int dw;                       // bytes per lane per sub-block / 4: 1 (nch = ceil(sub / 4)) or
                                   // 2 (nch = ceil(sub / 8), the two-dword table, sub >= 8)
 };

@@ -23,7 +23,8 @@ pytestmark = pytest.mark.gpu
 FUSED = ["lh_jit_decode_fused"]
 SMALL4 = ["lh_plan_small_kernel<4>", "lh_jit_decode"]
 SMALL8 = ["lh_plan_small_kernel<8>", "lh_jit_decode"]
-GENERIC_CF = ["lh_plan_kernel(closed form)", "lh_apply_jump_kernel"]
+# (e_max > 8: the in-place apply and phase B take their stripes by e, largest first)
+GENERIC_CF = ["lh_plan_kernel(closed form)", "lh_order_kernel", "lh_apply_jump_kernel"]
 GENERIC_S8 = ["lh_plan_small_kernel<8>", "lh_apply_jump_kernel"]
 # the generic decode's fallback (sub < 4, or the overlapping last dword lane alone in its
 # workgroup: sub = 256 t + 1..3): apply into a workspace, then scatter
