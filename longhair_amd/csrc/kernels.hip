@@ -1567,7 +1567,13 @@ hipError_t launch_inverse(const InverseArgs &a, hipStream_t st) {
     g.chunks_per_wg = cpw;
     const long long wgs = (long long)a.stripes * ((cps + cpw - 1) / cpw);
     if (!order_stripes(g.order, a.plan, a.plan_stride, a.stripes, a.e_max, st)) g.order = nullptr;
-    hipLaunchKernelGGL(lh_inverse_gt_kernel, dim3((unsigned)wgs), dim3(64u * (unsigned)((a.e_max + 7) / 8)), 0, st, g);
+    // Spread outputs (e_max > 32) over a power-of-two number of waves, so whole workgroups
+    // fill a CU's wave slots (k200/m56: 8 waves instead of 7, decode 0.594 / 0.583 -> 0.570 /
+    // 0.579 ms, profiles/r5w_phase_b_pow2.txt).
+    int nw = (a.e_max + 7) / 8;
+    if (!g.pack)
+        while (nw & (nw - 1)) nw += nw & -nw;  // round up
+    hipLaunchKernelGGL(lh_inverse_gt_kernel, dim3((unsigned)wgs), dim3(64u * (unsigned)nw), 0, st, g);
     note_launch(g.jump_fallback ? "lh_inverse_gt_kernel(fallback)" : "lh_inverse_gt_kernel");
     return hipGetLastError();
 }
