@@ -763,8 +763,31 @@ static int encode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
         }
         if (hard) return fail(kHipError, err);
     }
-    // Gather / strided encode / scatter, per chunk.  An invalid shape (m > 1 with k + m > 256
-    // or bytes % 8 != 0) still gets recovery block 0 first, as the reference.
+    // Generic shapes (no specialised module, or one still compiling): the jump-table apply
+    // reads the data blocks and writes the recovery blocks through the tables themselves.
+    if (k > 1 && m > 1 && k + m <= 256 && bytes % 8 == 0 && bytes / 8 >= 4) {
+        const uint8_t *G = nullptr;
+        if (int rc = device_generator(d, k, m, &G, nullptr, st)) return rc;
+        JumpApplyArgs a{};
+        a.in_ptrs = data_ptrs;
+        a.in_n = k;
+        a.out_ptrs = rec_ptrs;
+        a.out_n = m;
+        a.coef = G;
+        a.coef_stride = 0;
+        a.n_in = k;
+        a.n_out = m;
+        a.bytes = bytes;
+        a.sub = bytes / 8;
+        a.stripes = stripes;
+        a.per_stripe = 0;
+        jump_layout(d, a, false);
+        LH_HIP(launch_apply_jump(a, st));
+        return kOk;
+    }
+    // Gather / strided encode / scatter, per chunk (m = 1, k = 1, sub < 4).  An invalid shape
+    // (m > 1 with k + m > 256 or bytes % 8 != 0) still gets recovery block 0 first, as the
+    // reference.
     const bool invalid = m > 1 && k > 1 && (k + m > 256 || bytes % 8 != 0);
     const long long per = (long long)(k + m) * bytes;
     uint8_t *buf = nullptr;
@@ -868,7 +891,39 @@ static int decode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
             return kOk;
         }
     }
-    // Gather / strided decode / scatter, per chunk.  Only the slots the decode may have
+    // Generic shapes: the planner, then the jump-table apply in place through the table (the
+    // strided decode's rules: dword lanes from sub = 4, and the overlapping last lane of a
+    // sub-block must share its neighbour's workgroup).
+    if (k > 1 && m > 1) {
+        const int sub = bytes / 8, jnch = (sub + 3) / 4;
+        if (sub >= 4 && !(sub % 4 != 0 && jnch > 1 && (jnch - 1) % 64 == 0)) {
+            const int e_max = k < m ? k : m;
+            const long long plan_stride = PlanView::bytes(k, m, e_max);
+            Workspace *w = nullptr;
+            if (int rc = run_planner(d, st, k, m, e_max, stripes, d_rows, d_status, 0, true, &w)) return rc;
+            JumpApplyArgs a{};
+            a.in_ptrs = block_ptrs;
+            a.out_ptrs = block_ptrs;
+            a.in_n = k;
+            a.out_n = k;
+            a.coef = w->plan.ptr + PlanView::w_offset(k, m, e_max);
+            a.coef_stride = plan_stride;
+            a.plan = w->plan.ptr;
+            a.plan_stride = plan_stride;
+            a.n_in = k;
+            a.n_out = e_max;
+            a.bytes = bytes;
+            a.sub = sub;
+            a.stripes = stripes;
+            a.per_stripe = 1;
+            a.order = (int *)(w->plan.ptr + plan_order_offset(stripes, plan_stride));
+            jump_layout(d, a, true);
+            LH_HIP(launch_apply_jump(a, st));
+            return kOk;
+        }
+    }
+    // Gather / strided decode / scatter, per chunk (m = 1, k = 1, tiny or lone-tail blocks).
+    // Only the slots the decode may have
     // changed go back, judged by the rows before the call (a copy of the chunk's rows rides
     // at the end of the chunk): for k, m > 1 the slots that held recovery rows (row >= k) of
     // the stripes it decoded (status 0); for m = 1 the one output slot of cauchy_decode_m1

@@ -1051,6 +1051,20 @@ __device__ __forceinline__ void lh_ja_load(uint32_t (&d)[8], const uint8_t *col,
     }
 }
 
+// Input column j of the lane's stripe at its chunk offset, through the pointer table when
+// the batch has one; the output slot / row `o` likewise.
+// (PTR: a separate kernel instantiation, so the strided form keeps its register budget)
+template <bool PTR>
+__device__ __forceinline__ const uint8_t *lh_ja_col(const lh::JumpApplyArgs &a, const lh_ja_lane &l, int j) {
+    if constexpr (PTR) return a.in_ptrs[l.stripe * a.in_n + j] + l.p;
+    return a.in + l.stripe * a.in_stride + (long long)j * a.bytes + l.p;
+}
+template <bool PTR>
+__device__ __forceinline__ uint8_t *lh_ja_out(const lh::JumpApplyArgs &a, const lh_ja_lane &l, int o) {
+    if constexpr (PTR) return a.out_ptrs[l.stripe * a.out_n + o] + l.p;
+    return a.out + l.stripe * a.out_stride + (long long)o * a.bytes + l.p;
+}
+
 __device__ __forceinline__ void lh_ja_tables(const uint32_t (&d)[8], uint32_t (&tl)[16], uint32_t (&th)[16]) {
     tl[0] = th[0] = 0;
 #pragma unroll
@@ -1064,11 +1078,10 @@ __device__ __forceinline__ void lh_ja_tables(const uint32_t (&d)[8], uint32_t (&
 // One round: outputs i0 .. i0 + N - 1 of this wave over every input column.  GT: the table
 // once per code object (lh_mul_jump_g); else the in-asm table (lh_mul_jump_idx8, a table
 // straddling a 4 GiB boundary; coefficient 0 = body 0 leaves unused outputs unchanged).
-template <int N, bool GT>
+template <int N, bool GT, bool PTR = false>
 __device__ __forceinline__ void lh_ja_round(const lh::JumpApplyArgs &a, const lh_ja_lane &l, const uint8_t *coef,
                                             int i0, uint32_t (&acc)[8][8], uint32_t tlo, uint32_t thi) {
     const int lane = threadIdx.x & 63;
-    const uint8_t *in = a.in + l.stripe * a.in_stride + l.p;
     for (int jq = 0; jq * 64 < a.n_in; ++jq) {  // 64 columns per block of body addresses
         const int jc = jq * 64 + lane;
         uint32_t t[8], cpk0 = 0, cpk1 = 0;
@@ -1081,11 +1094,11 @@ __device__ __forceinline__ void lh_ja_round(const lh::JumpApplyArgs &a, const lh
         }
         const int nj = a.n_in - jq * 64 < 64 ? a.n_in - jq * 64 : 64;
         uint32_t cur[8];
-        lh_ja_load(cur, in + (long long)(jq * 64) * a.bytes, a.sub, l.active);
+        lh_ja_load(cur, lh_ja_col<PTR>(a, l, jq * 64), a.sub, l.active);
         for (int jl = 0; jl < nj; ++jl) {  // wave-uniform
             const int jn = jq * 64 + jl + 1 < a.n_in ? jq * 64 + jl + 1 : jq * 64 + jl;  // (the last reloads itself)
             uint32_t nxt[8];
-            lh_ja_load(nxt, in + (long long)jn * a.bytes, a.sub, l.active);
+            lh_ja_load(nxt, lh_ja_col<PTR>(a, l, jn), a.sub, l.active);
             uint32_t tl[16], th[16];
             lh_ja_tables(cur, tl, th);
             if constexpr (GT) {
@@ -1100,7 +1113,7 @@ __device__ __forceinline__ void lh_ja_round(const lh::JumpApplyArgs &a, const lh
     }
 }
 
-template <bool GT>
+template <bool GT, bool PTR>
 __device__ __forceinline__ void lh_apply_jump_body(const lh::JumpApplyArgs &a, uint32_t tlo, uint32_t thi) {
     const int lane = threadIdx.x & 63;
     const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), ng = (int)(blockDim.x >> 6);
@@ -1143,14 +1156,14 @@ __device__ __forceinline__ void lh_apply_jump_body(const lh::JumpApplyArgs &a, u
             for (int y = 0; y < 8; ++y) acc[i][y] = 0;
         switch (nout) {  // wave-uniform
             case 0: break;
-            case 1: lh_ja_round<1, GT>(a, l, coef, i0, acc, tlo, thi); break;
-            case 2: lh_ja_round<2, GT>(a, l, coef, i0, acc, tlo, thi); break;
-            case 3: lh_ja_round<3, GT>(a, l, coef, i0, acc, tlo, thi); break;
-            case 4: lh_ja_round<4, GT>(a, l, coef, i0, acc, tlo, thi); break;
-            case 5: lh_ja_round<5, GT>(a, l, coef, i0, acc, tlo, thi); break;
-            case 6: lh_ja_round<6, GT>(a, l, coef, i0, acc, tlo, thi); break;
-            case 7: lh_ja_round<7, GT>(a, l, coef, i0, acc, tlo, thi); break;
-            default: lh_ja_round<8, GT>(a, l, coef, i0, acc, tlo, thi); break;
+            case 1: lh_ja_round<1, GT, PTR>(a, l, coef, i0, acc, tlo, thi); break;
+            case 2: lh_ja_round<2, GT, PTR>(a, l, coef, i0, acc, tlo, thi); break;
+            case 3: lh_ja_round<3, GT, PTR>(a, l, coef, i0, acc, tlo, thi); break;
+            case 4: lh_ja_round<4, GT, PTR>(a, l, coef, i0, acc, tlo, thi); break;
+            case 5: lh_ja_round<5, GT, PTR>(a, l, coef, i0, acc, tlo, thi); break;
+            case 6: lh_ja_round<6, GT, PTR>(a, l, coef, i0, acc, tlo, thi); break;
+            case 7: lh_ja_round<7, GT, PTR>(a, l, coef, i0, acc, tlo, thi); break;
+            default: lh_ja_round<8, GT, PTR>(a, l, coef, i0, acc, tlo, thi); break;
         }
         // In place (decode): every wave of the workgroup has read every slot of this chunk
         // before any output overwrites one (the host runs a single round there).
@@ -1159,10 +1172,9 @@ __device__ __forceinline__ void lh_apply_jump_body(const lh::JumpApplyArgs &a, u
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 if (i < nout) {
-                    uint8_t *dst = pl ? a.out + l.stripe * a.out_stride + (long long)pl[16 + i0 + i] * a.bytes
-                                      : a.out + l.stripe * a.out_stride + (long long)(i0 + i) * a.bytes;
+                    uint8_t *dst = lh_ja_out<PTR>(a, l, pl ? (int)pl[16 + i0 + i] : i0 + i);
 #pragma unroll
-                    for (int y = 0; y < 8; ++y) *(lh_u32u *)(dst + l.p + (long long)y * a.sub) = acc[i][y];
+                    for (int y = 0; y < 8; ++y) *(lh_u32u *)(dst + (long long)y * a.sub) = acc[i][y];
                 }
             }
         }
@@ -1170,6 +1182,7 @@ __device__ __forceinline__ void lh_apply_jump_body(const lh::JumpApplyArgs &a, u
 }
 }  // namespace
 
+template <bool PTR>
 __global__ void __launch_bounds__(1024) lh_apply_jump_kernel(lh::JumpApplyArgs a) {
     uint32_t tlo, thi;
     asm volatile(
@@ -1182,10 +1195,10 @@ __global__ void __launch_bounds__(1024) lh_apply_jump_kernel(lh::JumpApplyArgs a
         :
         : "s92", "s93", "scc");
     if (tlo > 0xFFFFFFFFu - 256u * 68u) {  // the table straddles a 4 GiB boundary (never seen)
-        lh_apply_jump_body<false>(a, tlo, thi);
+        lh_apply_jump_body<false, PTR>(a, tlo, thi);
         return;
     }
-    lh_apply_jump_body<true>(a, tlo, thi);
+    lh_apply_jump_body<true, PTR>(a, tlo, thi);
 }
 
 // ---- two-dword form (a.dw == 2): a lane owns 8 bytes of every sub-block and a jump enters
@@ -1249,11 +1262,10 @@ __device__ __forceinline__ void lh_ja_tables2(const uint32_t (&d)[8][2], uint32_
     }
 }
 
-template <int N>
+template <int N, bool PTR>
 __device__ __forceinline__ bool lh_ja_round2(const lh::JumpApplyArgs &a, const lh_ja_lane &l, const uint8_t *coef,
                                              int i0, uint32_t (&acc)[4][16], uint32_t tlo, uint32_t thi) {
     const int lane = threadIdx.x & 63;
-    const uint8_t *in = a.in + l.stripe * a.in_stride + l.p;
     bool ok = true;
     for (int jq = 0; jq * 64 < a.n_in; ++jq) {
         const int jc = jq * 64 + lane;
@@ -1265,11 +1277,11 @@ __device__ __forceinline__ bool lh_ja_round2(const lh::JumpApplyArgs &a, const l
         }
         const int nj = a.n_in - jq * 64 < 64 ? a.n_in - jq * 64 : 64;
         uint32_t cur[8][2];
-        lh_ja_load2(cur, in + (long long)(jq * 64) * a.bytes, a.sub, l.active);
+        lh_ja_load2(cur, lh_ja_col<PTR>(a, l, jq * 64), a.sub, l.active);
         for (int jl = 0; jl < nj; ++jl) {  // wave-uniform
             const int jn = jq * 64 + jl + 1 < a.n_in ? jq * 64 + jl + 1 : jq * 64 + jl;
             uint32_t nxt[8][2];
-            lh_ja_load2(nxt, in + (long long)jn * a.bytes, a.sub, l.active);
+            lh_ja_load2(nxt, lh_ja_col<PTR>(a, l, jn), a.sub, l.active);
             uint32_t tl[16][2], th[16][2];
             lh_ja_tables2(cur, tl, th);
             if (ok) ok = lh_mul_jump_g2<N>(acc, tl, th, t, jl, tlo, thi);
@@ -1283,6 +1295,7 @@ __device__ __forceinline__ bool lh_ja_round2(const lh::JumpApplyArgs &a, const l
 // gt: the table's address is usable.  The host launches this kernel only after
 // probe_jump_tables found lh_inv_gtab2 within one 4 GiB page; a failed check here (or in the
 // debug build's target check) poisons the outputs, so the parity tests fail loudly.
+template <bool PTR>
 __device__ __forceinline__ void lh_apply_jump2_body(const lh::JumpApplyArgs &a, bool gt, uint32_t tlo,
                                                     uint32_t thi) {
     const int lane = threadIdx.x & 63;
@@ -1323,10 +1336,10 @@ __device__ __forceinline__ void lh_apply_jump2_body(const lh::JumpApplyArgs &a, 
         if (gt) {
             switch (nout) {  // wave-uniform
                 case 0: break;
-                case 1: ok = lh_ja_round2<1>(a, l, coef, i0, acc, tlo, thi); break;
-                case 2: ok = lh_ja_round2<2>(a, l, coef, i0, acc, tlo, thi); break;
-                case 3: ok = lh_ja_round2<3>(a, l, coef, i0, acc, tlo, thi); break;
-                default: ok = lh_ja_round2<4>(a, l, coef, i0, acc, tlo, thi); break;
+                case 1: ok = lh_ja_round2<1, PTR>(a, l, coef, i0, acc, tlo, thi); break;
+                case 2: ok = lh_ja_round2<2, PTR>(a, l, coef, i0, acc, tlo, thi); break;
+                case 3: ok = lh_ja_round2<3, PTR>(a, l, coef, i0, acc, tlo, thi); break;
+                default: ok = lh_ja_round2<4, PTR>(a, l, coef, i0, acc, tlo, thi); break;
             }
         }
         if (pl && ng > 1) __syncthreads();  // in place: every slot read before any is written
@@ -1334,13 +1347,12 @@ __device__ __forceinline__ void lh_apply_jump2_body(const lh::JumpApplyArgs &a, 
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 if (i < nout) {
-                    uint8_t *dst = pl ? a.out + l.stripe * a.out_stride + (long long)pl[16 + i0 + i] * a.bytes
-                                      : a.out + l.stripe * a.out_stride + (long long)(i0 + i) * a.bytes;
+                    uint8_t *dst = lh_ja_out<PTR>(a, l, pl ? (int)pl[16 + i0 + i] : i0 + i);
 #pragma unroll
                     for (int y = 0; y < 8; ++y) {
                         const unsigned long long v = ok ? ((unsigned long long)acc[i][2 * y + 1] << 32) | acc[i][2 * y]
                                                         : 0xDEADBEEFDEADBEEFull;
-                        *(lh_u64u *)(dst + l.p + (long long)y * a.sub) = v;
+                        *(lh_u64u *)(dst + (long long)y * a.sub) = v;
                     }
                 }
             }
@@ -1349,6 +1361,7 @@ __device__ __forceinline__ void lh_apply_jump2_body(const lh::JumpApplyArgs &a, 
 }
 }  // namespace
 
+template <bool PTR>
 __global__ void __launch_bounds__(768) lh_apply_jump2_kernel(lh::JumpApplyArgs a) {
     uint32_t tlo, thi;
     asm volatile(
@@ -1360,7 +1373,7 @@ __global__ void __launch_bounds__(768) lh_apply_jump2_kernel(lh::JumpApplyArgs a
         : "=s"(tlo), "=s"(thi)
         :
         : "s92", "s93", "scc");
-    lh_apply_jump2_body(a, tlo <= 0xFFFFFFFFu - 256u * 132u, tlo, thi);
+    lh_apply_jump2_body<PTR>(a, tlo <= 0xFFFFFFFFu - 256u * 132u, tlo, thi);
 }
 
 // The low words of the two jump tables' addresses (out[0]: lh_inv_gtab, out[1]: lh_inv_gtab2),
@@ -1500,8 +1513,11 @@ hipError_t launch_apply_jump(const JumpApplyArgs &a, hipStream_t st) {
         if (wgs > 0x7FFFFFFF) return hipErrorInvalidValue;
         JumpApplyArgs g = a;
         if (!order_stripes(g.order, a.plan, a.plan_stride, a.per_stripe ? a.stripes : 0, a.n_out, st)) g.order = nullptr;
-        hipLaunchKernelGGL(lh_apply_jump2_kernel, dim3((unsigned)wgs), dim3(64u * (unsigned)ng), 0, st, g);
-        note_launch("lh_apply_jump2_kernel");
+        if (a.in_ptrs)
+            hipLaunchKernelGGL(lh_apply_jump2_kernel<true>, dim3((unsigned)wgs), dim3(64u * (unsigned)ng), 0, st, g);
+        else
+            hipLaunchKernelGGL(lh_apply_jump2_kernel<false>, dim3((unsigned)wgs), dim3(64u * (unsigned)ng), 0, st, g);
+        note_launch(a.in_ptrs ? "lh_apply_jump2_kernel(pointer table)" : "lh_apply_jump2_kernel");
         return hipGetLastError();
     }
     if (a.dw != 1) return hipErrorInvalidValue;
@@ -1518,8 +1534,11 @@ hipError_t launch_apply_jump(const JumpApplyArgs &a, hipStream_t st) {
     if (wgs > 0x7FFFFFFF) return hipErrorInvalidValue;
     JumpApplyArgs g = a;
     if (!order_stripes(g.order, a.plan, a.plan_stride, a.per_stripe ? a.stripes : 0, a.n_out, st)) g.order = nullptr;
-    hipLaunchKernelGGL(lh_apply_jump_kernel, dim3((unsigned)wgs), dim3(64u * (unsigned)ng), 0, st, g);
-    note_launch("lh_apply_jump_kernel");
+    if (a.in_ptrs)
+        hipLaunchKernelGGL(lh_apply_jump_kernel<true>, dim3((unsigned)wgs), dim3(64u * (unsigned)ng), 0, st, g);
+    else
+        hipLaunchKernelGGL(lh_apply_jump_kernel<false>, dim3((unsigned)wgs), dim3(64u * (unsigned)ng), 0, st, g);
+    note_launch(a.in_ptrs ? "lh_apply_jump_kernel(pointer table)" : "lh_apply_jump_kernel");
     return hipGetLastError();
 }
 

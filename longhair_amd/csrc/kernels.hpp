@@ -75,6 +75,9 @@ struct JumpApplyArgs {
     long long plan_stride;
     int n_in, n_out, bytes, sub, nch, stripes;
     int per_stripe, wps;          // wps: workgroups per stripe (per_stripe 1) = ceil(nch / 64)
+    uint8_t *const *in_ptrs;      // pointer tables (cauchy_256_*_batch_ptrs), else NULL: input j of
+    uint8_t *const *out_ptrs;     // stripe s at in_ptrs[s*in_n + j], output i (or, per_stripe 1, the
+    int in_n, out_n;              // plan's slot i) at out_ptrs[s*out_n + i] (in, out, strides unused)
     int *order;                   // per_stripe 1: scratch of `stripes` ints, the stripes by e, largest
                                   // first (written by launch_apply_jump), or NULL: stripe order
     int dw;                       // bytes per lane per sub-block / 4: 1 (nch = ceil(sub / 4)) or

@@ -229,7 +229,7 @@ def test_dropin_mixed_pointers(lh):
 
 @pytest.mark.parametrize("k,m,nbytes,trace", [
     (29, 4, 1296, "lh_jit_encode(pointer table)"), (128, 32, 8192, "lh_jit_encode_win(pointer table)"),
-    (200, 3, 64, "lh_ptr_copy_kernel(gather)"), (10, 1, 100, "lh_ptr_copy_kernel(gather)"),
+    (200, 3, 64, "lh_apply_jump2_kernel(pointer table)"), (10, 1, 100, "lh_ptr_copy_kernel(gather)"),
     (1, 3, 40, "lh_ptr_copy_kernel(gather)")])
 def test_dropin_device_pointers(lh, oracle, k, m, nbytes, trace):
     """Blocks that already live in device memory go through the same entry points: every

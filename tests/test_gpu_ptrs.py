@@ -7,8 +7,9 @@ addresses included), so no two blocks of a stripe are adjacent or in order.  Res
 bit-identical to the strided batch calls on the same inputs (those are checked against the
 oracle in test_gpu_parity.py) and, on a sample of stripes, to the C oracle directly.  The
 launch trace shows which form ran: the specialised kernels reading the blocks in place
-("(pointer table)": the register networks and the windowed large-m kernels with the phase-B
-kernel) or the gather / strided / scatter form."""
+("(pointer table)": the register networks, the windowed large-m kernels with the phase-B
+kernel, and for shapes without a specialised module the generic jump apply) or the gather /
+strided / scatter form (m = 1, k = 1, sub-blocks under 4 bytes, the lone-last-lane decode)."""
 import numpy as np
 import pytest
 
@@ -66,8 +67,9 @@ ENCODE = [
     (128, 32, 8192, 3, "lh_jit_encode_win(pointer table)"),   # windowed large-m encode
     (40, 20, 4096, 6, "lh_jit_encode_win(pointer table)"),
     (200, 56, 65536, 2, "lh_jit_encode_win(pointer table)"),
-    (40, 20, 1024, 5, "lh_ptr_copy_kernel(gather)"),    # large m, sub % 256 != 0: generic, gathered
-    (200, 3, 64, 5, "lh_ptr_copy_kernel(gather)"),      # k > 128: generic kernels, gathered
+    (40, 20, 1024, 5, "lh_apply_jump_kernel(pointer table)"),   # large m, sub % 256 != 0: generic, in place
+    (200, 3, 64, 5, "lh_apply_jump2_kernel(pointer table)"),     # k > 128: generic, two-dword lanes (m <= 4)
+    (40, 20, 24, 5, "lh_ptr_copy_kernel(gather)"),               # sub < 4: the bytewise generic kernel, gathered
     (10, 1, 100, 7, "lh_ptr_copy_kernel(gather)"),      # m = 1, any block size
     (1, 3, 40, 5, "lh_ptr_copy_kernel(gather)"),        # k = 1 copies
 ]
@@ -119,8 +121,10 @@ DECODE = [
     (128, 32, 8192, 3, "lh_jit_decode_wide(pointer table)"),  # planner, phase A and phase B through the table
     (40, 20, 4096, 6, "lh_jit_decode_wide(pointer table)"),
     (200, 56, 65536, 3, "lh_jit_decode_wide(pointer table)"),
-    (40, 20, 1024, 5, "lh_ptr_copy_kernel(gather)"),
-    (200, 3, 64, 5, "lh_ptr_copy_kernel(gather)"),
+    (40, 20, 1024, 5, "lh_apply_jump_kernel(pointer table)"),
+    (200, 3, 64, 5, "lh_apply_jump_kernel(pointer table)"),
+    (40, 20, 4104, 3, "lh_ptr_copy_kernel(gather)"),   # sub 513: the last dword lane alone in its workgroup
+    (40, 20, 24, 5, "lh_ptr_copy_kernel(gather)"),
     (10, 1, 100, 7, "lh_ptr_copy_kernel(gather)"),
     (1, 3, 40, 5, "lh_ptr_copy_kernel(gather)"),
 ]
@@ -206,7 +210,7 @@ def test_decode_batch_ptrs_roundtrip_baseline_shape(lh):
     assert torch.equal(got, torch.gather(data, 1, lost.unsqueeze(2).expand(stripes, 4, nbytes)))
 
 
-@pytest.mark.parametrize("k,m,nbytes", [(200, 3, 64), (10, 1, 100), (40, 20, 1024)])
+@pytest.mark.parametrize("k,m,nbytes", [(40, 20, 24), (10, 1, 100), (1, 3, 40)])
 def test_ptrs_gather_in_chunks(lh, oracle, monkeypatch, k, m, nbytes):
     """The gather / strided / scatter form over several workspace chunks (the chunk capped by
     LONGHAIR_AMD_PTR_CHUNK_BYTES at 3 stripes for the encode, 3-4 for the decode; 11
