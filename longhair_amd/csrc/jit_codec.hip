@@ -450,7 +450,8 @@ struct lh_unroll_encode<LH_K> {
 // chunk unshifted (only LH_VLAST bytes are its own) and stores [sub - 8, sub) assembled with
 // the previous lane's word (DPP row_shr:1; the host checks both lanes share a DPP row).
 // That last lane's word pair may reach up to 16 bytes past its stripe's image (bytes that are
-// never its own): each ring carries 16 bytes of padding, so the read stays in the wave's ring.
+// never its own): when the image ends within 16 bytes of its slot's end, each ring carries 16
+// bytes of padding (LH_LPAD), so the read stays in the wave's ring.
 #ifndef LH_LDS
 #define LH_LDS 0
 #endif
@@ -461,8 +462,13 @@ struct lh_unroll_encode<LH_K> {
 #ifndef LH_LD
 #define LH_LD 4  // ring slots per wave (columns in flight + the one being read)
 #endif
+#ifndef LH_LDE
+#define LH_LDE LH_LD  // the encode's ring (its module is compiled apart from the decode's)
+#endif
 #define LH_LQ ((LH_SPW * LH_BYTES + 1023) / 1024)  // DMA instructions per column
 #define LH_VLAST (LH_SUB - 8 * (LH_NCH - 1))      // valid bytes of the last chunk of a sub-block
+// (ring padding: only when the image ends within 16 bytes of its slot's end)
+#define LH_LPAD ((LH_SPW * LH_BYTES + 16 > LH_LQ * 1024) ? 16 : 0)
 typedef unsigned int lh_u32x2a __attribute__((ext_vector_type(2)));
 // Bytes [S, S + 8) of the 16 little-endian bytes (a, b).
 template <int S>
@@ -530,11 +536,11 @@ __device__ __forceinline__ void lh_lds_put(unsigned char *p, const lh_word &w) {
 // LH_LDS_FLAT_ST: the encode's recovery blocks leave through the ring (below) when the
 // wave's output image fits it.
 #ifndef LH_LDS_FLAT_ST
-#define LH_LDS_FLAT_ST (LH_SPW * LH_M * LH_BYTES <= LH_LD * LH_LQ * 1024)
+#define LH_LDS_FLAT_ST (LH_SPW * LH_M * LH_BYTES <= LH_LDE * LH_LQ * 1024)
 #endif
 struct lh_ldsrc {
     const unsigned char *src[LH_LQ];  // this lane's chunk of DMA instruction q, column 0
-    unsigned char *ring;              // this wave's LH_LD slots of LH_LQ KiB
+    unsigned char *ring;              // this wave's LH_LDE slots of LH_LQ KiB
     __device__ __forceinline__ void issue(int x, int slot) const {
 #pragma unroll
         for (int q = 0; q < LH_LQ; ++q)
@@ -553,16 +559,16 @@ struct lh_unroll_encode_lds {
     __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], const lh_ldsrc &S, int lo, int lo8) {
         if constexpr (X < LH_K) {
             // this column's DMAs landed: all but those of the columns issued after it
-            constexpr int ahead = (LH_LD - 1) < (LH_K - 1 - X) ? (LH_LD - 1) : (LH_K - 1 - X);
+            constexpr int ahead = (LH_LDE - 1) < (LH_K - 1 - X) ? (LH_LDE - 1) : (LH_K - 1 - X);
             lh_wait_vmcnt<LH_LQ * ahead>();
             asm volatile("" ::: "memory");  // no LDS read moves above the wait
             lh_word d[8];
-            lh_slot_col(d, S.ring + (X % LH_LD) * (LH_LQ * 1024), lo, lo8);
+            lh_slot_col(d, S.ring + (X % LH_LDE) * (LH_LQ * 1024), lo, lo8);
             lh_column<X>(acc, d);
             lh_opaque(acc);
-            if constexpr (X + LH_LD < LH_K) {
+            if constexpr (X + LH_LDE < LH_K) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done
-                S.issue(X + LH_LD, X % LH_LD);
+                S.issue(X + LH_LDE, X % LH_LDE);
             }
             lh_unroll_encode_lds<X + 1>::run(acc, S, lo, lo8);
         }
@@ -591,7 +597,7 @@ __device__ __forceinline__ void lh_img_row(unsigned char *row, const lh_word (&a
 __device__ __forceinline__ void lh_encode_wave_lds(long long wave, const unsigned char *__restrict__ in,
                                                    long long in_stride, unsigned char *__restrict__ out,
                                                    long long out_stride, int stripes) {
-    __shared__ __attribute__((aligned(16))) unsigned char lh_lring[4][LH_LD * LH_LQ * 1024 + 16];
+    __shared__ __attribute__((aligned(16))) unsigned char lh_lring[4][LH_LDE * LH_LQ * 1024 + LH_LPAD];
     const int lane = threadIdx.x & 63;
     const int sl = lane / LH_NCH, c = lane - sl * LH_NCH;
     const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)wave) * LH_SPW;  // wave-uniform
@@ -607,7 +613,7 @@ __device__ __forceinline__ void lh_encode_wave_lds(long long wave, const unsigne
         S.src[q] = in + (s0 + js) * in_stride + (j - js * (LH_BYTES / 16)) * 16;
     }
 #pragma unroll
-    for (int q = 0; q < LH_LD; ++q)
+    for (int q = 0; q < LH_LDE; ++q)
         if (q < LH_K) S.issue(q, q);
     lh_word acc[LH_M][8];
 #pragma unroll
@@ -1447,7 +1453,7 @@ __device__ __forceinline__ void lh_fused_wave_lds(const lh_lane &l, long long wa
                                                   const unsigned char *scr, unsigned char *__restrict__ blocks,
                                                   long long stripe_stride, int stripes, const lh_fused_solve &sv,
                                                   lh_plan_regs &pr) {
-    __shared__ __attribute__((aligned(16))) unsigned char lh_dring[4][LH_LD * LH_LQ * 1024 + 16];
+    __shared__ __attribute__((aligned(16))) unsigned char lh_dring[4][LH_LD * LH_LQ * 1024 + LH_LPAD];
     const int lane = threadIdx.x & 63;
     const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)wave) * LH_SPW;  // wave-uniform
     if (s0 >= stripes) return;  // wave-uniform
