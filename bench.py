@@ -126,7 +126,17 @@ def setup_dist(dry, share_gpu=False):
     if not dry:
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()) if share_gpu else local)
     if world > 1:
-        dist.init_process_group(backend="gloo")
+        # gloo prints its connection report ("[Gloo] Rank r is connected to ...") on file
+        # descriptor 1 from C++; stdout carries only rank 0's JSON line, so fd 1 points at
+        # stderr while the group connects.
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group(backend="gloo")
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
     return world, rank, local
 
 
