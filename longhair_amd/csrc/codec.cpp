@@ -410,7 +410,8 @@ static int encode_batch(int k, int m, int bytes, int stripes, const uint8_t *d_d
             const unsigned threads = 64u * (unsigned)((m + cfg.rows_per_wave - 1) / cfg.rows_per_wave);
             long long in_stride = data_stride, out_stride = rec_stride;
             int n = stripes;
-            void *args[] = {(void *)&d_data, &in_stride, (void *)&d_rec, &out_stride, &n};
+            int bb = bytes;  // (windowed modules take the block size as an argument)
+            void *args[] = {(void *)&d_data, &in_stride, (void *)&d_rec, &out_stride, &n, &bb};
             LH_HIP(hipModuleLaunchKernel(jk->encode_win, (unsigned)blocks, 1, 1, threads, 1, 1, 0, st, args, nullptr));
             note_launch("lh_jit_encode_win");
             return kOk;
@@ -603,7 +604,8 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
             long long s1 = stride, s2 = plan_stride;
             const uint8_t *plan = w->plan.ptr;
             int nn = stripes;
-            void *args[] = {(void *)&d_blocks, &s1, (void *)&plan, &s2, (void *)&zero, &nn};
+            int bb = bytes;  // (windowed modules take the block size as an argument)
+            void *args[] = {(void *)&d_blocks, &s1, (void *)&plan, &s2, (void *)&zero, &nn, &bb};
             LH_HIP(hipModuleLaunchKernel(wk->decode_wide, (unsigned)(stripes * cps), 1, 1, threads, 1, 1, 0, st, args,
                                          nullptr));
             note_launch("lh_jit_decode_wide");
@@ -756,7 +758,8 @@ static int encode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
             const unsigned threads = 64u * (unsigned)((m + cfg.rows_per_wave - 1) / cfg.rows_per_wave);
             long long in_stride = (long long)k * 8, out_stride = (long long)m * 8;
             int n = stripes;
-            void *args[] = {(void *)&data_ptrs, &in_stride, (void *)&rec_ptrs, &out_stride, &n};
+            int bb = bytes;  // (windowed modules take the block size as an argument)
+            void *args[] = {(void *)&data_ptrs, &in_stride, (void *)&rec_ptrs, &out_stride, &n, &bb};
             LH_HIP(hipModuleLaunchKernel(jk->encode_win, (unsigned)blocks, 1, 1, threads, 1, 1, 0, st, args, nullptr));
             note_launch("lh_jit_encode_win(pointer table)");
             return kOk;
@@ -873,7 +876,8 @@ static int decode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
             long long s1 = (long long)k * 8, s2 = plan_stride;
             const uint8_t *plan = w->plan.ptr;
             int n = stripes;
-            void *args[] = {(void *)&block_ptrs, &s1, (void *)&plan, &s2, (void *)&zero, &n};
+            int bb = bytes;  // (windowed modules take the block size as an argument)
+            void *args[] = {(void *)&block_ptrs, &s1, (void *)&plan, &s2, (void *)&zero, &n, &bb};
             LH_HIP(hipModuleLaunchKernel(wk->decode_wide, (unsigned)(stripes * cps), 1, 1, threads, 1, 1, 0, st, args,
                                          nullptr));
             note_launch("lh_jit_decode_wide(pointer table)");

@@ -193,12 +193,13 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
            << (elim ? "const unsigned long long (&cpl)[LH_NQ], const unsigned int (&slv)[LH_NQ], "
                       "const unsigned char *__restrict__ pl"
                     : "const unsigned long long (&ptl)[LH_NP], const unsigned long long (&otl)[LH_NPO]")
-           << ", const int coff, const int loff) {\n";
+           << ", const int coff, const int loff, const int lh_bytes, const int lh_sub) {\n";
     else
     os << "__device__ __forceinline__ void lh_wg" << g << "(" << (elim ? "" : "const ") << "unsigned char *__restrict__ base, "
        << (elim ? "const unsigned int (&slv)[LH_NQ], const unsigned char *__restrict__ pl"
                 : "unsigned char *__restrict__ o")
-       << ", const unsigned char *__restrict__ sb, const unsigned char *__restrict__ zb) {\n";
+       << ", const unsigned char *__restrict__ sb, const unsigned char *__restrict__ zb, const int lh_bytes,"
+          " const int lh_sub) {\n";
     {  // (Starting the accumulators at R_r, loaded before the column loop, measured equal:
        // k128/m32 decode 4.12 / 4.11 ms, k200/m56 0.83 / 0.81 ms.)
         for (int r = r0; r < r1; ++r)
@@ -211,8 +212,8 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
         std::ostringstream e;
         if (c.ptr && elim) e << "(lh_pp(cpl, " << x << ") + coff)";
         else if (c.ptr) e << "(lh_pp(ptl, " << x << ") + coff)";
-        else if (elim) e << "lh_slot(slv, " << x << ", sb, zb)";
-        else e << "(sb + " << (long long)x * c.bytes << "LL)";
+        else if (elim) e << "lh_slot(slv, " << x << ", sb, zb, lh_bytes)";
+        else e << "(sb + (long long)" << x << " * lh_bytes)";
         return e.str();
     };
     auto dma = [&](int x, const char *ind) {
@@ -224,8 +225,8 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
     os << "  const int lane = threadIdx.x & 63;\n";
     for (int h = 0; h < 2; ++h)
         if (NG == 1 || g == h)
-            os << "  const unsigned int dof" << h << " = ((" << 64 * h << " + lane) >> 4) * " << c.sub
-               << "u + ((lane & 15) << 4);\n";
+            os << "  const unsigned int dof" << h << " = ((" << 64 * h << " + lane) >> 4) * (unsigned)lh_sub"
+               << " + ((lane & 15) << 4);\n";
     for (int q = 0; q < PF && q < k; ++q) dma(q, "  ");
     for (int x = 0; x < k; ++x) {
         os << "  {\n";
@@ -287,24 +288,24 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
             if (c.ptr)
                 os << "      unsigned char *rp = lh_pp(cpl, " << k + r << ") + loff;\n";
             else
-                os << "      unsigned char *rp = base + (long long)s * " << c.bytes << ";\n";
+                os << "      unsigned char *rp = base + (long long)s * lh_bytes;\n";
             for (int y = 0; y < 8; ++y)
-                os << "      const unsigned int r" << y << " = lh_ld_r(rp + " << y * c.sub << ");\n";
+                os << "      const unsigned int r" << y << " = lh_ld_r(rp + " << y << " * lh_sub);\n";
             for (int y = 0; y < 8; ++y)
-                os << "      lh_st(rp + " << y * c.sub << ", a" << (r - r0) << "_" << y << " ^ r" << y << ");\n";
+                os << "      lh_st(rp + " << y << " * lh_sub, a" << (r - r0) << "_" << y << " ^ r" << y << ");\n";
             os << "    }\n  }\n";
         }
     } else if (c.ptr) {
         for (int r = r0; r < r1; ++r) {
             os << "  {\n    unsigned char *op = lh_pp(otl, " << r << ") + loff;\n";
             for (int y = 0; y < 8; ++y)
-                os << "    lh_st(op + " << y * c.sub << ", a" << (r - r0) << "_" << y << ");\n";
+                os << "    lh_st(op + " << y << " * lh_sub, a" << (r - r0) << "_" << y << ");\n";
             os << "  }\n";
         }
     } else {
         for (int r = r0; r < r1; ++r)
             for (int y = 0; y < 8; ++y)
-                os << "  lh_st(o + " << (long long)r * c.bytes + y * c.sub << "LL, a" << (r - r0) << "_" << y << ");\n";
+                os << "  lh_st(o + (long long)" << r << " * lh_bytes + " << y << " * lh_sub, a" << (r - r0) << "_" << y << ");\n";
     }
     os << "}\n";
 }
@@ -314,23 +315,24 @@ static void emit_win_group(std::ostream &os, const JitConfig &c, const std::vect
 // from the stripe's plan held in VGPR lanes and read with v_readlane).
 // V_r is written back in place of R_r; phase B is lh_inverse_gt_kernel (kernels.hip).
 static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::vector<uint8_t> &G) {
-    const int R = c.rows_per_wave, NG = (c.m + R - 1) / R, CPS = c.sub / (64 * c.W);
+    const int R = c.rows_per_wave, NG = (c.m + R - 1) / R;
     const int e_max = std::min(c.k, c.m), km = c.k + c.m;
     os << "#define LH_NQ " << (km + 63) / 64 << "\n"
        << "__device__ __forceinline__ const unsigned char *lh_slot(const unsigned int (&slv)[LH_NQ], const int i,\n"
-       << "    const unsigned char *base, const unsigned char *zero) {\n"
+       << "    const unsigned char *base, const unsigned char *zero, const int bytes) {\n"
        << "  const unsigned int s = (unsigned int)__builtin_amdgcn_readlane((int)slv[i / 64], i % 64);\n"
-       << "  return s == 0xFFu ? zero : base + (long long)s * " << c.bytes << ";\n}\n";
+       << "  return s == 0xFFu ? zero : base + (long long)s * bytes;\n}\n";
     for (int g = 0; g < NG; ++g) emit_win_group(os, c, G, g);
     if (c.ptr) {
         // blocks: the pointer table, k slot pointers per stripe (row stride `stride` bytes)
         os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
            << "lh_jit_decode_wide(unsigned char *__restrict__ blocks, long long stride,\n"
            << "                   const unsigned char *__restrict__ plan, long long plan_stride,\n"
-           << "                   const unsigned char *__restrict__ zero_page, int stripes) {\n"
+           << "                   const unsigned char *__restrict__ zero_page, int stripes, int bytes) {\n"
            << "  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
+           << "  const int lh_sub = bytes >> 3, lh_cps = lh_sub / " << 64 * c.W << ";  // (the block size: an argument)\n"
            << "  const int lane = threadIdx.x & 63;\n"
-           << "  const long long stripe = blockIdx.x / " << CPS << ";\n"
+           << "  const long long stripe = blockIdx.x / lh_cps;\n"
            << "  if (stripe >= stripes) return;\n"
            << "  const unsigned char *pl = plan + stripe * plan_stride;\n"
            << "  if (pl[0] == 0) return;  // workgroup-uniform\n"
@@ -343,20 +345,21 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
            << "  unsigned long long cpl[LH_NQ];\n"
            << "#pragma unroll\n  for (int q = 0; q < LH_NQ; ++q)\n"
            << "    cpl[q] = slv[q] == 0xFFu ? (unsigned long long)zero_page : tab[slv[q]];\n"
-           << "  const int coff = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << ";\n";
+           << "  const int coff = (int)(blockIdx.x % lh_cps) * " << 64 * c.W << ";\n";
         for (int g = 0; g < NG; ++g)
             os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << "(cpl, slv, pl, coff, coff + lane * "
-               << c.W << ");\n";
+               << c.W << ", bytes, lh_sub);\n";
         os << "}\n";
         return;
     }
     os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
        << "lh_jit_decode_wide(unsigned char *__restrict__ blocks, long long stride,\n"
        << "                   const unsigned char *__restrict__ plan, long long plan_stride,\n"
-       << "                   const unsigned char *__restrict__ zero_page, int stripes) {\n";
+       << "                   const unsigned char *__restrict__ zero_page, int stripes, int bytes) {\n";
     os << "  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
+       << "  const int lh_sub = bytes >> 3, lh_cps = lh_sub / " << 64 * c.W << ";  // (the block size: an argument)\n"
        << "  const int lane = threadIdx.x & 63;\n"
-       << "  const long long stripe = blockIdx.x / " << CPS << ";\n"
+       << "  const long long stripe = blockIdx.x / lh_cps;\n"
        << "  if (stripe >= stripes) return;\n"
        << "  const unsigned char *pl = plan + stripe * plan_stride;\n"
        << "  if (pl[0] == 0) return;  // workgroup-uniform\n"
@@ -365,11 +368,11 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
        << "    const int i = q * 64 + lane;\n"
        << "    slv[q] = i < " << km << " ? (unsigned int)pl[" << 16 + e_max << " + i] : 0xFFu;\n"
        << "  }\n"
-       << "  const int chunk = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << ";\n"
+       << "  const int chunk = (int)(blockIdx.x % lh_cps) * " << 64 * c.W << ";\n"
        << "  unsigned char *b = blocks + stripe * stride + chunk + lane * " << c.W << ";\n";
     os << "  const unsigned char *sb = blocks + stripe * stride + chunk;\n"
        << "  const unsigned char *zb = zero_page + chunk;\n";
-    const std::string dargs = "(b, slv, pl, sb, zb)";
+    const std::string dargs = "(b, slv, pl, sb, zb, bytes, lh_sub)";
     for (int g = 0; g < NG; ++g) os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << dargs << ";\n";
     os << "}\n";
 }
@@ -377,9 +380,9 @@ static void emit_wide_decode(std::ostream &os, const JitConfig &c, const std::ve
 static std::string win_source_for(const JitConfig &c) {
     std::ostringstream os;
     const std::vector<uint8_t> G = generator_matrix(c.k, c.m);
-    const int R = c.rows_per_wave, NG = (c.m + R - 1) / R, CPS = c.sub / (64 * c.W);
+    const int R = c.rows_per_wave, NG = (c.m + R - 1) / R;
     os << "// longhair_amd windowed " << (c.win == 2 ? "decode" : "encode") << ", k=" << c.k << " m=" << c.m
-       << " bytes=" << c.bytes << "\n"
+       << " (block size: a kernel argument; one module serves every size with sub % " << 64 * c.W << " == 0)\n"
        << "#ifndef LH_NT\n#define LH_NT 1\n#endif\n"
        << "__device__ __forceinline__ unsigned int lh_ld(const unsigned char *p) {\n"
        << "#if LH_NT\n  return __builtin_nontemporal_load((const unsigned int *)p);\n#else\n"
@@ -440,33 +443,35 @@ static std::string win_source_for(const JitConfig &c) {
         // in / out: the pointer tables (k data, m recovery block pointers per stripe)
         os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
            << "lh_jit_encode_win(const unsigned char *__restrict__ in, long long in_stride,\n"
-           << "                  unsigned char *__restrict__ out, long long out_stride, int stripes) {\n"
+           << "                  unsigned char *__restrict__ out, long long out_stride, int stripes, int bytes) {\n"
            << "  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
-           << "  const long long stripe = blockIdx.x / " << CPS << ";\n"
+           << "  const int lh_sub = bytes >> 3, lh_cps = lh_sub / " << 64 * c.W << ";  // (the block size: an argument)\n"
+           << "  const long long stripe = blockIdx.x / lh_cps;\n"
            << "  if (stripe >= stripes) return;\n"
            << "  unsigned long long ptl[LH_NP], otl[LH_NPO];\n"
            << "  lh_ptab_lanes(ptl, (const unsigned long long *)(in + stripe * in_stride), " << c.k << ");\n"
            << "  lh_ptab_lanes(otl, (const unsigned long long *)(out + stripe * out_stride), " << c.m << ");\n"
-           << "  const int coff = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << ";\n";
+           << "  const int coff = (int)(blockIdx.x % lh_cps) * " << 64 * c.W << ";\n";
         for (int g = 0; g < NG; ++g)
             os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << "(ptl, otl, coff, coff + (int)(threadIdx.x & 63) * "
-               << c.W << ");\n";
+               << c.W << ", bytes, lh_sub);\n";
         os << "}\n";
         return os.str();
     }
     os << "extern \"C\" __global__ void __launch_bounds__(" << 64 * NG << ")\n"
        << "lh_jit_encode_win(const unsigned char *__restrict__ in, long long in_stride,\n"
-       << "                  unsigned char *__restrict__ out, long long out_stride, int stripes) {\n"
+       << "                  unsigned char *__restrict__ out, long long out_stride, int stripes, int bytes) {\n"
        << "  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
-       << "  const long long stripe = blockIdx.x / " << CPS << ";\n"
+       << "  const int lh_sub = bytes >> 3, lh_cps = lh_sub / " << 64 * c.W << ";  // (the block size: an argument)\n"
+       << "  const long long stripe = blockIdx.x / lh_cps;\n"
        << "  if (stripe >= stripes) return;\n"
-       << "  const int p = (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W << " + (int)(threadIdx.x & 63) * "
+       << "  const int p = (int)(blockIdx.x % lh_cps) * " << 64 * c.W << " + (int)(threadIdx.x & 63) * "
        << c.W << ";\n"
        << "  const unsigned char *b = in + stripe * in_stride + p;\n"
        << "  unsigned char *o = out + stripe * out_stride + p;\n";
-    os << "  const unsigned char *sb = in + stripe * in_stride + (int)(blockIdx.x % " << CPS << ") * " << 64 * c.W
+    os << "  const unsigned char *sb = in + stripe * in_stride + (int)(blockIdx.x % lh_cps) * " << 64 * c.W
        << ";\n";
-    const char *eargs = "(b, o, sb, nullptr)";
+    const char *eargs = "(b, o, sb, nullptr, bytes, lh_sub)";
     for (int g = 0; g < NG; ++g) os << "  " << (g ? "else " : "") << "if (g == " << g << ") lh_wg" << g << eargs << ";\n";
     os << "}\n";
     return os.str();
@@ -532,7 +537,8 @@ std::string jit_source_for(const JitConfig &c) {
 }
 
 JitCache::Key JitCache::key_of(const JitConfig &cfg) {
-    return Key(cfg.k, cfg.m, cfg.bytes, cfg.W, cfg.defines,
+    // (windowed modules take the block size as an argument: one per (k, m, W, ...))
+    return Key(cfg.k, cfg.m, cfg.win ? 0 : cfg.bytes, cfg.W, cfg.defines,
                cfg.lds * 1000000000 + cfg.ptr * 100000000 + (cfg.role + 3 * cfg.plain) * 10000000 +
                    cfg.win_split * 1000000 + cfg.win * 100000 + cfg.win_lds * 10000 +
                    cfg.rows_per_wave * 100 + cfg.win_pf);
