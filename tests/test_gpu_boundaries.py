@@ -332,6 +332,54 @@ def test_capture_never_allocates(lh):
     assert torch.equal(blocks, data) and torch.equal(rows[0].cpu(), torch.arange(k, dtype=torch.uint8))
 
 
+@pytest.mark.parametrize("off,pad", [(1, 0), (8, 0), (4, 12), (0, 2), (3, 5)])
+def test_misaligned_batch_buffers(lh, oracle, off, pad):
+    """The batch calls take any base address and stripe stride: the data, the recovery
+    blocks and the decode buffer at odd offsets and strides (the LDS-staged k29/m4 kernels'
+    DMAs then start off 16-byte boundaries); every stripe against the oracle, the bytes
+    around the blocks untouched."""
+    import torch
+    k, m, nbytes, stripes = 29, 4, 1296, 50
+    stride = k * nbytes + pad
+    data = lhutil.fill(off * 7 + pad, stripes * k * nbytes).reshape(stripes, k, nbytes)
+    xb = torch.full((off + stride * stripes + 64,), 0x5A, dtype=torch.uint8, device="cuda")
+    X = xb[off:].as_strided((stripes, k, nbytes), (stride, nbytes, 1))
+    X.copy_(_gpu(data))
+    rb = torch.full((off + (m * nbytes + pad) * stripes + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    R = rb[off:].as_strided((stripes, m, nbytes), (m * nbytes + pad, nbytes, 1))
+    lh.encode_batch(X, m, recovery=R)
+    torch.cuda.synchronize()
+    rec = R.cpu().numpy()
+    for s in range(stripes):
+        rc, exp = oracle.encode(k, m, data[s], nbytes)
+        assert rc == 0 and rec[s].tobytes() == exp.tobytes(), s
+    # decode in place from a misaligned buffer
+    scen = _scenarios(k, m, stripes, off * 31 + pad)
+    db = torch.full((off + stride * stripes + 64,), 0x3C, dtype=torch.uint8, device="cuda")
+    D = db[off:].as_strided((stripes, k, nbytes), (stride, nbytes, 1))
+    blocks = np.empty_like(data)
+    rows = np.empty((stripes, k), dtype=np.uint8)
+    for s, (slots, rws) in enumerate(scen):
+        for i, (kind, x) in enumerate(slots):
+            blocks[s, i] = data[s, x] if kind == "d" else rec[s, x]
+        rows[s] = rws
+    D.copy_(_gpu(blocks))
+    d_rows = _gpu(rows)
+    lh.decode_batch(D, d_rows, m)
+    torch.cuda.synchronize()
+    got, got_rows = D.cpu().numpy(), d_rows.cpu().numpy()
+    for s in range(stripes):
+        bufs = [blocks[s, i].copy() for i in range(k)]
+        rc, exp_rows = oracle.decode(k, m, bufs, list(rows[s]), nbytes)
+        assert list(got_rows[s]) == exp_rows, s
+        assert all(got[s, i].tobytes() == bufs[i].tobytes() for i in range(k)), s
+    raw = db.cpu().numpy()
+    assert (raw[:off] == 0x3C).all() and (raw[off + stride * stripes:] == 0x3C).all()
+    if pad:
+        body = raw[off:off + stride * stripes].reshape(stripes, stride)
+        assert (body[:, k * nbytes:] == 0x3C).all()
+
+
 @pytest.mark.parametrize("align", [128, 64])
 def test_aligned_decode_buffer(lh, oracle, align):
     """bench.py's aligned decode buffer (a padded stripe stride and an offset that put every
