@@ -197,44 +197,14 @@ __global__ void __launch_bounds__(256, LB) enc_pat(const uint8_t *__restrict__ i
     for (int y = 0; y < 8; ++y) gstore_nt<W>(o + r * BYTES + y * SUB, acc[HEAVY ? r : 0][y] ^ T{(uint32_t)r});
 }
 
-// ---------------------------------------------------------------- enc, aligned loads
-// 8-byte lanes, 21 per stripe, 3 stripes per wave, lane c owns sub-block bytes [8c, 8c + 8)
-// (lane 20: 160..167, only 160..161 valid).  MODE 1: a fake layout with 168-byte sub-blocks
-// (every load and store 8-byte aligned: the pure cost of misalignment).  MODE 2: the real
-// layout, each sub-block loaded from its 8-byte-aligned floor, the lane's bytes assembled
-// from its own word and the next lane's (DPP wave_shl:1 + v_alignbyte; shift 2b mod 8 is a
-// constant per sub-block), outputs stored 2-byte aligned as the kernel does, lane 20's
-// 8 bytes moved back to 154..161 with lane 19's (wave_shr:1 + v_alignbyte).
-__device__ __forceinline__ uint32_t dpp_next(uint32_t v) {  // lane i <- lane i + 1
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
-}
-__device__ __forceinline__ uint32_t dpp_prev(uint32_t v) {  // lane i <- lane i - 1
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
-}
-template <int B>
-__device__ __forceinline__ u32x2 realign(u32x2 w) {
-  constexpr int S = (2 * B) % 8;
-  if constexpr (S == 0) return w;
-  else if constexpr (S == 4) return u32x2{w.y, dpp_next(w.x)};
-  else if constexpr (S < 4) {
-    const uint32_t n0 = dpp_next(w.x);
-    return u32x2{__builtin_amdgcn_alignbyte(w.y, w.x, S), __builtin_amdgcn_alignbyte(n0, w.y, S)};
-  } else {
-    const uint32_t n0 = dpp_next(w.x), n1 = dpp_next(w.y);
-    return u32x2{__builtin_amdgcn_alignbyte(n0, w.y, S - 4), __builtin_amdgcn_alignbyte(n1, n0, S - 4)};
-  }
-}
-template <int B, int MODE>
-__device__ __forceinline__ u32x2 aload(__amdgpu_buffer_rsrc_t rs, int lbase, int soff) {
-  constexpr int SB = MODE == 1 ? 168 : SUB;
-  constexpr int S = MODE == 1 ? 0 : (2 * B) % 8;  // MODE 3: loads as MODE 2
-  const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(rs, lbase + B * SB - S, soff, 2);
-  if constexpr (MODE == 1) return w;
-  else return realign<B>(w);
-}
-template <int MODE, int PF>
+// ---------------------------------------------------------------- enc, aligned layout
+// 8-byte lanes, 21 per stripe, 3 stripes per wave, lane c owns sub-block bytes [8c, 8c + 8).
+// A fake layout with 168-byte sub-blocks: every load and store is 8-byte aligned, so the time
+// against enc_pat is the pure cost of the real layout's 2-byte alignment.  (A DPP-realign
+// variant of the real layout was removed in round 5: it wrote wrong bytes.)
+template <int PF>
 __global__ void __launch_bounds__(256) enc_al(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, int stripes) {
-  constexpr int NCH = 21, SPW = 3, SB = MODE == 1 ? 168 : SUB, BY = 8 * SB;
+  constexpr int NCH = 21, SPW = 3, SB = 168, BY = 8 * SB;
   const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63, sl = min(lane / NCH, SPW - 1), c = lane - (lane / NCH) * NCH;
   const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)wave) * SPW;
@@ -250,10 +220,8 @@ __global__ void __launch_bounds__(256) enc_al(const uint8_t *__restrict__ in, ui
     for (int y = 0; y < 8; ++y) acc[r][y] = u32x2{0, 0};
   u32x2 ring[PF][8];
   auto col = [&](int x, u32x2 (&d)[8]) {
-    d[0] = aload<0, MODE>(rs, lbase, x * BY); d[1] = aload<1, MODE>(rs, lbase, x * BY);
-    d[2] = aload<2, MODE>(rs, lbase, x * BY); d[3] = aload<3, MODE>(rs, lbase, x * BY);
-    d[4] = aload<4, MODE>(rs, lbase, x * BY); d[5] = aload<5, MODE>(rs, lbase, x * BY);
-    d[6] = aload<6, MODE>(rs, lbase, x * BY); d[7] = aload<7, MODE>(rs, lbase, x * BY);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) d[b] = __builtin_amdgcn_raw_buffer_load_b64(rs, lbase + b * SB, x * BY, 2);
   };
 #pragma unroll
   for (int q = 0; q < PF; ++q) col(q, ring[q]);
@@ -274,22 +242,12 @@ __global__ void __launch_bounds__(256) enc_al(const uint8_t *__restrict__ in, ui
       for (int b = 0; b < 8; ++b) ring[x % PF][b] = nxt[b];
   }
   if (lane >= SPW * NCH || s0 + sl >= stripes) return;
-  constexpr int OSB = MODE == 3 ? 168 : SB;  // MODE 3: outputs in 168-byte (aligned) sub-blocks
-  uint8_t *o = out + (s0 + sl) * (long long)(M * 8 * OSB);
+  uint8_t *o = out + (s0 + sl) * (long long)(M * 8 * SB);
 #pragma unroll
   for (int r = 0; r < M; ++r)
 #pragma unroll
-    for (int y = 0; y < 8; ++y) {
-      u32x2 v = acc[r][y] ^ u32x2{(uint32_t)r, 0};
-      int p = 8 * c;
-      if (MODE == 2) {  // lane 20: bytes 154..161 from lane 19's 152..159 and its own 160..161
-        const uint32_t l0 = dpp_prev(v.x), l1 = dpp_prev(v.y);
-        const u32x2 w = u32x2{__builtin_amdgcn_alignbyte(l1, l0, 2), __builtin_amdgcn_alignbyte(v.x, l1, 2)};
-        v = c == NCH - 1 ? w : v;
-        p = c == NCH - 1 ? SUB - 8 : p;
-      }
-      __builtin_nontemporal_store(v, (u32x2 *)(o + r * 8 * OSB + y * OSB + p));
-    }
+    for (int y = 0; y < 8; ++y)
+      __builtin_nontemporal_store(acc[r][y] ^ u32x2{(uint32_t)r, 0}, (u32x2 *)(o + r * 8 * SB + y * SB + 8 * c));
 }
 
 // ---------------------------------------------------------------- lds (DMA-staged columns)
@@ -483,36 +441,13 @@ int main(int argc, char **argv) {
     ENC(8, 3, false, 2, 1) ENC(8, 3, true, 2, 1) ENC(8, 2, true, 2, 1) ENC(8, 3, false, 0, 1)
     ENC(16, 1, false, 2, 1) ENC(16, 2, false, 2, 1) ENC(16, 3, false, 2, 1) ENC(16, 2, false, 0, 1)
     ENC(16, 1, true, 2, 1) ENC(16, 2, true, 2, 1) ENC(16, 1, true, 2, 2) ENC(16, 1, true, 0, 2) ENC(16, 1, true, 2, 3)
-    const int ga = (int)((STRIPES + 2) / 3 + 3) / 4;
-    // MODE 1 reads a 65536 x 29 x 1344-byte layout: fits the input allocation (2.55 < 2.46 + ...? no) -> fewer stripes
+    // the fake layout's stripes are larger (29 x 1344 B): as many as fit the same input bytes, time scaled to 65536
     {
       const int st1 = (int)(IN_BYTES / (K * 8 * 168));  // stripes of the fake layout in the same bytes
       const int g1 = (int)((st1 + 2) / 3 + 3) / 4;
-      const float ms = timeit([&] { enc_al<1, 3><<<g1, 256>>>(din, dout, st1); });
+      const float ms = timeit([&] { enc_al<3><<<g1, 256>>>(din, dout, st1); });
       printf("%-34s %8.4f ms %8.1f GB/s input (fake 168-B sub-blocks, %d stripes, scaled to 65536: %.4f ms)\n",
              "enc aligned-layout PF=3", ms, IN_BYTES / (ms * 1e-3) / 1e9, st1, ms * 65536.0 / st1);
-    }
-    rep("enc dpp-realign PF=3", timeit([&] { enc_al<2, 3><<<ga, 256>>>(din, dout, (int)STRIPES); }));
-    rep("enc dpp-realign PF=2", timeit([&] { enc_al<2, 2><<<ga, 256>>>(din, dout, (int)STRIPES); }));
-    rep("enc dpp-realign, aligned stores", timeit([&] { enc_al<3, 3><<<ga, 256>>>(din, dout, (int)STRIPES); }));
-    {  // the realigned loads must give the misaligned kernel's bytes
-      const size_t ob = (size_t)OUT_BYTES;
-      std::vector<uint8_t> h1(ob), h2(ob);
-      for (long long i = 0; i < IN_BYTES; i += 1 << 20)
-        CK(hipMemset(din + i, (int)((i >> 20) * 2654435761u >> 24), std::min<long long>(1 << 20, IN_BYTES - i)));
-      std::vector<uint8_t> rnd(1 << 20);
-      for (size_t i = 0; i < rnd.size(); ++i) rnd[i] = (uint8_t)((i * 2654435761u) >> 13);
-      for (long long i = 0; i < IN_BYTES; i += 1 << 20)
-        CK(hipMemcpy(din + i, rnd.data(), std::min<long long>(1 << 20, IN_BYTES - i), hipMemcpyHostToDevice));
-      CK(hipMemset(dout, 0, ob));
-      enc_pat<8, 3, true, 2, 1><<<(int)((STRIPES + 2) / 3 + 3) / 4, 256>>>(din, dout, (int)STRIPES);
-      CK(hipMemcpy(h1.data(), dout, ob, hipMemcpyDeviceToHost));
-      CK(hipMemset(dout, 0, ob));
-      enc_al<2, 3><<<ga, 256>>>(din, dout, (int)STRIPES);
-      CK(hipMemcpy(h2.data(), dout, ob, hipMemcpyDeviceToHost));
-      size_t bad = 0;
-      for (size_t i = 0; i < ob; ++i) bad += h1[i] != h2[i];
-      printf("enc dpp-realign bytes vs misaligned loads: %zu of %zu differ\n", bad, ob);
     }
   }
   if (want(argc, argv, "lds")) {
