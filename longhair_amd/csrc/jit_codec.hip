@@ -1417,22 +1417,44 @@ struct lh_dldsrc {
                 sv[q] == 0xFFu ? (int)0x80000000 : joff[q] + (int)sv[q] * LH_BYTES, 0, 0, LH_LDS_NT_DEC ? 2 : 0);
     }
 };
+// LH_LDG: the ring refilled LH_LDG slots at a time (after every LH_LDG-th column) instead of
+// one slot per column, each refill reading the slot maps it needs then: k29/m4 decode 0.577
+// -> 0.559 ms (profiles/r7a_tune_k29m4_ldg.txt; 2 and 3 alike, the encode unchanged).
+#ifndef LH_LDG
+#define LH_LDG (LH_LD > 2 ? 2 : 1)
+#endif
+#if LH_LDG < 1 || LH_LDG >= LH_LD
+#error "LH_LDG: 1 <= LH_LDG < LH_LD"
+#endif
+template <int C, int N>  // columns C .. C + N - 1 (those that exist) into their slots
+__device__ __forceinline__ void lh_dissue(const lh_dldsrc &S) {
+    if constexpr (N > 0 && C < LH_DCOLS) {
+        unsigned sv[LH_LQ];
+        S.slots<C>(sv);
+        S.issue(sv, C % LH_LD);
+        lh_dissue<C + 1, N - 1>(S);
+    }
+}
 template <int X>
 struct lh_unroll_decode_lds {
     __device__ __forceinline__ static void run(lh_word (&v)[LH_M][8], const lh_dldsrc &S, int lo, int lo8) {
         if constexpr (X < LH_DCOLS) {
-            constexpr int ahead = (LH_LD - 1) < (LH_DCOLS - 1 - X) ? (LH_LD - 1) : (LH_DCOLS - 1 - X);
+            constexpr int issued = (LH_LD + LH_LDG * (X / LH_LDG)) < LH_DCOLS ? (LH_LD + LH_LDG * (X / LH_LDG)) : LH_DCOLS;
+            constexpr int ahead = issued - 1 - X;
             unsigned sv[LH_LQ];
-            if constexpr (X + LH_LD < LH_DCOLS) S.slots<(X + LH_LD < LH_DCOLS ? X + LH_LD : 0)>(sv);
+            if constexpr (LH_LDG == 1 && X + LH_LD < LH_DCOLS) S.slots<(X + LH_LD < LH_DCOLS ? X + LH_LD : 0)>(sv);
             lh_wait_vmcnt<LH_LQ * ahead>();
             asm volatile("" ::: "memory");  // no LDS read moves above the wait
             lh_word d[8];
             lh_slot_col(d, S.ring + (X % LH_LD) * (LH_LQ * 1024), lo, lo8);
             lh_dcombine<X, LH_LDS_REC_FIRST>(v, d);
             lh_dopaque(v);
-            if constexpr (X + LH_LD < LH_DCOLS) {
+            if constexpr (LH_LDG == 1 && X + LH_LD < LH_DCOLS) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done
                 S.issue(sv, X % LH_LD);
+            } else if constexpr (LH_LDG > 1 && (X + 1) % LH_LDG == 0 && LH_LD + X + 1 - LH_LDG < LH_DCOLS) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slots' reads are done
+                lh_dissue<LH_LD + X + 1 - LH_LDG, LH_LDG>(S);
             }
             lh_unroll_decode_lds<X + 1>::run(v, S, lo, lo8);
         }
