@@ -456,8 +456,8 @@ struct lh_unroll_encode<LH_K> {
 #define LH_LDS 0
 #endif
 #if LH_LDS
-#if LH_W != 8 || LH_NCH > 64 || LH_BYTES % 16 != 0 || LH_BUF == 0
-#error "LH_LDS: 8-byte lanes, whole stripes per wave, 16-byte-multiple blocks, strided batches"
+#if LH_W != 8 || LH_NCH > 64 || LH_BYTES % 16 != 0 || (LH_BUF == 0 && !LH_PTR)
+#error "LH_LDS: 8-byte lanes, whole stripes per wave, 16-byte-multiple blocks, strided or pointer-table batches"
 #endif
 #ifndef LH_LD
 #define LH_LD 4  // ring slots per wave (columns in flight + the one being read)
@@ -538,15 +538,32 @@ __device__ __forceinline__ void lh_lds_put(unsigned char *p, const lh_word &w) {
 #ifndef LH_LDS_FLAT_ST
 #define LH_LDS_FLAT_ST (LH_SPW * LH_M * LH_BYTES <= LH_LDE * LH_LQ * 1024)
 #endif
+#if LH_PTR
+// Pointer-table batches: each wave copies its stripes' rows (LH_K data then LH_M recovery
+// block pointers) into LDS; a DMA lane reads its chunk's block pointer for column x there.
+#define LH_LPR (LH_K + LH_M)
+#endif
 struct lh_ldsrc {
+#if LH_PTR
+    const unsigned long long *pt;  // LDS: the wave's pointer rows [stripe][LH_LPR]
+    int pr[LH_LQ];                 // DMA chunk q: its stripe's row in pt
+    int off[LH_LQ];                // ... its offset in the block
+#else
     const unsigned char *src[LH_LQ];  // this lane's chunk of DMA instruction q, column 0
+#endif
     unsigned char *ring;              // this wave's LH_LDE slots of LH_LQ KiB
     __device__ __forceinline__ void issue(int x, int slot) const {
 #pragma unroll
-        for (int q = 0; q < LH_LQ; ++q)
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src[q] + (long long)x * LH_BYTES),
+        for (int q = 0; q < LH_LQ; ++q) {
+#if LH_PTR
+            const unsigned char *a = (const unsigned char *)pt[pr[q] + x] + off[q];
+#else
+            const unsigned char *a = src[q] + (long long)x * LH_BYTES;
+#endif
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)a,
                                              (__attribute__((address_space(3))) void *)(ring + slot * (LH_LQ * 1024) + q * 1024),
                                              16, 0, LH_NT ? 2 : 0);
+        }
     }
 };
 // s_waitcnt vmcnt(N) (gfx9 encoding, expcnt / lgkmcnt left at their maxima); N a constant.
@@ -605,12 +622,33 @@ __device__ __forceinline__ void lh_encode_wave_lds(long long wave, const unsigne
     const int nst = (int)((stripes - s0) < LH_SPW ? (stripes - s0) : LH_SPW);
     lh_ldsrc S;
     S.ring = lh_lring[threadIdx.x >> 6];
+#if LH_PTR
+    // in / out: the data and recovery pointer tables (rows of LH_K / LH_M block pointers)
+    __shared__ unsigned long long lh_lpt[4][LH_SPW * LH_LPR];
+    unsigned long long *prow = lh_lpt[threadIdx.x >> 6];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous stripe group's reads
+    __builtin_amdgcn_wave_barrier();
+    if (sl < nst) {
+        const unsigned long long *it = (const unsigned long long *)(in + (s0 + sl) * in_stride);
+        const unsigned long long *ot = (const unsigned long long *)(out + (s0 + sl) * out_stride);
+        for (int x = c; x < LH_LPR; x += LH_NCH) prow[sl * LH_LPR + x] = x < LH_K ? it[x] : ot[x - LH_K];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    S.pt = prow;
+#endif
 #pragma unroll
     for (int q = 0; q < LH_LQ; ++q) {  // every lane moves chunks, whatever its own stripe
         int j = 64 * q + lane;
         if (j >= nst * (LH_BYTES / 16)) j = nst * (LH_BYTES / 16) - 1;  // (lands past the image)
         const int js = j / (LH_BYTES / 16);
+#if LH_PTR
+        S.pr[q] = js * LH_LPR;
+        S.off[q] = (j - js * (LH_BYTES / 16)) * 16;
+#else
         S.src[q] = in + (s0 + js) * in_stride + (j - js * (LH_BYTES / 16)) * 16;
+#endif
     }
 #pragma unroll
     for (int q = 0; q < LH_LDE; ++q)
@@ -651,7 +689,12 @@ __device__ __forceinline__ void lh_encode_wave_lds(long long wave, const unsigne
             if (j < n) {
                 const int js = j / per, t = j - js * per;
                 const lh_u32x4a v = *(const lh_u32x4a *)(S.ring + js * (LH_M * LH_BYTES) + t * 16);
+#if LH_PTR
+                const int r = t / (LH_BYTES / 16);
+                unsigned char *dst = (unsigned char *)S.pt[js * LH_LPR + LH_K + r] + (t - r * (LH_BYTES / 16)) * 16;
+#else
                 unsigned char *dst = out + (s0 + js) * out_stride + t * 16;
+#endif
 #if LH_NT_ST
                 __builtin_nontemporal_store(v, (lh_u32x4a *)dst);
 #else
@@ -663,9 +706,14 @@ __device__ __forceinline__ void lh_encode_wave_lds(long long wave, const unsigne
     return;
 #endif
     if (sl >= nst) return;
-    unsigned char *o = out + (s0 + sl) * out_stride + (last ? LH_SUB - 8 : 8 * c);
+    const int p = last ? LH_SUB - 8 : 8 * c;
 #pragma unroll
-    for (int r = 0; r < LH_M; ++r)
+    for (int r = 0; r < LH_M; ++r) {
+#if LH_PTR
+        unsigned char *o = (unsigned char *)S.pt[sl * LH_LPR + LH_K + r] + p;
+#else
+        unsigned char *o = out + (s0 + sl) * out_stride + (long long)r * LH_BYTES + p;
+#endif
 #pragma unroll
         for (int y = 0; y < 8; ++y) {
             lh_word w = acc[r][y];
@@ -674,8 +722,9 @@ __device__ __forceinline__ void lh_encode_wave_lds(long long wave, const unsigne
                 w.v[0] = last ? f.v[0] : w.v[0];
                 w.v[1] = last ? f.v[1] : w.v[1];
             }
-            lh_store(o + (long long)r * LH_BYTES + y * LH_SUB, w);
+            lh_store(o + y * LH_SUB, w);
         }
+    }
 }
 #endif
 
@@ -1368,7 +1417,7 @@ __device__ __forceinline__ void lh_fused_solve::operator()(lh_plan_regs &pr) con
     for (int q = 0; q < LH_NOUT; ++q) asm volatile("" : "+v"(pr.outw[q]));
 }
 
-#if LH_LDS
+#if LH_LDS && !LH_PTR
 // The fused decode with its columns staged like the encode's (LH_LDS = 1): the wave's
 // LH_SPW stripes of column X (stream order, lh_dcol) arrive as LH_LQ buffer_load_dwordx4
 // ... lds per column into the wave's ring, chunk j = 64 q + lane of the image
@@ -1563,7 +1612,7 @@ __device__ __forceinline__ void lh_fused_wave_lds(const lh_lane &l, long long wa
         }
     }
 }
-#endif  // LH_LDS
+#endif  // LH_LDS && !LH_PTR
 
 #ifndef LH_DEC_LB
 #define LH_DEC_LB 1  // min waves per SIMD the register allocator must allow (tools/tune.py)
@@ -1595,7 +1644,7 @@ __device__ __forceinline__ void lh_fused_body(unsigned char *__restrict__ blocks
         sv.glog = glog;
         unsigned int rowv[LH_NRW];
         lh_fused_rows(l, c, rows, rowv);
-#if LH_LDS
+#if LH_LDS && !LH_PTR
         (void)zero_page;
         const bool work = l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr);
         lh_fused_wave_lds(l, lh_w, c, sl, work, &scratch[wid][0][0], blocks, stripe_stride, stripes, sv, pr);
