@@ -109,12 +109,12 @@ bool jit_ptr_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     if (!jit_config_for(k, m, bytes, decode, cfg)) return false;
     if ((long long)(cfg->spw ? cfg->spw : 1) * k > 1024) return false;  // LDS: 4 waves x 8 B x spw x (k + 1) <= 35 KiB
     cfg->ptr = 1;
-    // LDS staging for the encode (its DMA lanes read their block pointers from the wave's
-    // pointer rows in LDS) when the ring plus those rows keep two workgroups per CU; the
-    // fused decode's staging addresses its columns through a buffer resource (strided only).
+    // LDS staging (the DMA lanes read their block pointers from the wave's pointer rows in
+    // LDS) when the ring plus those rows keep two workgroups per CU; for the fused decode
+    // (whose plan scratch shares the budget) when its rows take at most 4 KiB.
     const long long spw = cfg->spw ? cfg->spw : 1, lq = (spw * bytes + 1023) / 1024;
     const long long lds_bytes = 4 * (4 * lq * 1024 + 16) + 4 * spw * (k + m) * 8;
-    if (decode || lds_bytes > 80 * 1024) cfg->lds = 0;
+    if (lds_bytes > 80 * 1024 || (decode && 4 * spw * (k + 1) * 8 > 4096)) cfg->lds = 0;
     return true;
 }
 

@@ -552,18 +552,28 @@ struct lh_ldsrc {
     const unsigned char *src[LH_LQ];  // this lane's chunk of DMA instruction q, column 0
 #endif
     unsigned char *ring;              // this wave's LH_LDE slots of LH_LQ KiB
-    __device__ __forceinline__ void issue(int x, int slot) const {
+    // The lanes' source addresses of column x (LH_PTR: read from the pointer rows early, so
+    // the refill after a column does not wait on LDS).
+    __device__ __forceinline__ void addrs(int x, const unsigned char *(&a)[LH_LQ]) const {
 #pragma unroll
-        for (int q = 0; q < LH_LQ; ++q) {
+        for (int q = 0; q < LH_LQ; ++q)
 #if LH_PTR
-            const unsigned char *a = (const unsigned char *)pt[pr[q] + x] + off[q];
+            a[q] = (const unsigned char *)pt[pr[q] + x] + off[q];
 #else
-            const unsigned char *a = src[q] + (long long)x * LH_BYTES;
+            a[q] = src[q] + (long long)x * LH_BYTES;
 #endif
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)a,
+    }
+    __device__ __forceinline__ void issue(const unsigned char *const (&a)[LH_LQ], int slot) const {
+#pragma unroll
+        for (int q = 0; q < LH_LQ; ++q)
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)a[q],
                                              (__attribute__((address_space(3))) void *)(ring + slot * (LH_LQ * 1024) + q * 1024),
                                              16, 0, LH_NT ? 2 : 0);
-        }
+    }
+    __device__ __forceinline__ void issue(int x, int slot) const {
+        const unsigned char *a[LH_LQ];
+        addrs(x, a);
+        issue(a, slot);
     }
 };
 // s_waitcnt vmcnt(N) (gfx9 encoding, expcnt / lgkmcnt left at their maxima); N a constant.
@@ -577,6 +587,8 @@ struct lh_unroll_encode_lds {
         if constexpr (X < LH_K) {
             // this column's DMAs landed: all but those of the columns issued after it
             constexpr int ahead = (LH_LDE - 1) < (LH_K - 1 - X) ? (LH_LDE - 1) : (LH_K - 1 - X);
+            const unsigned char *a[LH_LQ];
+            if constexpr (LH_PTR && X + LH_LDE < LH_K) S.addrs(X + LH_LDE, a);
             lh_wait_vmcnt<LH_LQ * ahead>();
             asm volatile("" ::: "memory");  // no LDS read moves above the wait
             lh_word d[8];
@@ -585,7 +597,8 @@ struct lh_unroll_encode_lds {
             lh_opaque(acc);
             if constexpr (X + LH_LDE < LH_K) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done
-                S.issue(X + LH_LDE, X % LH_LDE);
+                if constexpr (LH_PTR) S.issue(a, X % LH_LDE);
+                else S.issue(X + LH_LDE, X % LH_LDE);
             }
             lh_unroll_encode_lds<X + 1>::run(acc, S, lo, lo8);
         }
@@ -1417,7 +1430,7 @@ __device__ __forceinline__ void lh_fused_solve::operator()(lh_plan_regs &pr) con
     for (int q = 0; q < LH_NOUT; ++q) asm volatile("" : "+v"(pr.outw[q]));
 }
 
-#if LH_LDS && !LH_PTR
+#if LH_LDS
 // The fused decode with its columns staged like the encode's (LH_LDS = 1): the wave's
 // LH_SPW stripes of column X (stream order, lh_dcol) arrive as LH_LQ buffer_load_dwordx4
 // ... lds per column into the wave's ring, chunk j = 64 q + lane of the image
@@ -1426,7 +1439,10 @@ __device__ __forceinline__ void lh_fused_solve::operator()(lh_plan_regs &pr) con
 // recovery row) or a stripe with nothing to do gets an out-of-range offset: zeros into the
 // ring, no memory request.  Compute lanes read their words as the encode's do and store
 // the recovered blocks as it stores recovery blocks (the last lane of a stripe funnels the
-// previous lane's word).
+// previous lane's word).  Pointer-table batches (LH_PTR): the wave's stripes' rows of block
+// pointers (slot order, the zero page at LH_K) copied into LDS, each DMA lane's address its
+// chunk's slot pointer from there, absent columns read from the zero page (L2-resident) --
+// flat global_load_lds, no buffer range to clip against.
 // Column order and cache policy of this form (profiles/r5i_tune_k29m4_lds_dec.txt, k29/m4:
 // 0.611 ms register ring; 0.588 staged, recovery rows first, default policy; 0.577 recovery
 // rows last with non-temporal loads -- the slots the outputs overwrite are then no longer
@@ -1445,8 +1461,14 @@ struct lh_dmoff {  // scratch offset of column X's slot byte
     static constexpr int v = D::rec ? LH_SR_REC + D::r : LH_SR_SRC + D::x;
 };
 struct lh_dldsrc {
+#if LH_PTR
+    const unsigned long long *pt;  // LDS: the wave's pointer rows [stripe][LH_K + 1]
+    int prow[LH_LQ];               // DMA chunk q: its stripe's row in pt
+    int joff[LH_LQ];               // ... its offset in the block
+#else
     __amdgpu_buffer_rsrc_t rs;
     int joff[LH_LQ];  // DMA chunk q: byte offset in the wave's stripes (block 0)
+#endif
     int jsc[LH_LQ];   // ... its stripe's scratch offset, or -1: nothing to do there
     const unsigned char *scr;  // the wave's scratch (LDS)
     unsigned char *ring;
@@ -1461,9 +1483,16 @@ struct lh_dldsrc {
     __device__ __forceinline__ void issue(const unsigned (&sv)[LH_LQ], int slot) const {
 #pragma unroll
         for (int q = 0; q < LH_LQ; ++q)
+#if LH_PTR
+            __builtin_amdgcn_global_load_lds(
+                (__attribute__((address_space(1))) void *)((const unsigned char *)pt[prow[q] + (sv[q] == 0xFFu ? LH_K : (int)sv[q])] + joff[q]),
+                (__attribute__((address_space(3))) void *)(ring + slot * (LH_LQ * 1024) + q * 1024), 16, 0,
+                LH_LDS_NT_DEC ? 2 : 0);
+#else
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                 rs, (__attribute__((address_space(3))) void *)(ring + slot * (LH_LQ * 1024) + q * 1024), 16,
                 sv[q] == 0xFFu ? (int)0x80000000 : joff[q] + (int)sv[q] * LH_BYTES, 0, 0, LH_LDS_NT_DEC ? 2 : 0);
+#endif
     }
 };
 // LH_LDG: the ring refilled LH_LDG slots at a time (after every LH_LDG-th column) instead of
@@ -1523,7 +1552,7 @@ __device__ __forceinline__ void lh_decode_lds_prologue(const lh_dldsrc &S) {
 __device__ __forceinline__ void lh_fused_wave_lds(const lh_lane &l, long long wave, int c, int sl, bool work,
                                                   const unsigned char *scr, unsigned char *__restrict__ blocks,
                                                   long long stripe_stride, int stripes, const lh_fused_solve &sv,
-                                                  lh_plan_regs &pr) {
+                                                  lh_plan_regs &pr, const unsigned char *zero_page) {
     __shared__ __attribute__((aligned(16))) unsigned char lh_dring[4][LH_LD * LH_LQ * 1024 + LH_LPAD];
     const int lane = threadIdx.x & 63;
     const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)wave) * LH_SPW;  // wave-uniform
@@ -1532,7 +1561,25 @@ __device__ __forceinline__ void lh_fused_wave_lds(const lh_lane &l, long long wa
     const unsigned long long wm = __ballot(work);
     if (wm == 0) return;  // wave-uniform
     lh_dldsrc S;
+#if LH_PTR
+    // blocks: the pointer table (rows of LH_K block pointers, stride stripe_stride bytes)
+    __shared__ unsigned long long lh_dpt[4][LH_SPW * (LH_K + 1)];
+    unsigned long long *prow = lh_dpt[threadIdx.x >> 6];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous stripe group's reads
+    __builtin_amdgcn_wave_barrier();
+    if (sl < nst) {
+        const unsigned long long *t = (const unsigned long long *)(blocks + (s0 + sl) * stripe_stride);
+        for (int x = c; x <= LH_K; x += LH_NCH)
+            prow[sl * (LH_K + 1) + x] = x < LH_K ? t[x] : (unsigned long long)zero_page;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    S.pt = prow;
+#else
+    (void)zero_page;
     S.rs = __builtin_amdgcn_make_buffer_rsrc(blocks + s0 * stripe_stride, 0, (int)(nst * stripe_stride), 0x00020000);
+#endif
     S.scr = scr;
     S.ring = lh_dring[threadIdx.x >> 6];
 #pragma unroll
@@ -1540,7 +1587,12 @@ __device__ __forceinline__ void lh_fused_wave_lds(const lh_lane &l, long long wa
         int j = 64 * q + lane;
         if (j >= nst * (LH_BYTES / 16)) j = nst * (LH_BYTES / 16) - 1;  // (lands past the image)
         const int js = j / (LH_BYTES / 16);
+#if LH_PTR
+        S.prow[q] = js * (LH_K + 1);
+        S.joff[q] = (j - js * (LH_BYTES / 16)) * 16;
+#else
         S.joff[q] = js * (int)stripe_stride + (j - js * (LH_BYTES / 16)) * 16;
+#endif
         S.jsc[q] = js * LH_SR | (((wm >> (js * LH_NCH)) & 1ull) ? 0 : (int)0x80000000);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous group's ring reads are done
@@ -1563,7 +1615,9 @@ __device__ __forceinline__ void lh_fused_wave_lds(const lh_lane &l, long long wa
     // profiles/r5l_tune_k29m4_flat_dec.txt, 0.604 against 0.574 ms.)
     const int e = pr.e;
     const bool last = l.last;
+#if !LH_PTR
     unsigned char *base = blocks + l.stripe * stripe_stride + (last ? LH_SUB - 8 : 8 * c);
+#endif
 #pragma unroll
     for (int i = 0; i < LH_EMAX; ++i) {
         if (i < e) {  // stripe-uniform: the funnel's source lane is active too
@@ -1598,7 +1652,11 @@ __device__ __forceinline__ void lh_fused_wave_lds(const lh_lane &l, long long wa
                 lh_pin8(o);
 #endif
             }
+#if LH_PTR
+            unsigned char *dst = (unsigned char *)S.pt[sl * (LH_K + 1) + LH_BYTE(pr.outw, i)] + (last ? LH_SUB - 8 : 8 * c);
+#else
             unsigned char *dst = base + (long long)LH_BYTE(pr.outw, i) * LH_BYTES;
+#endif
 #pragma unroll
             for (int y = 0; y < 8; ++y) {
                 lh_word w = o[y];
@@ -1612,7 +1670,7 @@ __device__ __forceinline__ void lh_fused_wave_lds(const lh_lane &l, long long wa
         }
     }
 }
-#endif  // LH_LDS && !LH_PTR
+#endif  // LH_LDS
 
 #ifndef LH_DEC_LB
 #define LH_DEC_LB 1  // min waves per SIMD the register allocator must allow (tools/tune.py)
@@ -1644,10 +1702,9 @@ __device__ __forceinline__ void lh_fused_body(unsigned char *__restrict__ blocks
         sv.glog = glog;
         unsigned int rowv[LH_NRW];
         lh_fused_rows(l, c, rows, rowv);
-#if LH_LDS && !LH_PTR
-        (void)zero_page;
+#if LH_LDS
         const bool work = l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr);
-        lh_fused_wave_lds(l, lh_w, c, sl, work, &scratch[wid][0][0], blocks, stripe_stride, stripes, sv, pr);
+        lh_fused_wave_lds(l, lh_w, c, sl, work, &scratch[wid][0][0], blocks, stripe_stride, stripes, sv, pr, zero_page);
 #else
         if (l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr))
             lh_decode_body<PF>(l, lh_w, blocks, stripe_stride, pr, zero_page, stripes, sv);
