@@ -92,6 +92,10 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
         if (sub - 8 * (nch2 - 1) != 8)
             for (int s = 0; s < spw; ++s) dpp_ok = dpp_ok && (s * nch2 + nch2 - 1) % 16 != 0;
         cfg->lds = dpp_ok ? 1 : 0;
+        // The encode's LDS also holds its stripes' block-pointer rows (spw x (k + m) x 8 bytes
+        // per wave): keep ring plus rows within two workgroups per CU.
+        const long long lq = ((long long)spw * bytes + 1023) / 1024;
+        if (!decode && 4 * (4 * lq * 1024 + 16) + 4ll * spw * (k + m) * 8 > 80 * 1024) cfg->lds = 0;
     }
     // One role per module: an encode module holds lh_jit_encode only, a decode module the one
     // decode kernel its calls launch (the fused plan for e_max <= 4, one stripe per <= 64
@@ -109,12 +113,11 @@ bool jit_ptr_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     if (!jit_config_for(k, m, bytes, decode, cfg)) return false;
     if ((long long)(cfg->spw ? cfg->spw : 1) * k > 1024) return false;  // LDS: 4 waves x 8 B x spw x (k + 1) <= 35 KiB
     cfg->ptr = 1;
-    // LDS staging (the DMA lanes read their block pointers from the wave's pointer rows in
-    // LDS) when the ring plus those rows keep two workgroups per CU; for the fused decode
-    // (whose plan scratch shares the budget) when its rows take at most 4 KiB.
-    const long long spw = cfg->spw ? cfg->spw : 1, lq = (spw * bytes + 1023) / 1024;
-    const long long lds_bytes = 4 * (4 * lq * 1024 + 16) + 4 * spw * (k + m) * 8;
-    if (lds_bytes > 80 * 1024 || (decode && 4 * spw * (k + 1) * 8 > 4096)) cfg->lds = 0;
+    // LDS staging as for strided batches (the encode's pointer rows already counted by
+    // jit_config_for); the fused decode's rows (its plan scratch shares the budget) at most
+    // 4 KiB.
+    const long long spw = cfg->spw ? cfg->spw : 1;
+    if (decode && 4 * spw * (k + 1) * 8 > 4096) cfg->lds = 0;
     return true;
 }
 

@@ -538,30 +538,23 @@ __device__ __forceinline__ void lh_lds_put(unsigned char *p, const lh_word &w) {
 #ifndef LH_LDS_FLAT_ST
 #define LH_LDS_FLAT_ST (LH_SPW * LH_M * LH_BYTES <= LH_LDE * LH_LQ * 1024)
 #endif
-#if LH_PTR
-// Pointer-table batches: each wave copies its stripes' rows (LH_K data then LH_M recovery
-// block pointers) into LDS; a DMA lane reads its chunk's block pointer for column x there.
+// Block pointers in LDS: each wave writes its stripes' rows (LH_K data then LH_M recovery
+// block addresses: from the pointer tables with LH_PTR, else computed from base and stride)
+// into LDS; a DMA lane's source for column x is its chunk's row entry plus the chunk's offset,
+// read before the column's wait, and the stores take their rows' entries.  For strided
+// batches too: k29/m4 encode 0.532 -> 0.502 ms against per-lane 64-bit source pointers
+// advanced by x * bytes (profiles/r7q_tune_k29m4_erows.txt; found because the pointer-table
+// form ran faster, r7n_seq_probe_ptr.txt; padding the ring to the same LDS size: no change).
 #define LH_LPR (LH_K + LH_M)
-#endif
 struct lh_ldsrc {
-#if LH_PTR
     const unsigned long long *pt;  // LDS: the wave's pointer rows [stripe][LH_LPR]
     int pr[LH_LQ];                 // DMA chunk q: its stripe's row in pt
     int off[LH_LQ];                // ... its offset in the block
-#else
-    const unsigned char *src[LH_LQ];  // this lane's chunk of DMA instruction q, column 0
-#endif
-    unsigned char *ring;              // this wave's LH_LDE slots of LH_LQ KiB
-    // The lanes' source addresses of column x (LH_PTR: read from the pointer rows early, so
-    // the refill after a column does not wait on LDS).
+    unsigned char *ring;           // this wave's LH_LDE slots of LH_LQ KiB
+    // The lanes' source addresses of column x.
     __device__ __forceinline__ void addrs(int x, const unsigned char *(&a)[LH_LQ]) const {
 #pragma unroll
-        for (int q = 0; q < LH_LQ; ++q)
-#if LH_PTR
-            a[q] = (const unsigned char *)pt[pr[q] + x] + off[q];
-#else
-            a[q] = src[q] + (long long)x * LH_BYTES;
-#endif
+        for (int q = 0; q < LH_LQ; ++q) a[q] = (const unsigned char *)pt[pr[q] + x] + off[q];
     }
     __device__ __forceinline__ void issue(const unsigned char *const (&a)[LH_LQ], int slot) const {
 #pragma unroll
@@ -588,7 +581,7 @@ struct lh_unroll_encode_lds {
             // this column's DMAs landed: all but those of the columns issued after it
             constexpr int ahead = (LH_LDE - 1) < (LH_K - 1 - X) ? (LH_LDE - 1) : (LH_K - 1 - X);
             const unsigned char *a[LH_LQ];
-            if constexpr (LH_PTR && X + LH_LDE < LH_K) S.addrs(X + LH_LDE, a);
+            if constexpr (X + LH_LDE < LH_K) S.addrs(X + LH_LDE, a);
             lh_wait_vmcnt<LH_LQ * ahead>();
             asm volatile("" ::: "memory");  // no LDS read moves above the wait
             lh_word d[8];
@@ -597,8 +590,7 @@ struct lh_unroll_encode_lds {
             lh_opaque(acc);
             if constexpr (X + LH_LDE < LH_K) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done
-                if constexpr (LH_PTR) S.issue(a, X % LH_LDE);
-                else S.issue(X + LH_LDE, X % LH_LDE);
+                S.issue(a, X % LH_LDE);
             }
             lh_unroll_encode_lds<X + 1>::run(acc, S, lo, lo8);
         }
@@ -635,33 +627,33 @@ __device__ __forceinline__ void lh_encode_wave_lds(long long wave, const unsigne
     const int nst = (int)((stripes - s0) < LH_SPW ? (stripes - s0) : LH_SPW);
     lh_ldsrc S;
     S.ring = lh_lring[threadIdx.x >> 6];
-#if LH_PTR
-    // in / out: the data and recovery pointer tables (rows of LH_K / LH_M block pointers)
+    // LH_PTR: in / out are the data and recovery pointer tables (rows of LH_K / LH_M pointers)
     __shared__ unsigned long long lh_lpt[4][LH_SPW * LH_LPR];
     unsigned long long *prow = lh_lpt[threadIdx.x >> 6];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous stripe group's reads
     __builtin_amdgcn_wave_barrier();
     if (sl < nst) {
+#if LH_PTR
         const unsigned long long *it = (const unsigned long long *)(in + (s0 + sl) * in_stride);
         const unsigned long long *ot = (const unsigned long long *)(out + (s0 + sl) * out_stride);
         for (int x = c; x < LH_LPR; x += LH_NCH) prow[sl * LH_LPR + x] = x < LH_K ? it[x] : ot[x - LH_K];
+#else
+        for (int x = c; x < LH_LPR; x += LH_NCH)
+            prow[sl * LH_LPR + x] = x < LH_K ? (unsigned long long)(in + (s0 + sl) * in_stride + (long long)x * LH_BYTES)
+                                             : (unsigned long long)(out + (s0 + sl) * out_stride + (long long)(x - LH_K) * LH_BYTES);
+#endif
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     S.pt = prow;
-#endif
 #pragma unroll
     for (int q = 0; q < LH_LQ; ++q) {  // every lane moves chunks, whatever its own stripe
         int j = 64 * q + lane;
         if (j >= nst * (LH_BYTES / 16)) j = nst * (LH_BYTES / 16) - 1;  // (lands past the image)
         const int js = j / (LH_BYTES / 16);
-#if LH_PTR
         S.pr[q] = js * LH_LPR;
         S.off[q] = (j - js * (LH_BYTES / 16)) * 16;
-#else
-        S.src[q] = in + (s0 + js) * in_stride + (j - js * (LH_BYTES / 16)) * 16;
-#endif
     }
 #pragma unroll
     for (int q = 0; q < LH_LDE; ++q)
@@ -702,12 +694,8 @@ __device__ __forceinline__ void lh_encode_wave_lds(long long wave, const unsigne
             if (j < n) {
                 const int js = j / per, t = j - js * per;
                 const lh_u32x4a v = *(const lh_u32x4a *)(S.ring + js * (LH_M * LH_BYTES) + t * 16);
-#if LH_PTR
                 const int r = t / (LH_BYTES / 16);
                 unsigned char *dst = (unsigned char *)S.pt[js * LH_LPR + LH_K + r] + (t - r * (LH_BYTES / 16)) * 16;
-#else
-                unsigned char *dst = out + (s0 + js) * out_stride + t * 16;
-#endif
 #if LH_NT_ST
                 __builtin_nontemporal_store(v, (lh_u32x4a *)dst);
 #else
@@ -722,11 +710,7 @@ __device__ __forceinline__ void lh_encode_wave_lds(long long wave, const unsigne
     const int p = last ? LH_SUB - 8 : 8 * c;
 #pragma unroll
     for (int r = 0; r < LH_M; ++r) {
-#if LH_PTR
         unsigned char *o = (unsigned char *)S.pt[sl * LH_LPR + LH_K + r] + p;
-#else
-        unsigned char *o = out + (s0 + sl) * out_stride + (long long)r * LH_BYTES + p;
-#endif
 #pragma unroll
         for (int y = 0; y < 8; ++y) {
             lh_word w = acc[r][y];

@@ -61,7 +61,8 @@ def test_specialisation_policy():
 def test_lds_staging_policy():
     """jit.cpp jit_config_for: the register networks stage their columns by LDS-DMA for 8-byte
     lanes, whole stripes per wave and 16-byte-multiple blocks, unless a stripe's partial last
-    lane would open a 16-lane DPP row (its stores funnel the previous lane's word)."""
+    lane would open a 16-lane DPP row (its stores funnel the previous lane's word) or the
+    encode's ring plus its stripes' block-pointer rows would not fit two workgroups per CU."""
     import longhair_amd
     assert longhair_amd.lds_staged(29, 4, 1296)        # nch 21, spw 3: last lanes 20, 41, 62
     assert longhair_amd.lds_staged(64, 4, 4096)        # nch 64: the last lane is whole
@@ -69,6 +70,7 @@ def test_lds_staging_policy():
     assert not longhair_amd.lds_staged(29, 4, 1040)    # nch 17, spw 3: lane 16 is a last lane
     assert not longhair_amd.lds_staged(29, 8, 1296)    # m = 8: 4-byte lanes
     assert not longhair_amd.lds_staged(100, 12, 800)   # no register network
+    assert not longhair_amd.lds_staged(64, 4, 64)      # spw 64: the encode's pointer rows would not fit
 
 
 def test_no_device_gpu_policy_fails_loudly():
