@@ -1480,21 +1480,30 @@ struct lh_dldsrc {
     }
 };
 // LH_LDG: the ring refilled LH_LDG slots at a time (after every LH_LDG-th column) instead of
-// one slot per column, each refill reading the slot maps it needs then: k29/m4 decode 0.577
-// -> 0.559 ms (profiles/r7a_tune_k29m4_ldg.txt; 2 and 3 alike, the encode unchanged).
+// one slot per column: k29/m4 decode 0.577 -> 0.559 ms (profiles/r7a_tune_k29m4_ldg.txt; 2
+// and 3 alike, the encode unchanged).  The refill's slot maps are read before the wait of the
+// column that ends its group (0.561 -> 0.558 ms against reading them at the issue,
+// r7w_tune_k29m4_dec_slot_prefetch.txt).
 #ifndef LH_LDG
 #define LH_LDG (LH_LD > 2 ? 2 : 1)
 #endif
 #if LH_LDG < 1 || LH_LDG >= LH_LD
 #error "LH_LDG: 1 <= LH_LDG < LH_LD"
 #endif
-template <int C, int N>  // columns C .. C + N - 1 (those that exist) into their slots
-__device__ __forceinline__ void lh_dissue(const lh_dldsrc &S) {
+// Columns C .. C + N - 1 (those that exist): their slot maps read into sv[0 .. N - 1] (before
+// the wait of the column that ends the group), then their DMAs issued into their slots.
+template <int C, int N>
+__device__ __forceinline__ void lh_dslots(const lh_dldsrc &S, unsigned (&sv)[LH_LDG][LH_LQ]) {
     if constexpr (N > 0 && C < LH_DCOLS) {
-        unsigned sv[LH_LQ];
-        S.slots<C>(sv);
-        S.issue(sv, C % LH_LD);
-        lh_dissue<C + 1, N - 1>(S);
+        S.slots<C>(sv[LH_LDG - N]);
+        lh_dslots<C + 1, N - 1>(S, sv);
+    }
+}
+template <int C, int N>
+__device__ __forceinline__ void lh_dissue(const lh_dldsrc &S, const unsigned (&sv)[LH_LDG][LH_LQ]) {
+    if constexpr (N > 0 && C < LH_DCOLS) {
+        S.issue(sv[LH_LDG - N], C % LH_LD);
+        lh_dissue<C + 1, N - 1>(S, sv);
     }
 }
 template <int X>
@@ -1505,6 +1514,9 @@ struct lh_unroll_decode_lds {
             constexpr int ahead = issued - 1 - X;
             unsigned sv[LH_LQ];
             if constexpr (LH_LDG == 1 && X + LH_LD < LH_DCOLS) S.slots<(X + LH_LD < LH_DCOLS ? X + LH_LD : 0)>(sv);
+            constexpr bool refill = LH_LDG > 1 && (X + 1) % LH_LDG == 0 && LH_LD + X + 1 - LH_LDG < LH_DCOLS;
+            unsigned svg[LH_LDG][LH_LQ];
+            if constexpr (refill) lh_dslots<LH_LD + X + 1 - LH_LDG, LH_LDG>(S, svg);
             lh_wait_vmcnt<LH_LQ * ahead>();
             asm volatile("" ::: "memory");  // no LDS read moves above the wait
             lh_word d[8];
@@ -1514,9 +1526,9 @@ struct lh_unroll_decode_lds {
             if constexpr (LH_LDG == 1 && X + LH_LD < LH_DCOLS) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done
                 S.issue(sv, X % LH_LD);
-            } else if constexpr (LH_LDG > 1 && (X + 1) % LH_LDG == 0 && LH_LD + X + 1 - LH_LDG < LH_DCOLS) {
+            } else if constexpr (refill) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slots' reads are done
-                lh_dissue<LH_LD + X + 1 - LH_LDG, LH_LDG>(S);
+                lh_dissue<LH_LD + X + 1 - LH_LDG, LH_LDG>(S, svg);
             }
             lh_unroll_decode_lds<X + 1>::run(v, S, lo, lo8);
         }
