@@ -32,8 +32,10 @@
  *
  * Buffers may be host memory (pageable or pinned) or HIP device memory.  Where a call runs
  * is the dispatch policy of cauchy_256_dispatch.h: by default (AUTO) a small all-host call
- * runs on the host SIMD engine and every other call on the GPU; the library needs a GPU
- * under every policy.  For batches of stripes resident in device memory use
+ * runs on the host SIMD engine and every other call on the GPU.  No GPU is needed under
+ * AUTO or HOST: without one every drop-in call runs on the host engine (under GPU, init and
+ * the drop-in calls return -2).  For batches of stripes
+ * resident in device memory use
  * cauchy_256_batch.h, which avoids the per-call PCIe round trip.
  */
 #ifndef LONGHAIR_AMD_CAUCHY_256_H

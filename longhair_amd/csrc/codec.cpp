@@ -293,12 +293,19 @@ static int workspace(Device *d, hipStream_t st, size_t plan_bytes, size_t work_b
     return kOk;
 }
 
-// Grid for a specialised kernel: one 4-wave block per 4 waves of work, optionally capped
-// (LONGHAIR_AMD_GRID) to run persistent, grid-stride waves.
+// Grid for a specialised kernel: one 4-wave block per 4 waves of work.
 static long long jit_blocks(const JitConfig &cfg, int stripes) {
     const long long waves = cfg.spw ? (stripes + cfg.spw - 1) / cfg.spw : (long long)stripes * cfg.wps;
     long long blocks = (waves + 3) / 4;
     return blocks;
+}
+// The encode's grid: a persistent encode (cfg.pers) runs as many blocks as stay resident, each
+// wave taking an equal share of the stripes; any grid is correct, so an unknown occupancy
+// keeps one block per 4 waves of work.
+static long long jit_encode_blocks(const Device *d, const JitKernels *jk, int stripes) {
+    const long long blocks = jit_blocks(jk->cfg, stripes);
+    if (!jk->cfg.pers || jk->encode_blocks_per_cu <= 0 || d->cus <= 0) return blocks;
+    return std::min(blocks, (long long)d->cus * jk->encode_blocks_per_cu);
 }
 
 static int generic_word(int sub) {
@@ -388,13 +395,13 @@ static int encode_batch(int k, int m, int bytes, int stripes, const uint8_t *d_d
         bool hard = false;
         const JitKernels *jk = jit_lookup(d, cfg, allow_compile, &err, &hard);
         if (jk) {
-            const long long blocks = jit_blocks(cfg, stripes);
+            const long long blocks = jit_encode_blocks(d, jk, stripes);
             if (blocks > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
             long long in_stride = data_stride, out_stride = rec_stride;
             int n = stripes;
             void *args[] = {(void *)&d_data, &in_stride, (void *)&d_rec, &out_stride, &n};
             LH_HIP(hipModuleLaunchKernel(jk->encode, (unsigned)blocks, 1, 1, 256,
-                                         1, 1, 0, st, args, nullptr));
+                                         1, 1, jk->encode_dyn_lds, st, args, nullptr));
             note_launch("lh_jit_encode");
             return kOk;
         }
@@ -538,8 +545,7 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         return kOk;
     }
     // Large m (<= 64), sub % (64 W) == 0, after the planner: the windowed phase-A kernel
-    // (V_r in place of R_r) and lh_inverse_kernel (phase B), or the fused windowed decode
-    // (phase A into an LDS tile, phase B from it; LONGHAIR_AMD_WIN_SPLIT=0).
+    // lh_jit_decode_wide (V_r in place of R_r), then lh_inverse_gt_kernel (phase B).
     JitConfig wcfg;
     const JitKernels *wk = nullptr;
     if (generic && jit_win_config_for(k, m, bytes, &wcfg, true)) {
@@ -737,7 +743,7 @@ static int encode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
         bool hard = false;
         const JitKernels *jk = jit_lookup(d, cfg, allow_compile, &err, &hard);
         if (jk) {
-            const long long blocks = jit_blocks(cfg, stripes);
+            const long long blocks = jit_encode_blocks(d, jk, stripes);
             if (blocks > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
             long long in_stride = (long long)k * 8, out_stride = (long long)m * 8;
             int n = stripes;

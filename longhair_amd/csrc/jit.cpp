@@ -106,6 +106,13 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     cfg->plain = decode && !(emax <= 4 && nch2 <= 64 && k <= 64 && std::getenv("LONGHAIR_AMD_NO_FUSED_PLAN") == nullptr);
     cfg->defines.clear();
     if (const char *d = std::getenv("LONGHAIR_AMD_JIT_DEFINES")) cfg->defines = d;
+    // Resident encode workgroups per CU (dynamic LDS pads the rest): a tuning define for now.
+    if (!decode) {
+        const size_t at = cfg->defines.find("LH_WGCU=");
+        cfg->enc_wgcu = at == std::string::npos ? 0 : std::atoi(cfg->defines.c_str() + at + 8);
+    }
+    // Persistent LDS encode (jit_codec.hip LH_PERS): a tuning define for now.
+    cfg->pers = (!decode && cfg->lds && k >= 8 && (cfg->defines.find("LH_PERS=1") != std::string::npos || cfg->defines.find("LH_PERS=2") != std::string::npos)) ? 1 : 0;
     return true;
 }
 
@@ -633,13 +640,22 @@ JitMode batch_jit_mode() {
 // Background compilations run on ONE long-lived worker thread fed by a queue (round 5,
 // a thread per compilation stayed mapped until process exit, so a process meeting
 // many shapes grew without bound).  The worker is started by the first background request.
-// Exit: the worker registers a drain handler with atexit() right after its first hiprtc
-// compilation returns, i.e. after hiprtc has created its own lazily constructed state, so at
-// exit the handler (run in reverse order of registration) drops the queued requests and waits
-// for the one in flight while hiprtc is still intact.  (A compilation still in flight when
-// the process exits before the first one ever finished is the one case the handler cannot
-// cover: then the worker is detached by the registry's destructor.)
+// Exit: before that first request is queued, the posting thread compiles a
+// trivial program, so hiprtc's lazily constructed state (and its exit-time teardown) exists
+// before the drain handler is registered with atexit(); handlers and static destructors run
+// in reverse order, so at exit the drain runs first: it drops the queued requests and joins
+// the worker (waiting for the compilation in flight) while hiprtc is still intact.  The
+// worker is never detached.
 namespace {
+void warm_hiprtc() {
+    hiprtcProgram p;
+    if (hiprtcCreateProgram(&p, "extern \"C\" __global__ void lh_warm() {}", "lh_warm.hip", 0, nullptr, nullptr) !=
+        HIPRTC_SUCCESS)
+        return;
+    const char *opts[] = {"--offload-arch=gfx950", "-O0"};
+    (void)hiprtcCompileProgram(p, 2, opts);
+    hiprtcDestroyProgram(&p);
+}
 struct CompileWorker {
     std::mutex mu;
     std::condition_variable cv, idle_cv;
@@ -647,8 +663,16 @@ struct CompileWorker {
     std::thread th;
     bool busy = false, stop = false, drain_registered = false;
     void post(std::function<void()> f) {
-        std::lock_guard<std::mutex> g(mu);
+        std::unique_lock<std::mutex> g(mu);
         if (stop) return;  // exiting: the request stays pending, its shape on the generic kernels
+        if (!drain_registered) {
+            drain_registered = true;
+            g.unlock();
+            warm_hiprtc();
+            std::atexit(drain_at_exit);
+            g.lock();
+            if (stop) return;
+        }
         q.push_back(std::move(f));
         if (!th.joinable()) th = std::thread([this] { run(); });
         cv.notify_one();
@@ -665,13 +689,10 @@ struct CompileWorker {
                 busy = true;
             }
             f();
-            bool reg = false;
             {
                 std::lock_guard<std::mutex> g(mu);
                 busy = false;
-                if (!drain_registered) reg = drain_registered = true;
             }
-            if (reg) std::atexit(drain_at_exit);
             idle_cv.notify_all();
         }
     }
@@ -691,12 +712,7 @@ struct CompileWorker {
         if (th.joinable() && th.get_id() != std::this_thread::get_id()) th.join();
     }
     static void drain_at_exit();
-    ~CompileWorker() {
-        std::lock_guard<std::mutex> g(mu);
-        stop = true;
-        q.clear();
-        if (th.joinable()) th.detach();  // (see above: only reached with a first compile in flight)
-    }
+    ~CompileWorker() { shutdown(); }  // (the drain handler has normally joined it already)
 };
 CompileWorker &compile_worker() {
     static CompileWorker w;
@@ -788,6 +804,24 @@ const JitKernels *JitCache::load_locked(const Key &key, const JitConfig &cfg, st
     kern.decode_fused = fn("lh_jit_decode_fused");
     kern.encode_win = fn("lh_jit_encode_win");
     kern.decode_wide = fn("lh_jit_decode_wide");
+    if (kern.encode && cfg.enc_wgcu > 0) {
+        int st = 0;
+        if (hipFuncGetAttribute(&st, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, kern.encode) != hipSuccess) {
+            (void)hipGetLastError();
+            st = 0;
+        }
+        const int per = 160 * 1024 / cfg.enc_wgcu;  // gfx950: 160 KiB of LDS per CU
+        kern.encode_dyn_lds = st > 0 && per - 1024 > st ? (unsigned)(per - 1024 - st + 16) : 0u;
+        if (kern.encode_dyn_lds && st + (int)kern.encode_dyn_lds > 160 * 1024) kern.encode_dyn_lds = 0;
+    }
+    if (kern.encode && cfg.pers) {
+        int n = 0;
+        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern.encode, 256, kern.encode_dyn_lds) != hipSuccess) {
+            (void)hipGetLastError();
+            n = 0;
+        }
+        kern.encode_blocks_per_cu = n;
+    }
     // (one role per register-network module: the encode, or one of the two decodes)
     if (!kern.encode && !kern.decode && !kern.decode_fused && !kern.encode_win && !kern.decode_wide) {
         *err = "specialised module has no kernel";

@@ -418,6 +418,26 @@ def test_aligned_decode_buffer(lh, oracle, align):
     assert (raw[pad] == 0x5A).all()
 
 
+def test_exit_during_background_compile(tmp_path):
+    """A short-lived process that meets a new shape and exits at once, its background hiprtc
+    compilation still running (jit.cpp CompileWorker): the exit-time drain joins the
+    worker while hiprtc is intact, so the process ends cleanly (exit code 0, no abort)."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import sys, torch; sys.path.insert(0, %r); import longhair_amd as lh\n"
+        "assert lh.cauchy_256_init() == 0\n"
+        "x = torch.zeros((8, 11, 72), dtype=torch.uint8, device='cuda')\n"
+        "lh.encode_batch(x, 3); torch.cuda.synchronize()\n"
+        "print('trace', lh.last_launch(), flush=True)\n"
+    ) % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LONGHAIR_AMD_JIT_SYNC="0", LONGHAIR_AMD_CACHE_DIR=str(tmp_path))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    assert "lh_apply_jump" in r.stdout, r.stdout  # it ran on the generic kernels, compile in flight
+
+
 def test_jit_compiles_in_background(lh, oracle, monkeypatch, tmp_path):
     """A batch call on a shape with no specialised module returns at once on the generic
     kernels while hiprtc compiles the module on a background thread (no lock held: other
