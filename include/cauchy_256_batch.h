@@ -98,9 +98,12 @@ const char *cauchy_256_last_launch(void);
  * 1 = run-time specialised (JIT) network, 2 (decode only) = specialised network with the
  * erasure plan computed inside the same kernel, 3 (encode only) = run-time specialised
  * 4-bit-windowed network for large m, 4 (decode only) = per-stripe planner + fused
- * windowed decode for large m (m <= 64).  `what` = 0 for encode, 1 for decode; `what` = 2:
- * 1 when the shape's register networks (encode, and the decode with the in-kernel plan)
- * stage their columns in LDS by LDS-DMA, else 0. */
+ * windowed decode for large m (m <= 64).  `what` = 0 for encode, 1 for decode.
+ * `what` = 2 (encode) / 5 (decode): 1 when the shape's register network stages its columns in
+ * LDS by LDS-DMA, else 0.  `what` = 6 (encode) / 7 (decode): the dword lanes per sub-block of
+ * the generic jump kernel on the current device (1: lh_apply_jump_kernel, 2:
+ * lh_apply_jump2_kernel), 0 when the generic kernels below dword lanes serve the shape; -2
+ * without a device. */
 int cauchy_256_batch_path(int k, int m, int block_bytes, int what);
 
 /* Compile the specialised kernels of a shape into the on-disk code-object cache

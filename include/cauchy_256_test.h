@@ -1,4 +1,6 @@
-/* cauchy_256_test.h -- test-only hooks of liblonghair_amd.so (not part of the drop-in API).
+/* cauchy_256_test.h -- test-only hooks (not part of the drop-in API).  Exported by the checked
+ * build only (liblonghair_amd_check.so, `make LH_DEBUG=1`, which defines LH_TEST_HOOKS); the
+ * product library liblonghair_amd.so has none, so no caller can inject a failure into it.
  *
  * SURVEY 8(b) asks that no C++ exception crosses the C ABI: every int-returning entry point
  * of cauchy_256.h, cauchy_256_batch.h and cauchy_256_dispatch.h catches whatever the

@@ -319,10 +319,20 @@ def batch_path(k, m, block_bytes, decode=False):
     return {0: "generic", 1: "jit", 2: "jit-fused", 3: "jit-win", 4: "jit-wide"}[code]
 
 
-def lds_staged(k, m, block_bytes):
-    """True when the shape's register networks stage their columns by LDS-DMA (jit.cpp
-    jit_config_for, jit_codec.hip LH_LDS)."""
-    return lib().cauchy_256_batch_path(k, m, block_bytes, 2) == 1
+def lds_staged(k, m, block_bytes, decode=False):
+    """True when the shape's encode (decode) register network stages its columns by LDS-DMA
+    (jit.cpp jit_config_for, jit_codec.hip LH_LDS)."""
+    return lib().cauchy_256_batch_path(k, m, block_bytes, 5 if decode else 2) == 1
+
+
+def jump_lanes(k, m, block_bytes, decode=False):
+    """Dword lanes per sub-block of the generic jump kernel the library launches for this
+    shape on the current device (codec.cpp jump_layout): 1 = lh_apply_jump_kernel, 2 =
+    lh_apply_jump2_kernel, 0 = the generic kernels below dword lanes."""
+    rc = lib().cauchy_256_batch_path(k, m, block_bytes, 7 if decode else 6)
+    if rc < 0:
+        raise LonghairError(rc, "cauchy_256_batch_path")
+    return rc
 
 
 def kernel_names(k, m, block_bytes):
@@ -335,8 +345,8 @@ def kernel_names(k, m, block_bytes):
         return sub % w != 0 and nch > 1 and (nch - 1) % 64 == 0
 
     old_dec = small or lone_tail(4)
-    two_dec = sub >= 512 and min(k, m) <= 4 and not lone_tail(8)  # codec.cpp jump_layout
-    two_enc = sub >= 8 and m <= 4
+    two_dec = not old_dec and jump_lanes(k, m, block_bytes, True) == 2  # (the library's own choice)
+    two_enc = not small and jump_lanes(k, m, block_bytes) == 2
     jump_enc = "lh_apply_generic_kernel" if small else ("lh_apply_jump2_kernel" if two_enc else "lh_apply_jump_kernel")
     enc = {"generic": [jump_enc], "jit": ["lh_jit_encode"],
            "jit-win": ["lh_jit_encode_win"]}[batch_path(k, m, block_bytes)]

@@ -55,8 +55,27 @@ EXPORTS = {
     "cauchy_256_set_dispatch": (ctypes.c_int, [ctypes.c_int, ctypes.c_longlong]),
     "cauchy_256_get_dispatch": (ctypes.c_int, []),
     "cauchy_256_host_isa": (ctypes.c_char_p, []),
+}
+# Bound only where the library exports them: the test-only hook lives in the checked build
+# (liblonghair_amd_check.so, LH_TEST_HOOKS), not in the product library.
+OPTIONAL_EXPORTS = {
     "cauchy_256_debug_throw_next": (None, []),
 }
+
+
+def bind(l):
+    """Set the ctypes signatures of a loaded copy of the library (every EXPORTS symbol must
+    exist; OPTIONAL_EXPORTS where present)."""
+    for name, (res, args) in EXPORTS.items():
+        f = getattr(l, name)
+        f.restype = res
+        f.argtypes = args
+    for name, (res, args) in OPTIONAL_EXPORTS.items():
+        if hasattr(l, name):
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+    return l
 
 
 def lib():
@@ -67,9 +86,6 @@ def lib():
             raise OSError(f"{library_path} is missing: run `make -C longhair_amd/csrc` "
                           "(longhair_amd has no CPU fallback)")
         l = ctypes.CDLL(library_path)
-        for name, (res, args) in EXPORTS.items():
-            f = getattr(l, name)
-            f.restype = res
-            f.argtypes = args
+        bind(l)
         _lib = l
     return _lib

@@ -55,8 +55,10 @@ static int internal_error() noexcept {
     return kHipError;
 }
 
-// Test-only (cauchy_256_debug_throw_next, include/cauchy_256_test.h): the calling thread's
-// next guarded entry point throws inside its guard.
+// Test-only (cauchy_256_debug_throw_next, include/cauchy_256_test.h; built into the checked
+// library only, LH_TEST_HOOKS): the calling thread's next guarded entry point throws inside
+// its guard.
+#ifdef LH_TEST_HOOKS
 thread_local int g_throw_next = 0;
 static void test_hook() {
     if (g_throw_next) {
@@ -64,6 +66,9 @@ static void test_hook() {
         throw std::runtime_error("exception injected by cauchy_256_debug_throw_next");
     }
 }
+#else
+static inline void test_hook() {}
+#endif
 
 void note_launch(const char *kernel) {
     const std::string k(kernel);
@@ -299,15 +304,11 @@ static long long jit_blocks(const JitConfig &cfg, int stripes) {
     long long blocks = (waves + 3) / 4;
     return blocks;
 }
-// The encode's grid: a persistent encode (cfg.pers) runs as many blocks as stay resident, each
-// wave taking an equal share of the stripes; any grid is correct, so an unknown occupancy
-// keeps one block per 4 waves of work.
-static long long jit_encode_blocks(const Device *d, const JitKernels *jk, int stripes) {
-    const long long blocks = jit_blocks(jk->cfg, stripes);
-    if (!jk->cfg.pers || jk->encode_blocks_per_cu <= 0 || d->cus <= 0) return blocks;
-    return std::min(blocks, (long long)d->cus * jk->encode_blocks_per_cu);
+// The encode's grid: one block per cfg.enc_wpb waves of work.
+static long long jit_encode_blocks(const JitConfig &cfg, int stripes) {
+    const long long waves = cfg.spw ? (stripes + cfg.spw - 1) / cfg.spw : (long long)stripes * cfg.wps;
+    return (waves + cfg.enc_wpb - 1) / cfg.enc_wpb;
 }
-
 static int generic_word(int sub) {
     if (sub >= 4) return 4;
     if (sub >= 2) return 2;
@@ -395,13 +396,13 @@ static int encode_batch(int k, int m, int bytes, int stripes, const uint8_t *d_d
         bool hard = false;
         const JitKernels *jk = jit_lookup(d, cfg, allow_compile, &err, &hard);
         if (jk) {
-            const long long blocks = jit_encode_blocks(d, jk, stripes);
+            const long long blocks = jit_encode_blocks(cfg, stripes);
             if (blocks > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
             long long in_stride = data_stride, out_stride = rec_stride;
             int n = stripes;
             void *args[] = {(void *)&d_data, &in_stride, (void *)&d_rec, &out_stride, &n};
-            LH_HIP(hipModuleLaunchKernel(jk->encode, (unsigned)blocks, 1, 1, 256,
-                                         1, 1, jk->encode_dyn_lds, st, args, nullptr));
+            LH_HIP(hipModuleLaunchKernel(jk->encode, (unsigned)blocks, 1, 1, 64u * (unsigned)cfg.enc_wpb,
+                                         1, 1, jk->dyn_lds, st, args, nullptr));
             note_launch("lh_jit_encode");
             return kOk;
         }
@@ -540,7 +541,8 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         int n = stripes;
         void *args[] = {(void *)&d_blocks, &s1, (void *)&d_rows, (void *)&d_status, (void *)&zero,
                         (void *)&gexp, (void *)&glog, &n};
-        LH_HIP(hipModuleLaunchKernel(fn, (unsigned)jit_blocks(cfg, stripes), 1, 1, 256, 1, 1, 0, st, args, nullptr));
+        LH_HIP(hipModuleLaunchKernel(fn, (unsigned)jit_blocks(cfg, stripes), 1, 1, 256, 1, 1, jk->dyn_lds, st, args,
+                                     nullptr));
         note_launch("lh_jit_decode_fused");
         return kOk;
     }
@@ -743,7 +745,7 @@ static int encode_batch_ptrs(int k, int m, int bytes, int stripes, uint8_t *cons
         bool hard = false;
         const JitKernels *jk = jit_lookup(d, cfg, allow_compile, &err, &hard);
         if (jk) {
-            const long long blocks = jit_encode_blocks(d, jk, stripes);
+            const long long blocks = jit_blocks(cfg, stripes);
             if (blocks > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
             long long in_stride = (long long)k * 8, out_stride = (long long)m * 8;
             int n = stripes;
@@ -1627,8 +1629,18 @@ LH_API int cauchy_256_jit_precompile(int k, int m, int block_bytes) {
 LH_API int cauchy_256_batch_path(int k, int m, int block_bytes, int what) {
     LH_TRY
         lh::JitConfig cfg;
-        if (what == 2)  // 1: the register networks stage their columns by LDS-DMA (LH_LDS)
-            return lh::jit_config_for(k, m, block_bytes, false, &cfg) && cfg.lds ? 1 : 0;
+        if (what == 2 || what == 5)  // 1: the register network stages its columns by LDS-DMA (LH_LDS)
+            return lh::jit_config_for(k, m, block_bytes, what == 5, &cfg) && cfg.lds ? 1 : 0;
+        if (what == 6 || what == 7) {  // the generic jump kernel's lane width (jump_layout)
+            if (block_bytes <= 0 || block_bytes % 8 || block_bytes / 8 < 4) return 0;
+            lh::Device *d = nullptr;
+            if (int rc = lh::current_device(&d)) return rc;
+            lh::JumpApplyArgs a{};
+            a.sub = block_bytes / 8;
+            a.n_out = what == 6 ? m : (k < m ? k : m);
+            lh::jump_layout(d, a, what == 7);
+            return a.dw;
+        }
         if (!lh::jit_config_for(k, m, block_bytes, what == 1, &cfg)) {
             if (what == 0) return lh::jit_win_config_for(k, m, block_bytes, &cfg) ? 3 : 0;
             return lh::jit_win_config_for(k, m, block_bytes, &cfg, true) ? 4 : 0;
@@ -1715,8 +1727,11 @@ LH_API int cauchy_256_get_dispatch(void) {
 
 LH_API const char *cauchy_256_host_isa(void) { return lh::host::isa_name(); }
 
-// Test-only (include/cauchy_256_test.h): the calling thread's next guarded entry point
-// throws inside its exception barrier, which must turn it into -3.
+// Test-only (include/cauchy_256_test.h; the checked library only, LH_TEST_HOOKS): the
+// calling thread's next guarded entry point throws inside its exception barrier, which must
+// turn it into -3.  The product library does not export it.
+#ifdef LH_TEST_HOOKS
 LH_API void cauchy_256_debug_throw_next(void) { lh::g_throw_next = 1; }
+#endif
 
 }  // extern "C"

@@ -107,12 +107,15 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     cfg->defines.clear();
     if (const char *d = std::getenv("LONGHAIR_AMD_JIT_DEFINES")) cfg->defines = d;
     // Resident encode workgroups per CU (dynamic LDS pads the rest): a tuning define for now.
-    if (!decode) {
+    {
         const size_t at = cfg->defines.find("LH_WGCU=");
-        cfg->enc_wgcu = at == std::string::npos ? 0 : std::atoi(cfg->defines.c_str() + at + 8);
+        cfg->wgcu = at == std::string::npos ? 0 : std::atoi(cfg->defines.c_str() + at + 8);
     }
-    // Persistent LDS encode (jit_codec.hip LH_PERS): a tuning define for now.
-    cfg->pers = (!decode && cfg->lds && k >= 8 && (cfg->defines.find("LH_PERS=1") != std::string::npos || cfg->defines.find("LH_PERS=2") != std::string::npos)) ? 1 : 0;
+    if (!decode && cfg->lds) {
+        const size_t at = cfg->defines.find("LH_WPB=");
+        const int wpb = at == std::string::npos ? 4 : std::atoi(cfg->defines.c_str() + at + 7);
+        cfg->enc_wpb = (wpb >= 1 && wpb <= 4 && cfg->defines.find("LH_CPS=") != std::string::npos) ? wpb : 4;
+    }
     return true;
 }
 
@@ -804,23 +807,16 @@ const JitKernels *JitCache::load_locked(const Key &key, const JitConfig &cfg, st
     kern.decode_fused = fn("lh_jit_decode_fused");
     kern.encode_win = fn("lh_jit_encode_win");
     kern.decode_wide = fn("lh_jit_decode_wide");
-    if (kern.encode && cfg.enc_wgcu > 0) {
+    if (hipFunction_t f = kern.encode ? kern.encode : kern.decode_fused ? kern.decode_fused : kern.decode;
+        f && cfg.wgcu > 0 && !cfg.win) {
         int st = 0;
-        if (hipFuncGetAttribute(&st, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, kern.encode) != hipSuccess) {
+        if (hipFuncGetAttribute(&st, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, f) != hipSuccess) {
             (void)hipGetLastError();
             st = 0;
         }
-        const int per = 160 * 1024 / cfg.enc_wgcu;  // gfx950: 160 KiB of LDS per CU
-        kern.encode_dyn_lds = st > 0 && per - 1024 > st ? (unsigned)(per - 1024 - st + 16) : 0u;
-        if (kern.encode_dyn_lds && st + (int)kern.encode_dyn_lds > 160 * 1024) kern.encode_dyn_lds = 0;
-    }
-    if (kern.encode && cfg.pers) {
-        int n = 0;
-        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern.encode, 256, kern.encode_dyn_lds) != hipSuccess) {
-            (void)hipGetLastError();
-            n = 0;
-        }
-        kern.encode_blocks_per_cu = n;
+        const int per = 160 * 1024 / cfg.wgcu;  // gfx950: 160 KiB of LDS per CU
+        kern.dyn_lds = st > 0 && per - 1024 > st ? (unsigned)(per - 1024 - st + 16) : 0u;
+        if (kern.dyn_lds && st + (int)kern.dyn_lds > 160 * 1024) kern.dyn_lds = 0;
     }
     // (one role per register-network module: the encode, or one of the two decodes)
     if (!kern.encode && !kern.decode && !kern.decode_fused && !kern.encode_win && !kern.decode_wide) {

@@ -34,10 +34,9 @@ struct JitConfig {
                           // 2 = the decode module: lh_jit_decode_fused, or lh_jit_decode when
                           // the fused plan does not apply or is switched off (plain = 1)
     int plain = 0;
-    int enc_wgcu = 0;     // encode: resident workgroups per CU forced by dynamic LDS (0: natural)
-    int pers = 0;         // LDS encode: persistent waves, the column ring carried across stripe
-                          // groups (LH_PERS, jit_codec.hip); the host caps the grid at the
-                          // resident workgroups
+    int wgcu = 0;         // register networks: resident workgroups per CU of the module's kernel,
+                          // forced by dynamic LDS (0: natural)
+    int enc_wpb = 4;      // encode: waves per workgroup (LH_WPB, multi-column-step encode only)
     int lanes_per_launch_unit() const { return 64; }
 };
 
@@ -48,8 +47,7 @@ struct JitKernels {
     hipFunction_t decode_fused = nullptr;  // plan computed in-kernel (e_max <= 4)
     hipFunction_t encode_win = nullptr;    // windowed large-m encode (win modules)
     hipFunction_t decode_wide = nullptr;   // fused windowed decode (win == 2 modules, m <= 64)
-    int encode_blocks_per_cu = 0;          // resident 256-thread workgroups of `encode` (cfg.pers)
-    unsigned encode_dyn_lds = 0;           // dynamic LDS bytes per launch of `encode` (cfg.enc_wgcu)
+    unsigned dyn_lds = 0;                  // dynamic LDS bytes per launch of the module's kernel (cfg.wgcu)
     JitConfig cfg{};
 };
 

@@ -787,6 +787,9 @@ __device__ __forceinline__ void lh_encode_wave_lds(long long wave, const unsigne
 #ifndef LH_CPS
 #define LH_CPS 1
 #endif
+#ifndef LH_WPB
+#define LH_WPB 4  // waves per workgroup of the LH_CPS encode (the host launches LH_WPB x 64 threads)
+#endif
 #if LH_LDS && LH_CPS > 1 && !LH_PTR
 #define LH_CCH (LH_BYTES / 16)                              // 16-byte chunks per block
 #define LH_SCH (LH_CPS * LH_CCH)                            // ... per stripe and step
@@ -833,10 +836,49 @@ struct lh_unroll_cps {
         }
     }
 };
+#ifndef LH_CPS_FLAT
+#define LH_CPS_FLAT 0  // (per-lane stores: at one workgroup per CU the slot-image stores measured slower)
+#endif
+// Recovery rows per slot image (the slot holds LH_SQ KiB).
+#define LH_CRP ((LH_SQ * 1024) / (LH_SPW * LH_BYTES) < LH_M ? (LH_SQ * 1024) / (LH_SPW * LH_BYTES) : LH_M)
+#if LH_CRP >= 1
+template <int R0>
+struct lh_cps_flat {
+    __device__ __forceinline__ static void run(const lh_word (&acc)[LH_M][8], unsigned char *slot,
+                                               unsigned char *__restrict__ out, long long out_stride, long long s0,
+                                               int nst, int sl, int c, bool last) {
+        if constexpr (R0 < LH_M) {
+            constexpr int nr = (LH_M - R0) < LH_CRP ? (LH_M - R0) : LH_CRP;
+            unsigned char *img = slot + (sl < LH_SPW ? sl : LH_SPW - 1) * (nr * LH_BYTES) + (last ? LH_SUB - 8 : 8 * c);
+#pragma unroll
+            for (int r = 0; r < nr; ++r) lh_img_row<0>(img + r * LH_BYTES, acc[R0 + r], last, sl < nst);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the image is complete
+            constexpr int per = nr * LH_BYTES / 16;  // chunks per stripe
+            const int n = nst * per, lane = threadIdx.x & 63;
+#pragma unroll
+            for (int q = 0; q < (LH_SPW * per + 63) / 64; ++q) {
+                const int j = 64 * q + lane;
+                if (j < n) {
+                    const int js = j / per, t = j - js * per;
+                    const lh_u32x4a v = *(const lh_u32x4a *)(slot + j * 16);
+                    unsigned char *dst = out + (s0 + js) * out_stride + R0 * LH_BYTES + t * 16;
+#if LH_NT_ST
+                    __builtin_nontemporal_store(v, (lh_u32x4a *)dst);
+#else
+                    *(lh_u32x4a *)dst = v;
+#endif
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done
+            lh_cps_flat<R0 + nr>::run(acc, slot, out, out_stride, s0, nst, sl, c, last);
+        }
+    }
+};
+#endif
 __device__ __forceinline__ void lh_encode_wave_cps(long long wave, const unsigned char *__restrict__ in,
                                                    long long in_stride, unsigned char *__restrict__ out,
                                                    long long out_stride, int stripes) {
-    __shared__ __attribute__((aligned(16))) unsigned char lh_cring[4][LH_SSLOT];
+    __shared__ __attribute__((aligned(16))) unsigned char lh_cring[LH_WPB][LH_SSLOT];
     const int lane = threadIdx.x & 63;
     const int sl = lane / LH_NCH, c = lane - sl * LH_NCH;
     const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)wave) * LH_SPW;  // wave-uniform
@@ -866,32 +908,10 @@ __device__ __forceinline__ void lh_encode_wave_cps(long long wave, const unsigne
     lh_unroll_cps<0>::run(acc, rs, voff, slot, lo, lo8);
     const bool last = c == LH_NCH - 1;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every slot read of the last step done
-#if LH_SPW * LH_M * LH_BYTES <= LH_SQ * 1024
-    // The recovery blocks [stripe][row][bytes] assembled in the slot, stored as 16-byte chunks.
-    {
-        unsigned char *img = slot + (sl < LH_SPW ? sl : LH_SPW - 1) * (LH_M * LH_BYTES) + (last ? LH_SUB - 8 : 8 * c);
-#pragma unroll
-        for (int r = 0; r < LH_M; ++r) lh_img_row<0>(img + r * LH_BYTES, acc[r], last, sl < nst);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    {
-        constexpr int per = LH_M * LH_BYTES / 16;  // chunks per stripe
-        const int n = nst * per;
-#pragma unroll
-        for (int q = 0; q < (LH_SPW * per + 63) / 64; ++q) {
-            const int j = 64 * q + lane;
-            if (j < n) {
-                const int js = j / per, t = j - js * per;
-                const lh_u32x4a v = *(const lh_u32x4a *)(slot + j * 16);
-                unsigned char *dst = out + (s0 + js) * out_stride + t * 16;
-#if LH_NT_ST
-                __builtin_nontemporal_store(v, (lh_u32x4a *)dst);
-#else
-                *(lh_u32x4a *)dst = v;
-#endif
-            }
-        }
-    }
+#if LH_CPS_FLAT && LH_CRP >= 1
+    // The recovery blocks leave through the slot, LH_CRP rows at a time ([stripe][row][bytes]
+    // images, 16-byte stores of contiguous runs; a stripe's rows are contiguous in memory).
+    lh_cps_flat<0>::run(acc, slot, out, out_stride, s0, nst, sl, c, last);
 #else
     if (sl >= nst) return;
     const int p = last ? LH_SUB - 8 : 8 * c;
@@ -911,336 +931,7 @@ __device__ __forceinline__ void lh_encode_wave_cps(long long wave, const unsigne
 #endif
 }
 #endif  // LH_CPS
-#if LH_LDS && LH_CPS > 1 && !LH_PTR && LH_PERS
-// Persistent form of the multi-column steps (LH_PERS = 1: each wave a contiguous run of
-// stripes; 2: stripe groups dealt round-robin over the waves).  The last step of a group,
-// once its slot is read, issues the next group's first step into it, then the group's
-// recovery blocks leave by per-lane stores from the accumulators, overlapping that step's
-// landing; no workgroup ends and restarts between groups.
-template <int T>
-struct lh_unroll_cpsp {
-    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], const lh_u32x4r &rs, const int (&voff)[LH_SQ],
-                                               unsigned char *slot, int lo, int lo8, bool first, bool more,
-                                               const lh_u32x4r &rsn, const int (&voffn)[LH_SQ]) {
-        if constexpr (T < LH_NSTEP) {
-            if (T == 0 && !first) lh_wait_vmcnt<LH_M * 8>();  // (the previous group's stores follow this DMA)
-            else lh_wait_vmcnt<0>();
-            asm volatile("" ::: "memory");
-            lh_cps_cols<T, 0>::run(acc, slot, lo, lo8);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done
-            if constexpr (T + 1 < LH_NSTEP) {
-                constexpr int x1 = (T + 1) * LH_CPS;
-#pragma unroll
-                for (int q = 0; q < LH_SQ; ++q) {
-                    int v = voff[q];
-                    if constexpr (T + 2 == LH_NSTEP && LH_LASTC < LH_CPS) {
-                        const int r = (64 * q + (int)(threadIdx.x & 63)) % LH_SCH;
-                        v = r < LH_LASTC * LH_CCH ? v : (int)0x80000000;
-                    }
-                    lh_dma16_bufs<LH_NT>(rs, v, x1 * LH_BYTES, slot + q * 1024);
-                }
-            } else {
-                if (more)
-#pragma unroll
-                    for (int q = 0; q < LH_SQ; ++q) lh_dma16_bufs<LH_NT>(rsn, voffn[q], 0, slot + q * 1024);
-            }
-            lh_unroll_cpsp<T + 1>::run(acc, rs, voff, slot, lo, lo8, first, more, rsn, voffn);
-        }
-    }
-};
-__device__ __forceinline__ void lh_cps_voff(int (&voff)[LH_SQ], int nst, long long in_stride) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int q = 0; q < LH_SQ; ++q) {
-        const int j = 64 * q + lane, js = j / LH_SCH, r = j - js * LH_SCH;
-        voff[q] = js < nst ? js * (int)in_stride + r * 16 : (int)0x80000000;
-    }
-}
-__device__ __forceinline__ void lh_encode_pers_cps(const unsigned char *__restrict__ in, long long in_stride,
-                                                   unsigned char *__restrict__ out, long long out_stride, int stripes) {
-    __shared__ __attribute__((aligned(16))) unsigned char lh_cring[4][LH_SSLOT];
-    const int lane = threadIdx.x & 63;
-    const int sl = lane / LH_NCH, c = lane - sl * LH_NCH;
-    const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
-    const long long w = (long long)__builtin_amdgcn_readfirstlane((int)((lh_block_id() * blockDim.x + threadIdx.x) >> 6));
-#if LH_PERS == 2
-    const long long s_lo = w * LH_SPW, s_hi = stripes, s_step = nw * LH_SPW;
-#else
-    const long long s_lo = w * stripes / nw, s_hi = (w + 1) * stripes / nw, s_step = LH_SPW;
-#endif
-    if (s_lo >= s_hi) return;
-    unsigned char *slot = lh_cring[threadIdx.x >> 6];
-    int voff[LH_SQ], voffn[LH_SQ];
-    int nst = (int)((s_hi - s_lo) < LH_SPW ? (s_hi - s_lo) : LH_SPW);
-    lh_u32x4r rs = lh_rsrc(in + s_lo * in_stride, (unsigned)(nst * in_stride));
-    lh_cps_voff(voff, nst, in_stride);
-#pragma unroll
-    for (int q = 0; q < LH_SQ; ++q) lh_dma16_bufs<LH_NT>(rs, voff[q], 0, slot + q * 1024);
-    const int lo = (sl < LH_SPW ? sl : LH_SPW - 1) * (LH_CPS * LH_BYTES) + 8 * c;
-    int lo8 = lo + 8;
-    asm volatile("" : "+v"(lo8));
-    const bool last = c == LH_NCH - 1;
-    const int p = last ? LH_SUB - 8 : 8 * c;
-    bool first = true;
-    for (long long s = s_lo; s < s_hi; s += s_step) {
-        const long long sn = s + s_step;
-        const bool more = sn < s_hi;
-        const int nstn = more ? (int)((s_hi - sn) < LH_SPW ? (s_hi - sn) : LH_SPW) : LH_SPW;
-        const lh_u32x4r rsn = lh_rsrc(in + (more ? sn : s) * in_stride, (unsigned)(nstn * in_stride));
-        if (nstn == LH_SPW) {
-#pragma unroll
-            for (int q = 0; q < LH_SQ; ++q) voffn[q] = voff[q];
-        } else {
-            lh_cps_voff(voffn, nstn, in_stride);
-        }
-        if (nst < LH_SPW && first) lh_cps_voff(voff, nst, in_stride);  // (already so: kept for clarity)
-        lh_word acc[LH_M][8];
-#pragma unroll
-        for (int r = 0; r < LH_M; ++r)
-#pragma unroll
-            for (int y = 0; y < 8; ++y)
-#pragma unroll
-                for (int i = 0; i < LH_NW; ++i) acc[r][y].v[i] = 0;
-        lh_unroll_cpsp<0>::run(acc, rs, voff, slot, lo, lo8, first, more, rsn, voffn);
-        if (sl < nst) {
-            unsigned char *o = out + (s + sl) * out_stride + p;
-#pragma unroll
-            for (int r = 0; r < LH_M; ++r)
-#pragma unroll
-                for (int y = 0; y < 8; ++y) {
-                    lh_word wv = acc[r][y];
-                    if constexpr (LH_VLAST != 8) {
-                        const lh_word f = lh_funnel<LH_VLAST>(lh_row_shr1(wv.v[0]), lh_row_shr1(wv.v[1]), wv.v[0], wv.v[1]);
-                        wv.v[0] = last ? f.v[0] : wv.v[0];
-                        wv.v[1] = last ? f.v[1] : wv.v[1];
-                    }
-                    lh_store(o + (long long)r * LH_BYTES + y * LH_SUB, wv);
-                }
-        }
-        rs = rsn;
-        nst = nstn;
-#pragma unroll
-        for (int q = 0; q < LH_SQ; ++q) voff[q] = voffn[q];
-        first = false;
-    }
-}
-#endif
 
-// ------------------------------------------------------------ persistent LDS encode
-// LH_PERS = 1 (jit.cpp: LDS encodes with k >= LH_LDE): the host launches as many workgroups
-// as stay resident (2 per CU at k29/m4) and wave w codes the stripes [w S / N, (w + 1) S / N)
-// of the N waves, LH_SPW at a time.  The column ring runs on across stripe groups: column t
-// of the wave's stream (t = group * LH_K + x) lands in slot t mod LH_LDE, and the last
-// LH_LDE - 1 columns of a group issue the first columns of the next one, so the next group's
-// loads are in flight while this group's recovery blocks are assembled and stored.  Those
-// leave row by row through the one free slot (the slot of the group's last column; a row of
-// the wave's stripes, LH_SPW x bytes, always fits a slot), whose DMA is issued after the last
-// row.  vmcnt counts stores and loads of a wave in issue order (gfx9 has one counter; LLVM's
-// waitcnt insertion makes the same assumption), so the waits of the next group's first
-// columns count the stores issued between their DMAs.  Every wave does the same work (32
-// stripes each at 65 536 stripes over 2 048 waves): no tail of partly filled rounds of
-// workgroups, and no workgroup launches after the first.
-#ifndef LH_PERS
-#define LH_PERS 0
-#endif
-#if LH_PERS
-#if LH_K < 2 * LH_LDE
-#error "LH_PERS: at least 2 LH_LDE columns (a group's prefetch reaches into the next group only)"
-#endif
-// Store instructions of one group's recovery rows (full groups: every one has a live lane).
-#define LH_PST (LH_M * LH_LQ)
-// Block-pointer rows of the group starting at stripe s (nst stripes; the slots past them
-// repeat the last stripe so that every DMA lane reads valid memory).
-__device__ __forceinline__ void lh_pers_rows(unsigned long long *prow, const unsigned char *__restrict__ in,
-                                             long long in_stride, unsigned char *__restrict__ out,
-                                             long long out_stride, long long s, int nst, int sl, int c) {
-    if (sl >= LH_SPW) return;
-    const long long st = s + (sl < nst ? sl : nst - 1);
-#if LH_PTR
-    const unsigned long long *it = (const unsigned long long *)(in + st * in_stride);
-    const unsigned long long *ot = (const unsigned long long *)(out + st * out_stride);
-    for (int x = c; x < LH_LPR; x += LH_NCH) prow[sl * LH_LPR + x] = x < LH_K ? it[x] : ot[x - LH_K];
-#else
-    for (int x = c; x < LH_LPR; x += LH_NCH)
-        prow[sl * LH_LPR + x] = x < LH_K ? (unsigned long long)(in + st * in_stride + (long long)x * LH_BYTES)
-                                         : (unsigned long long)(out + st * out_stride + (long long)(x - LH_K) * LH_BYTES);
-#endif
-}
-__device__ __forceinline__ void lh_wave_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-struct lh_pers_src {
-    const unsigned long long *pt, *ptn;  // LDS: this group's and the next group's pointer rows
-    int pr[LH_LQ], off[LH_LQ];
-    unsigned char *ring;
-    int rot;    // slot of the group's column 0
-    bool more;  // a next group exists (wave-uniform)
-    __device__ __forceinline__ unsigned char *slot(int xm) const {  // xm = x mod LH_LDE
-        int s = xm + rot;
-        s = s >= LH_LDE ? s - LH_LDE : s;
-        return ring + s * (LH_LQ * 1024);
-    }
-    __device__ __forceinline__ void addrs(const unsigned long long *p, int x, const unsigned char *(&a)[LH_LQ]) const {
-#pragma unroll
-        for (int q = 0; q < LH_LQ; ++q) a[q] = (const unsigned char *)p[pr[q] + x] + off[q];
-    }
-    __device__ __forceinline__ void issue(const unsigned char *const (&a)[LH_LQ], unsigned char *dst) const {
-#pragma unroll
-        for (int q = 0; q < LH_LQ; ++q)
-            lh_dma16<LH_NT>(a[q], dst + q * 1024);
-    }
-};
-// Column X of a group.  `after`: VMEM instructions issued after column X's DMAs and before
-// this wait: the next LH_LDE - 1 columns' DMAs, plus (first group excepted) the previous
-// group's stores for the columns whose DMAs preceded them.
-template <int X>
-struct lh_unroll_pers {
-    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], const lh_pers_src &S, int lo, int lo8, bool first) {
-        if constexpr (X < LH_K) {
-            constexpr int nx = X + LH_LDE;  // stream column this slot receives next
-            const unsigned char *a[LH_LQ];
-            if constexpr (nx < LH_K) S.addrs(S.pt, nx, a);
-            else if constexpr (X < LH_K - 1) {
-                if (S.more) S.addrs(S.ptn, nx - LH_K, a);
-            }
-            // Columns issued after X: min(LDE - 1, K - 1 - X) in this group, the rest in the next
-            // group (only if there is one) -- the last column's refill waits for the stores.
-            constexpr int own = (LH_LDE - 1) < (LH_K - 1 - X) ? (LH_LDE - 1) : (LH_K - 1 - X);
-            static_assert(LH_LQ * (LH_LDE - 1) + LH_PST <= 63, "vmcnt is 6 bits");
-            if (X < LH_LDE - 1 && !first) {
-                lh_wait_vmcnt<LH_LQ * (LH_LDE - 1) + LH_PST>();  // (LH_K >= 2 LH_LDE: own == LH_LDE - 1)
-            } else if (S.more || own == LH_LDE - 1) {
-                lh_wait_vmcnt<LH_LQ * (LH_LDE - 1)>();
-            } else {
-                lh_wait_vmcnt<LH_LQ * own>();
-            }
-            asm volatile("" ::: "memory");  // no LDS read moves above the wait
-            unsigned char *sl = S.slot(X % LH_LDE);
-            lh_word d[8];
-            lh_slot_col(d, sl, lo, lo8);
-            lh_column<X>(acc, d);
-            lh_opaque(acc);
-            if constexpr (nx < LH_K) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done
-                S.issue(a, sl);
-            } else if constexpr (X < LH_K - 1) {
-                if (S.more) {
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    S.issue(a, sl);
-                }
-            }
-            lh_unroll_pers<X + 1>::run(acc, S, lo, lo8, first);
-        }
-    }
-};
-
-__device__ __forceinline__ void lh_encode_pers(const unsigned char *__restrict__ in, long long in_stride,
-                                               unsigned char *__restrict__ out, long long out_stride, int stripes) {
-    __shared__ __attribute__((aligned(16))) unsigned char lh_pring[4][LH_LDE * LH_LQ * 1024 + LH_LPAD];
-    __shared__ unsigned long long lh_ppt[4][2][LH_SPW * LH_LPR];
-    const int lane = threadIdx.x & 63;
-    const int sl = lane / LH_NCH, c = lane - sl * LH_NCH;
-    const int wid = threadIdx.x >> 6;
-    const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
-    const long long w = (long long)__builtin_amdgcn_readfirstlane((int)((lh_block_id() * blockDim.x + threadIdx.x) >> 6));
-#if LH_PERS == 2
-    // (probe) groups dealt round-robin: group i of the wave is group w + i nw of the batch
-    const long long s_lo = w * LH_SPW, s_hi = stripes, s_step = nw * LH_SPW;
-#else
-    const long long s_lo = w * stripes / nw, s_hi = (w + 1) * stripes / nw, s_step = LH_SPW;  // wave-uniform
-#endif
-    if (s_lo >= s_hi) return;
-    lh_pers_src S;
-    S.ring = lh_pring[wid];
-    S.rot = 0;
-    unsigned long long *rows0 = lh_ppt[wid][0], *rows1 = lh_ppt[wid][1];
-#pragma unroll
-    for (int q = 0; q < LH_LQ; ++q) {  // every lane moves chunks, whatever its own stripe
-        int j = 64 * q + lane;
-        if (j >= LH_SPW * (LH_BYTES / 16)) j = LH_SPW * (LH_BYTES / 16) - 1;  // (lands past the image)
-        const int js = j / (LH_BYTES / 16);
-        S.pr[q] = js * LH_LPR;
-        S.off[q] = (j - js * (LH_BYTES / 16)) * 16;
-    }
-    const int lo = (sl < LH_SPW ? sl : LH_SPW - 1) * LH_BYTES + 8 * c;
-    int lo8 = lo + 8;
-    asm volatile("" : "+v"(lo8));
-    const bool last = c == LH_NCH - 1;
-    // Group 0: its rows and its first LH_LDE columns.
-    {
-        const int nst = (int)((s_hi - s_lo) < LH_SPW ? (s_hi - s_lo) : LH_SPW);
-        lh_pers_rows(rows0, in, in_stride, out, out_stride, s_lo, nst, sl, c);
-        lh_wave_fence();
-        S.pt = rows0;
-#pragma unroll
-        for (int q = 0; q < LH_LDE; ++q) {
-            const unsigned char *a[LH_LQ];
-            S.addrs(S.pt, q, a);
-            S.issue(a, S.ring + q * (LH_LQ * 1024));
-        }
-    }
-    bool first = true;
-    for (long long s = s_lo; s < s_hi; s += s_step) {
-        const int nst = (int)((s_hi - s) < LH_SPW ? (s_hi - s) : LH_SPW);
-        const long long sn = s + s_step;
-        S.more = sn < s_hi;
-        unsigned long long *nrows = (S.pt == rows0) ? rows1 : rows0;
-        if (S.more) {
-            // (the next group's rows: its previous user, the group before this one, is done)
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            lh_pers_rows(nrows, in, in_stride, out, out_stride, sn, (int)((s_hi - sn) < LH_SPW ? (s_hi - sn) : LH_SPW),
-                         sl, c);
-            lh_wave_fence();
-        }
-        S.ptn = nrows;
-        lh_word acc[LH_M][8];
-#pragma unroll
-        for (int r = 0; r < LH_M; ++r)
-#pragma unroll
-            for (int y = 0; y < 8; ++y)
-#pragma unroll
-                for (int i = 0; i < LH_NW; ++i) acc[r][y].v[i] = 0;
-        lh_unroll_pers<0>::run(acc, S, lo, lo8, first);
-        // Recovery rows through the free slot (the last column's), one row at a time.
-        unsigned char *fs = S.slot((LH_K - 1) % LH_LDE);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last column's reads are done
-        constexpr int per = LH_BYTES / 16;  // chunks per block
-        const int n = nst * per;
-#pragma unroll
-        for (int r = 0; r < LH_M; ++r) {
-            lh_img_row<0>(fs + (sl < LH_SPW ? sl : LH_SPW - 1) * LH_BYTES + (last ? LH_SUB - 8 : 8 * c), acc[r], last,
-                          sl < nst);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the row's image is complete
-#pragma unroll
-            for (int q = 0; q < LH_LQ; ++q) {
-                const int j = 64 * q + lane;
-                if (j < n) {
-                    const int js = j / per, t = j - js * per;
-                    const lh_u32x4a v = *(const lh_u32x4a *)(fs + j * 16);
-                    unsigned char *dst = (unsigned char *)S.pt[js * LH_LPR + LH_K + r] + t * 16;
-#if LH_NT_ST
-                    __builtin_nontemporal_store(v, (lh_u32x4a *)dst);
-#else
-                    *(lh_u32x4a *)dst = v;
-#endif
-                }
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done
-        }
-        if (S.more) {  // the free slot's refill: the next group's column LH_LDE - 1
-            const unsigned char *a[LH_LQ];
-            S.addrs(S.ptn, LH_LDE - 1, a);
-            S.issue(a, fs);
-        }
-        S.pt = nrows;
-        S.rot = (S.rot + LH_K % LH_LDE) % LH_LDE;
-        first = false;
-    }
-}
-#endif  // LH_PERS
 #endif
 
 __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned char *__restrict__ in,
@@ -1309,11 +1000,7 @@ __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned ch
 extern "C" __global__ void __launch_bounds__(256, LH_ENC_LB)
 lh_jit_encode(const unsigned char *__restrict__ in, long long in_stride,
               unsigned char *__restrict__ out, long long out_stride, int stripes) {
-#if LH_LDS && LH_PERS && LH_CPS > 1 && !LH_PTR
-    lh_encode_pers_cps(in, in_stride, out, out_stride, stripes);
-#elif LH_LDS && LH_PERS
-    lh_encode_pers(in, in_stride, out, out_stride, stripes);
-#elif LH_LDS && LH_CPS > 1 && !LH_PTR
+#if LH_LDS && LH_CPS > 1 && !LH_PTR
     LH_WAVE_LOOP(stripes) { lh_encode_wave_cps(lh_w, in, in_stride, out, out_stride, stripes); }
 #elif LH_LDS
     LH_WAVE_LOOP(stripes) { lh_encode_wave_lds(lh_w, in, in_stride, out, out_stride, stripes); }

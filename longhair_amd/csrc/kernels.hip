@@ -1194,8 +1194,8 @@ __global__ void __launch_bounds__(1024) lh_apply_jump_kernel(lh::JumpApplyArgs a
         : "=s"(tlo), "=s"(thi)
         :
         : "s92", "s93", "scc");
-    if (tlo > 0xFFFFFFFFu - 256u * 68u) {  // the table straddles a 4 GiB boundary (never seen)
-        lh_apply_jump_body<false, PTR>(a, tlo, thi);
+    if (a.jump_fallback || tlo > 0xFFFFFFFFu - 256u * 68u) {  // the table straddles a 4 GiB boundary
+        lh_apply_jump_body<false, PTR>(a, tlo, thi);              // (never seen), or the tests' switch
         return;
     }
     lh_apply_jump_body<true, PTR>(a, tlo, thi);
@@ -1534,11 +1534,14 @@ hipError_t launch_apply_jump(const JumpApplyArgs &a, hipStream_t st) {
     if (wgs > 0x7FFFFFFF) return hipErrorInvalidValue;
     JumpApplyArgs g = a;
     if (!order_stripes(g.order, a.plan, a.plan_stride, a.per_stripe ? a.stripes : 0, a.n_out, st)) g.order = nullptr;
+    const char *fb = std::getenv("LONGHAIR_AMD_INV_FALLBACK");  // (tests: the in-asm table)
+    g.jump_fallback = fb && std::atoi(fb) ? 1 : 0;
     if (a.in_ptrs)
         hipLaunchKernelGGL(lh_apply_jump_kernel<true>, dim3((unsigned)wgs), dim3(64u * (unsigned)ng), 0, st, g);
     else
         hipLaunchKernelGGL(lh_apply_jump_kernel<false>, dim3((unsigned)wgs), dim3(64u * (unsigned)ng), 0, st, g);
-    note_launch(a.in_ptrs ? "lh_apply_jump_kernel(pointer table)" : "lh_apply_jump_kernel");
+    note_launch(g.jump_fallback ? (a.in_ptrs ? "lh_apply_jump_kernel(pointer table, fallback)" : "lh_apply_jump_kernel(fallback)")
+                                : (a.in_ptrs ? "lh_apply_jump_kernel(pointer table)" : "lh_apply_jump_kernel"));
     return hipGetLastError();
 }
 

@@ -82,6 +82,8 @@ struct JumpApplyArgs {
                                   // first (written by launch_apply_jump), or NULL: stripe order
     int dw;                       // bytes per lane per sub-block / 4: 1 (nch = ceil(sub / 4)) or
                                   // 2 (nch = ceil(sub / 8), the two-dword table, sub >= 8)
+    int jump_fallback;            // dw 1: the in-asm table (set by launch_apply_jump from
+                                  // LONGHAIR_AMD_INV_FALLBACK, tests), as a straddling table would
 };
 
 struct XorArgs {

@@ -10,9 +10,9 @@ import lhutil
 REPO = lhutil.REPO
 
 
-def _declared_functions():
+def _declared_functions(headers=("cauchy_256.h", "cauchy_256_batch.h", "cauchy_256_dispatch.h")):
     names = set()
-    for h in ("cauchy_256.h", "cauchy_256_batch.h", "cauchy_256_dispatch.h", "cauchy_256_test.h"):
+    for h in headers:
         text = open(os.path.join(REPO, "include", h)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         for m in re.finditer(r"^\s*(?:extern\s+)?(?:const\s+)?\w+\s*\*?\s*(\w+)\s*\(", text, flags=re.M):
@@ -35,6 +35,12 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
     assert set(_native.EXPORTS) == _declared_functions()
     assert longhair_amd.lib() is not None
+    # the test-only header's hooks: in the checked build, not in the product
+    hooks = _declared_functions(("cauchy_256_test.h",))
+    assert set(_native.OPTIONAL_EXPORTS) == hooks
+    check = ctypes.CDLL(os.path.join(os.path.dirname(_native.library_path), "liblonghair_amd_check.so"))
+    for name in hooks:
+        assert hasattr(check, name) and not hasattr(lib, name), name
 
 
 def test_block_layout_matches_reference():
@@ -146,7 +152,12 @@ def test_no_exception_crosses_the_abi():
     injected by the test-only hook at the start of the guarded body) comes back as -3 with
     cauchy_256_last_error() naming it, never as std::terminate in the caller."""
     import longhair_amd
-    lib = longhair_amd.lib()
+    from longhair_amd import _native
+    # the hook is built into the checked library only (LH_TEST_HOOKS); the product has none
+    assert not hasattr(longhair_amd.lib(), "cauchy_256_debug_throw_next")
+    check = os.path.join(os.path.dirname(longhair_amd.library_path), "liblonghair_amd_check.so")
+    assert os.path.exists(check), "build the checked library (__graft_entry__.build())"
+    lib = _native.bind(ctypes.CDLL(check))
     buf = (ctypes.c_ubyte * 64)()
     tab = (ctypes.c_void_p * 8)()
     blocks = (lhutil.Block * 4)()

@@ -31,6 +31,7 @@ GENERIC_S8 = ["lh_plan_small_kernel<8>", "lh_apply_jump_kernel"]
 OLD_CF = ["lh_plan_kernel(closed form)", "lh_apply_generic_kernel", "lh_scatter_kernel"]
 JUMP = ["lh_apply_jump_kernel"]
 JUMP2 = ["lh_apply_jump2_kernel"]  # two-dword lanes (codec.cpp jump_layout)
+JUMP_FB = ["lh_apply_jump_kernel(fallback)"]  # the in-asm table (LONGHAIR_AMD_INV_FALLBACK)
 GEN = {"LONGHAIR_AMD_PATH": "generic"}
 PS4_JUMP = ["lh_plan_small_kernel<4>", "lh_apply_jump_kernel"]
 PS4_JUMP2 = ["lh_plan_small_kernel<4>", "lh_apply_jump2_kernel"]
@@ -89,7 +90,8 @@ BOUNDARIES = [
     ("jump2-n5-sub520", 40, 5, 4160, 8, GEN, JUMP, PS8_JUMP),
     ("jump2-n4-sub516", 40, 4, 4128, 8, GEN, JUMP2, PS4_JUMP),  # (sub % 8 = 4, nch 65: lone)
     # the in-asm one-dword table (and the address-probe fallback) for every jump apply
-    ("jump2-n4-fallback", 40, 4, 4160, 8, dict(GEN, LONGHAIR_AMD_INV_FALLBACK="1"), JUMP, PS4_JUMP),
+    ("jump2-n4-fallback", 40, 4, 4160, 8, dict(GEN, LONGHAIR_AMD_INV_FALLBACK="1"), JUMP_FB,
+     ["lh_plan_small_kernel<4>", "lh_apply_jump_kernel(fallback)"]),
     # phase B: V rows staged 16 at a time for e_max <= 32, all at once above
     ("jump-emax32", 40, 32, 2048, 8, {}, ["lh_jit_encode_win"], WIDE16),
     ("jump-emax33", 40, 33, 2048, 8, {}, ["lh_jit_encode_win"], WIDE64),
