@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <deque>
 #include <functional>
 #include <sstream>
@@ -106,21 +107,32 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     cfg->plain = decode && !(emax <= 4 && nch2 <= 64 && k <= 64 && std::getenv("LONGHAIR_AMD_NO_FUSED_PLAN") == nullptr);
     cfg->defines.clear();
     if (const char *d = std::getenv("LONGHAIR_AMD_JIT_DEFINES")) cfg->defines = d;
-    // Resident encode workgroups per CU (dynamic LDS pads the rest): a tuning define for now.
-    {
-        const size_t at = cfg->defines.find("LH_WGCU=");
-        cfg->wgcu = at == std::string::npos ? 0 : std::atoi(cfg->defines.c_str() + at + 8);
-    }
-    if (!decode && cfg->lds) {
-        const size_t at = cfg->defines.find("LH_WPB=");
-        const int wpb = at == std::string::npos ? 4 : std::atoi(cfg->defines.c_str() + at + 7);
-        cfg->enc_wpb = (wpb >= 1 && wpb <= 4 && cfg->defines.find("LH_CPS=") != std::string::npos) ? wpb : 4;
-    }
+    // The LDS encode of strided batches fetches LH_CPS = 5 columns per DMA step (one step in
+    // flight) and runs one 4-wave workgroup per CU (dynamic LDS pads the rest): k29/m4 encode
+    // 0.502-0.509 -> 0.489-0.491 ms against the one-column ring at two workgroups per CU
+    // (profiles/r9e_tune_k29m4_cps.txt; 3 columns 0.496, 4: 0.501, 6: 0.498, 7: 0.513; two
+    // workgroups per CU 0.534; jit_codec.hip LH_CPS).  At least two steps (k >= 4).
+    // Tuning overrides in LONGHAIR_AMD_JIT_DEFINES: LH_CPS=, LH_WGCU=, LH_WPB=.
+    auto knob = [&](const char *name, int dflt) {
+        const size_t at = cfg->defines.find(name);
+        return at == std::string::npos ? dflt : std::atoi(cfg->defines.c_str() + at + std::strlen(name));
+    };
+    cfg->cps = 1;
+    if (!decode && cfg->lds) cfg->cps = std::max(1, std::min(5, k / 2));
+    cfg->cps = knob("LH_CPS=", cfg->cps);
+    if (cfg->cps > 1 && !(!decode && cfg->lds && k >= 2 * cfg->cps)) cfg->cps = 1;
+    cfg->wgcu = knob("LH_WGCU=", cfg->cps > 1 ? 1 : 0);
+    const int wpb = knob("LH_WPB=", 4);
+    cfg->enc_wpb = (cfg->cps > 1 && wpb >= 1 && wpb <= 4) ? wpb : 4;
     return true;
 }
 
 bool jit_ptr_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     if (!jit_config_for(k, m, bytes, decode, cfg)) return false;
+    // (the multi-column steps read a stripe's columns as one contiguous run: strided batches only)
+    cfg->cps = 1;
+    cfg->enc_wpb = 4;
+    if (cfg->defines.find("LH_WGCU=") == std::string::npos) cfg->wgcu = 0;
     if ((long long)(cfg->spw ? cfg->spw : 1) * k > 1024) return false;  // LDS: 4 waves x 8 B x spw x (k + 1) <= 35 KiB
     cfg->ptr = 1;
     // LDS staging as for strided batches (the encode's pointer rows already counted by
@@ -529,6 +541,7 @@ std::string jit_source_for(const JitConfig &c) {
        << "\n#define LH_SPW " << (c.spw ? c.spw : 1) << "\n#define LH_WPS " << (c.wps ? c.wps : 1) << "\n";
     if (c.ptr) os << "#define LH_PTR 1\n#define LH_BUF 0\n";
     if (c.lds) os << "#ifndef LH_LDS\n#define LH_LDS 1\n#endif\n";  // (a LONGHAIR_AMD_JIT_DEFINES value wins)
+    if (c.cps > 1 && !c.ptr) os << "#ifndef LH_CPS\n#define LH_CPS " << c.cps << "\n#endif\n";
     if (c.role) os << "#define LH_ROLE " << c.role << "\n#define LH_DEC_PLAIN " << c.plain << "\n";
     const std::vector<uint8_t> g = generator_matrix(c.k, c.m);
     os << "static constexpr unsigned char LH_BM[" << c.m << "][" << c.k << "][8] = {";

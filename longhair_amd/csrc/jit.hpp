@@ -36,6 +36,7 @@ struct JitConfig {
     int plain = 0;
     int wgcu = 0;         // register networks: resident workgroups per CU of the module's kernel,
                           // forced by dynamic LDS (0: natural)
+    int cps = 1;          // LDS encode of strided batches: columns per DMA step (LH_CPS)
     int enc_wpb = 4;      // encode: waves per workgroup (LH_WPB, multi-column-step encode only)
     int lanes_per_launch_unit() const { return 64; }
 };

@@ -546,13 +546,20 @@ __device__ __forceinline__ void lh_lds_put(unsigned char *p, const lh_word &w) {
 // advanced by x * bytes (profiles/r7q_tune_k29m4_erows.txt; found because the pointer-table
 // form ran faster, r7n_seq_probe_ptr.txt; padding the ring to the same LDS size: no change).
 // One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4): `lds` the wave-uniform LDS address
-// of lane 0's 16 bytes.  Issued from inline asm so the compiler does not see an LDS write in
-// flight: with the builtin, its waitcnt pass could not tell a ring slot being read from the
-// slots being filled (one __shared__ array) and put s_waitcnt vmcnt(0) before every column's
-// first LDS read, draining the whole ring once per column.  Landing is ordered by the kernels'
-// own counted vmcnt waits (lh_wait_vmcnt) instead.
+// of lane 0's 16 bytes.
+// Round 6 found that with the builtin, hipcc's waitcnt pass cannot tell a ring slot being read
+// from the slots being filled (one __shared__ array) and puts s_waitcnt vmcnt(0) before every
+// column's first LDS read: the "4-slot ring" of the one-column kernels ran one column per wave
+// at a time.  Issued from inline asm (LH_ASM_DMA=1) the compiler sees no LDS write in flight
+// and the kernels' own counted waits (lh_wait_vmcnt) order the landing, so the ring really
+// runs 3 columns deep -- and measured SLOWER: encode 0.533 against 0.501 ms, decode 0.566
+// against 0.554 (ring depth 2 / 3: 0.562 / 0.557; profiles/r9a_tune_k29m4_asm_dma.txt).  The
+// HBM stream of this access pattern prefers fewer, longer runs in flight over deeper
+// prefetch (tools/ubench_r6.hip), which the multi-column steps below turn into a design:
+// they issue their DMAs from asm (lh_dma16_bufs) with one step in flight by construction.
+// The builtin (with its drain) stays the default of the one-column kernels.
 #ifndef LH_ASM_DMA
-#define LH_ASM_DMA 1
+#define LH_ASM_DMA 0
 #endif
 template <int NT>
 __device__ __forceinline__ void lh_dma16(const void *src, const void *lds) {
@@ -610,11 +617,24 @@ __device__ __forceinline__ void lh_dma16_buf(const lh_u32x4r &rs, int voff, cons
         asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "{m0}"(m) : "memory");
 }
 // ... with a wave-uniform byte offset `soff` added (SGPR soffset).
+#ifndef LH_CPS_POLI
+#define LH_CPS_POLI 0  // cache policy of the multi-column-step DMAs: 0 nt, 1 sc1 nt, 2 sc0 nt, 3 sc0 sc1 nt
+#endif
+#if LH_CPS_POLI == 1
+#define LH_CPS_POL "sc1 nt"
+#elif LH_CPS_POLI == 2
+#define LH_CPS_POL "sc0 nt"
+#elif LH_CPS_POLI == 3
+#define LH_CPS_POL "sc0 sc1 nt"
+#else
+#define LH_CPS_POL "nt"
+#endif
 template <int NT>
 __device__ __forceinline__ void lh_dma16_bufs(const lh_u32x4r &rs, int voff, int soff, const void *lds) {
     const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)lds);
     if constexpr (NT)
-        asm volatile("buffer_load_dwordx4 %0, %1, %2 offen nt lds" ::"v"(voff), "s"(rs), "s"(soff), "{m0}"(m) : "memory");
+        asm volatile("buffer_load_dwordx4 %0, %1, %2 offen " LH_CPS_POL " lds" ::"v"(voff), "s"(rs), "s"(soff), "{m0}"(m)
+                     : "memory");
     else
         asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rs), "s"(soff), "{m0}"(m) : "memory");
 }
@@ -811,27 +831,48 @@ struct lh_cps_cols {
         }
     }
 };
+#ifndef LH_CPS_AHEAD
+#define LH_CPS_AHEAD 0  // 1: two slots, step T + 1 issued before step T is combined (tools/tune.py)
+#endif
+// Step T1's DMAs into `slot` (the last step's chunks past column LH_K out of range).
+template <int T1>
+__device__ __forceinline__ void lh_cps_issue(const lh_u32x4r &rs, const int (&voff)[LH_SQ], unsigned char *slot) {
+    constexpr int x1 = T1 * LH_CPS;  // first column of the step
+#pragma unroll
+    for (int q = 0; q < LH_SQ; ++q) {
+        int v = voff[q];
+        if constexpr (T1 + 1 == LH_NSTEP && LH_LASTC < LH_CPS) {  // last step: columns < LH_K only
+            const int r = (64 * q + (int)(threadIdx.x & 63)) % LH_SCH;
+            v = r < LH_LASTC * LH_CCH ? v : (int)0x80000000;
+        }
+        lh_dma16_bufs<LH_NT>(rs, v, x1 * LH_BYTES, slot + q * 1024);
+    }
+}
 template <int T>
 struct lh_unroll_cps {
     __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], const lh_u32x4r &rs, const int (&voff)[LH_SQ],
                                                unsigned char *slot, int lo, int lo8) {
         if constexpr (T < LH_NSTEP) {
+#if LH_CPS_AHEAD
+            unsigned char *cur = slot + (T & 1) * LH_SSLOT;
+            if constexpr (T + 1 < LH_NSTEP) {
+                lh_cps_issue<T + 1>(rs, voff, slot + ((T + 1) & 1) * LH_SSLOT);  // (its slot was read at T - 1)
+                lh_wait_vmcnt<LH_SQ>();  // step T landed, T + 1 in flight
+            } else {
+                lh_wait_vmcnt<0>();
+            }
+            asm volatile("" ::: "memory");
+            lh_cps_cols<T, 0>::run(acc, cur, lo, lo8);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done
+#else
             lh_wait_vmcnt<0>();  // this step's DMAs landed (the only ones in flight)
             asm volatile("" ::: "memory");
             lh_cps_cols<T, 0>::run(acc, slot, lo, lo8);
             if constexpr (T + 1 < LH_NSTEP) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done
-                constexpr int x1 = (T + 1) * LH_CPS;  // first column of the next step
-#pragma unroll
-                for (int q = 0; q < LH_SQ; ++q) {
-                    int v = voff[q];
-                    if constexpr (T + 2 == LH_NSTEP && LH_LASTC < LH_CPS) {  // last step: columns < LH_K only
-                        const int r = (64 * q + (int)(threadIdx.x & 63)) % LH_SCH;
-                        v = r < LH_LASTC * LH_CCH ? v : (int)0x80000000;
-                    }
-                    lh_dma16_bufs<LH_NT>(rs, v, x1 * LH_BYTES, slot + q * 1024);
-                }
+                lh_cps_issue<T + 1>(rs, voff, slot);
             }
+#endif
             lh_unroll_cps<T + 1>::run(acc, rs, voff, slot, lo, lo8);
         }
     }
@@ -878,7 +919,7 @@ struct lh_cps_flat {
 __device__ __forceinline__ void lh_encode_wave_cps(long long wave, const unsigned char *__restrict__ in,
                                                    long long in_stride, unsigned char *__restrict__ out,
                                                    long long out_stride, int stripes) {
-    __shared__ __attribute__((aligned(16))) unsigned char lh_cring[LH_WPB][LH_SSLOT];
+    __shared__ __attribute__((aligned(16))) unsigned char lh_cring[LH_WPB][(1 + LH_CPS_AHEAD) * LH_SSLOT];
     const int lane = threadIdx.x & 63;
     const int sl = lane / LH_NCH, c = lane - sl * LH_NCH;
     const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)wave) * LH_SPW;  // wave-uniform

@@ -670,6 +670,17 @@ KNOB_VARIANTS = [
     # the LDS-staged forms' other ring depth, cache policy, column order and direct stores
     ("defines-ld2-nt0-ldsrecfirst-direct", {"LONGHAIR_AMD_JIT_DEFINES": "LH_LD=2,LH_NT=0,LH_LDS_NT_DEC=0,LH_LDS_REC_FIRST=1,LH_LDS_FLAT_ST=0"},
      ["lh_jit_decode_fused"]),
+    # the decode ring refilled one and three slots at a time (default two, LH_LDG)
+    ("defines-ldg1", {"LONGHAIR_AMD_JIT_DEFINES": "LH_LDG=1"}, ["lh_jit_decode_fused"]),
+    ("defines-ldg3", {"LONGHAIR_AMD_JIT_DEFINES": "LH_LDG=3"}, ["lh_jit_decode_fused"]),
+    # DMAs from asm (no compiler drain: the rings really run LH_LD - 1 columns deep, counted waits)
+    ("defines-asm-dma", {"LONGHAIR_AMD_JIT_DEFINES": "LH_ASM_DMA=1"}, ["lh_jit_decode_fused"]),
+    # the encode's one-column ring (LH_CPS=1; the pointer-table encode's form) and other
+    # multi-column-step shapes: 3 columns (partial last step), 2-wave workgroups, two slots,
+    # slot-image stores
+    ("defines-cps1", {"LONGHAIR_AMD_JIT_DEFINES": "LH_CPS=1"}, ["lh_jit_decode_fused"]),
+    ("defines-cps3-wpb2-ahead-flat", {"LONGHAIR_AMD_JIT_DEFINES": "LH_CPS=3,LH_WPB=2,LH_WGCU=2,LH_CPS_AHEAD=1,LH_CPS_FLAT=1"},
+     ["lh_jit_decode_fused"]),
 ]
 
 

@@ -24,7 +24,29 @@ PTR_SHAPES = [(29, 4, 1296), (29, 8, 1296), (10, 6, 24), (64, 5, 4096), (64, 3, 
 # Modules of the knob variants the GPU tests run (tests/test_gpu_parity.py KNOB_VARIANTS).
 KNOB_JOBS = [((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_LDS=0,LH_PF=2,LH_NT=0,LH_XCD=0"}),
              ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_LDS=0,LH_REC_FIRST=0,LH_PF_DEC=2"}),
-             ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_LD=2,LH_NT=0,LH_LDS_NT_DEC=0,LH_LDS_REC_FIRST=1,LH_LDS_FLAT_ST=0"})]
+             ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_LD=2,LH_NT=0,LH_LDS_NT_DEC=0,LH_LDS_REC_FIRST=1,LH_LDS_FLAT_ST=0"}),
+             ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_LDG=1"}),
+             ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_LDG=3"}),
+             ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_ASM_DMA=1"}),
+             ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_CPS=1"}),
+             ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_CPS=3,LH_WPB=2,LH_WGCU=2,LH_CPS_AHEAD=1,LH_CPS_FLAT=1"})]
+
+
+def lds_sample(n, seed=606):
+    """A seeded sample of n shapes served by the LDS-staged register networks:
+    k in [2, 64], m in [2, 4], 16-byte-multiple blocks up to 4 KiB; encode lh_jit_encode and
+    decode lh_jit_decode_fused, both staging their columns by LDS-DMA."""
+    import numpy as np
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = []
+    while len(out) < n:
+        k, m, b = int(rng.integers(2, 65)), int(rng.integers(2, 5)), 16 * int(rng.integers(1, 257))
+        if (k, m, b) in out:
+            continue
+        if (lh.batch_path(k, m, b) == "jit" and lh.batch_path(k, m, b, True) == "jit-fused"
+                and lh.lds_staged(k, m, b) and lh.lds_staged(k, m, b, True)):
+            out.append((k, m, b))
+    return out
 
 
 def boundary_jobs():
@@ -55,6 +77,24 @@ def main():
                 os.unlink(p)
                 print("pruned", f)
         return
+    if sys.argv[1:2] == ["--lds-sample"]:
+        # tools/stress.py --lds-sample N: the sample's encode and decode modules (and the
+        # pointer-table forms of the first quarter), largest first, on every core
+        n = int(sys.argv[2])
+        shapes = lds_sample(n)
+        jobs_list = [(sh, part, {}) for sh in shapes for part in ("enc", "dec")]
+        jobs_list += [(sh, part, {"LONGHAIR_AMD_PRECOMPILE_PTR": "1"}) for sh in shapes[:n // 4] for part in ("enc", "dec")]
+        jobs_list.sort(key=lambda j: -j[0][0] * j[0][2])
+        cmd = [sys.executable, os.path.abspath(__file__)]
+
+        def run1(job):
+            shape, part, extra = job
+            env = dict(os.environ, LONGHAIR_AMD_PRECOMPILE_PART=part, **extra)
+            return subprocess.run(cmd + [str(v) for v in shape], env=env, stdout=subprocess.DEVNULL)
+        with ThreadPoolExecutor(max(1, min(8, os.cpu_count() or 2))) as pool:
+            runs = list(pool.map(run1, jobs_list))
+        print(f"{len(shapes)} shapes, {len(jobs_list)} modules, {sum(r.returncode != 0 for r in runs)} failed")
+        sys.exit(1 if any(r.returncode for r in runs) else 0)
     if sys.argv[1:] == ["--all"]:
         # One child process per (shape, part), largest network first (k * m): hiprtc is
         # single-threaded and the big modules take minutes, so the rest compile beside them

@@ -5,7 +5,11 @@ the generic kernels for the rest -- encode + decode random stripes (random erasu
 recovery rows and slot order) through the strided batch calls, compare a sample of stripes
 with the C oracle, and run the same inputs through the pointer-table calls on scattered
 blocks, which must give identical bytes, rows and status.
-Usage: python tools/stress.py SECONDS [SEED]   (prints one line per shape, FAIL lines on mismatch)"""
+Usage: python tools/stress.py SECONDS [SEED] [--lds-sample N]   (prints one line per shape, FAIL lines
+on mismatch, then a count of the shapes each kernel served)
+--lds-sample N: draw the shapes from the first N of tools/precompile.py's seeded sample of
+LDS-staged register-network shapes (lds_sample(): encode lh_jit_encode, decode
+lh_jit_decode_fused, 16-byte-multiple blocks), whose modules that tool compiles beforehand."""
 import os
 import sys
 import time
@@ -49,12 +53,18 @@ def gather(place):
     return out.view(S, n, B)
 
 
-def one(rng, oracle):
-    k = int(rng.choice([2, 3, 5, 8, 12, 17, 29, 40, 64, 100, 128, 200]))
-    m = int(rng.choice([1, 2, 3, 4, 6, 8, 12, 16, 20, 32]))
-    if k + m > 256:
-        m = 256 - k
-    nbytes = 8 * int(rng.choice([1, 2, 3, 21, 64, 162, 256, 512, 1024]))
+COUNTS = {}
+
+
+def one(rng, oracle, shapes=None):
+    if shapes:
+        k, m, nbytes = shapes[int(rng.integers(0, len(shapes)))]
+    else:
+        k = int(rng.choice([2, 3, 5, 8, 12, 17, 29, 40, 64, 100, 128, 200]))
+        m = int(rng.choice([1, 2, 3, 4, 6, 8, 12, 16, 20, 32]))
+        if k + m > 256:
+            m = 256 - k
+        nbytes = 8 * int(rng.choice([1, 2, 3, 21, 64, 162, 256, 512, 1024]))
     stripes = int(rng.integers(1, 40))
     g = torch.Generator(device="cuda").manual_seed(int(rng.integers(1 << 30)))
     data = torch.randint(0, 256, (stripes, k, nbytes), dtype=torch.uint8, device="cuda", generator=g)
@@ -96,22 +106,34 @@ def one(rng, oracle):
     torch.cuda.synchronize()
     if not (torch.equal(pstat, sstat) and torch.equal(pr, sr) and torch.equal(gather(place), sb)):
         bad.append("decode_ptrs")
+    for name in set(enc_trace) | set(dec_trace) | set(ptr_trace):
+        COUNTS[name] = COUNTS.get(name, 0) + 1
     print(f"k={k} m={m} bytes={nbytes} stripes={stripes} enc={'+'.join(enc_trace)} dec={'+'.join(dec_trace)} "
           f"ptr={'+'.join(ptr_trace)} {'FAIL ' + ','.join(bad) if bad else 'ok'}", flush=True)
     return not bad
 
 
 def main():
-    secs = float(sys.argv[1]) if len(sys.argv) > 1 else 60
-    seed = int(sys.argv[2]) if len(sys.argv) > 2 else int(time.time())
-    print(f"seed {seed}", flush=True)
+    args = list(sys.argv[1:])
+    shapes = None
+    if "--lds-sample" in args:
+        i = args.index("--lds-sample")
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        import precompile
+        shapes = precompile.lds_sample(int(args[i + 1]))
+        del args[i:i + 2]
+    secs = float(args[0]) if len(args) > 0 else 60
+    seed = int(args[1]) if len(args) > 1 else int(time.time())
+    print(f"seed {seed}" + (f", {len(shapes)} LDS-sample shapes" if shapes else ""), flush=True)
     rng = np.random.Generator(np.random.PCG64(seed))
     assert lh.cauchy_256_init() == 0
     oracle = lhutil.Oracle()
     t0, n, fails = time.time(), 0, 0
     while time.time() - t0 < secs:
         n += 1
-        fails += 0 if one(rng, oracle) else 1
+        fails += 0 if one(rng, oracle, shapes) else 1
+    print("kernels (shapes served): " + ", ".join(f"{k} {v}" for k, v in sorted(COUNTS.items(), key=lambda kv: -kv[1])),
+          flush=True)
     print(f"{n} shapes, {fails} failed", flush=True)
     sys.exit(1 if fails else 0)
 
