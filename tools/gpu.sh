@@ -78,6 +78,14 @@ for step in "$@"; do
       csvf=$(find "$OUT/sq_$cfg/p1" -name "*counter_collection.csv" | head -1)
       python3 tools/sq_summary.py "$csvf" "$cfg" "$OUT/sq_$cfg/summary.json" > /dev/null || exit 1
       head -c 3000 "$OUT/sq_$cfg/summary.json"; echo ;;
+    sqc)
+      # instruction-fetch side: waits with an instruction ready vs I-cache misses
+      cfg=${arg:-k128m32}
+      mkdir -p "$OUT/sqc_$cfg"
+      timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_IFETCH SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_INSTS_VALU --kernel-trace -d "$OUT/sqc_$cfg/p1" -o run --output-format csv -- python3 tools/prof_kernels.py "$cfg" > "$OUT/sqc_$cfg/p1.log" 2>&1 || fail "$step" "$OUT/sqc_$cfg/p1.log"
+      csvf=$(find "$OUT/sqc_$cfg/p1" -name "*counter_collection.csv" | head -1)
+      python3 tools/sq_summary.py "$csvf" "$cfg" "$OUT/sqc_$cfg/summary.json" > /dev/null || exit 1
+      head -c 4000 "$OUT/sqc_$cfg/summary.json"; echo ;;
     pcie)
       timeout -k 10 600 python tools/pcie_bench.py k29m4 k200m56 > "$OUT/pcie.json" 2> "$OUT/pcie.err" || fail pcie "$OUT/pcie.err"
       cat "$OUT/pcie.json" ;;
