@@ -103,7 +103,9 @@ const char *cauchy_256_last_launch(void);
  * LDS by LDS-DMA, else 0.  `what` = 6 (encode) / 7 (decode): the dword lanes per sub-block of
  * the generic jump kernel on the current device (1: lh_apply_jump_kernel, 2:
  * lh_apply_jump2_kernel), 0 when the generic kernels below dword lanes serve the shape; -2
- * without a device. */
+ * without a device.  `what` = 8: 1 when the (k, m) block-size family module (one module per
+ * (k, m) for every 16-byte-multiple size up to 4 KiB with m <= 6) can serve the encode: batch
+ * and drop-in encodes take it while no size-specialised module is loaded or cached. */
 int cauchy_256_batch_path(int k, int m, int block_bytes, int what);
 
 /* Compile the specialised kernels of a shape into the on-disk code-object cache

@@ -395,15 +395,33 @@ static int encode_batch(int k, int m, int bytes, int stripes, const uint8_t *d_d
         std::string err;
         bool hard = false;
         const JitKernels *jk = jit_lookup(d, cfg, allow_compile, &err, &hard);
+        // No size-specialised module yet (compiling in the background, or a drop-in call, which
+        // never compiles): the (k, m) block-size family's module, if loaded or cached (a batch
+        // call queues its compilation too).
+        JitConfig fcfg;
+        if (!jk && !hard && !cfg.family && jit_family_config_for(k, m, bytes, &fcfg) &&
+            data_stride * fcfg.spw < (1ll << 31)) {
+            std::string ferr;
+            bool fhard = false;
+            if (const JitKernels *fk = jit_lookup(d, fcfg, allow_compile, &ferr, &fhard)) {
+                jk = fk;
+                cfg = fcfg;
+            }
+        }
         if (jk) {
-            const long long blocks = jit_encode_blocks(cfg, stripes);
+            long long blocks = jit_encode_blocks(cfg, stripes);
+            int bb = bytes;
+            if (cfg.family) {  // (the family kernel takes the block size; spw follows from it)
+                const long long spw = 64 / ((bytes / 8 + 7) / 8);
+                blocks = ((stripes + spw - 1) / spw + cfg.enc_wpb - 1) / cfg.enc_wpb;
+            }
             if (blocks > 0x7FFFFFFF) return fail(kInvalid, "batch too large");
             long long in_stride = data_stride, out_stride = rec_stride;
             int n = stripes;
-            void *args[] = {(void *)&d_data, &in_stride, (void *)&d_rec, &out_stride, &n};
+            void *args[] = {(void *)&d_data, &in_stride, (void *)&d_rec, &out_stride, &n, &bb};
             LH_HIP(hipModuleLaunchKernel(jk->encode, (unsigned)blocks, 1, 1, 64u * (unsigned)cfg.enc_wpb,
                                          1, 1, jk->dyn_lds, st, args, nullptr));
-            note_launch("lh_jit_encode");
+            note_launch(cfg.family ? "lh_jit_encode(family)" : "lh_jit_encode");
             return kOk;
         }
         if (hard) return fail(kHipError, err);
@@ -1609,6 +1627,10 @@ LH_API int cauchy_256_jit_precompile(int k, int m, int block_bytes) {
             if (part && std::string(part) != (dec ? "dec" : "enc")) continue;
             if (lh::jit_config_for(k, m, block_bytes, dec == 1, &cfg)) {
                 if (!lh::compile_code_object(cfg, &code, &err)) return lh::fail(lh::kHipError, err);
+                // the (k, m) block-size family's encode module too (one per (k, m): shared)
+                if (!dec && !cfg.family && lh::jit_family_config_for(k, m, block_bytes, &cfg) &&
+                    !lh::compile_code_object(cfg, &code, &err))
+                    return lh::fail(lh::kHipError, err);
                 // the pointer-table form (cauchy_256_*_batch_ptrs) as well, with LONGHAIR_AMD_PRECOMPILE_PTR=1
                 const char *ptr = std::getenv("LONGHAIR_AMD_PRECOMPILE_PTR");
                 if (ptr && std::string(ptr) == "1" && lh::jit_ptr_config_for(k, m, block_bytes, dec == 1, &cfg) &&
@@ -1631,6 +1653,8 @@ LH_API int cauchy_256_batch_path(int k, int m, int block_bytes, int what) {
         lh::JitConfig cfg;
         if (what == 2 || what == 5)  // 1: the register network stages its columns by LDS-DMA (LH_LDS)
             return lh::jit_config_for(k, m, block_bytes, what == 5, &cfg) && cfg.lds ? 1 : 0;
+        if (what == 8)  // 1: a block-size family module can serve the encode (jit_codec.hip LH_FAMILY)
+            return lh::jit_family_ok(k, m, block_bytes) ? 1 : 0;
         if (what == 6 || what == 7) {  // the generic jump kernel's lane width (jump_layout)
             if (block_bytes <= 0 || block_bytes % 8 || block_bytes / 8 < 4) return 0;
             lh::Device *d = nullptr;

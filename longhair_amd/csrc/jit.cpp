@@ -36,7 +36,30 @@ long long generator_ones(int k, int m) {
     return ones;
 }
 
+// The encode's block-size family serves (k, m, bytes) when: 16-byte-multiple blocks, 8-byte
+// lanes with at most 64 per stripe (bytes <= 4096), the 8 x m accumulator words of 8-byte
+// lanes within the register budget (m <= 6), at least two steps of columns (k >= 4), and, when
+// the last lane of a stripe holds a partial word, every stripe's last lane in the same DPP row
+// of 16 as its neighbour (its stores funnel that lane's word).
+bool jit_family_ok(int k, int m, int bytes) {
+    if (k < 4 || m < 2 || k + m > 256 || k > kMaxJitColumns || bytes <= 0 || bytes % 16 != 0) return false;
+    if (m * 8 * 2 > kMaxAccDwords) return false;
+    const int sub = bytes / 8, nch = (sub + 7) / 8;
+    if (nch > 64) return false;
+    const int spw = 64 / nch;
+    if (sub - 8 * (nch - 1) != 8)
+        for (int s = 0; s < spw; ++s)
+            if ((s * nch + nch - 1) % 16 == 0) return false;
+    return generator_ones(k, m) <= kMaxNetworkOnes;
+}
+
+static bool config_impl(int k, int m, int bytes, bool decode, JitConfig *cfg, bool allow_family);
+
 bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
+    return config_impl(k, m, bytes, decode, cfg, true);
+}
+
+static bool config_impl(int k, int m, int bytes, bool decode, JitConfig *cfg, bool allow_family) {
     if (const char *env = std::getenv("LONGHAIR_AMD_PATH")) {
         if (std::string(env) == "generic") return false;
     }
@@ -124,11 +147,48 @@ bool jit_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
     cfg->wgcu = knob("LH_WGCU=", cfg->cps > 1 ? 1 : 0);
     const int wpb = knob("LH_WPB=", 4);
     cfg->enc_wpb = (cfg->cps > 1 && wpb >= 1 && wpb <= 4) ? wpb : 4;
+    // Block-size family (jit_codec.hip LH_FAMILY): the multi-column-step encode with the block
+    // size a kernel argument, keyed by (k, m) alone.
+    cfg->family = 0;
+    // (LH_FAMILY=1, tests: the family module even where a size-specialised one would serve)
+    if (allow_family && !decode && knob("LH_FAMILY=", 0) && jit_family_config_for(k, m, bytes, cfg)) return true;
+    return true;
+}
+
+bool jit_family_config_for(int k, int m, int bytes, JitConfig *cfg) {
+    if (const char *env = std::getenv("LONGHAIR_AMD_PATH")) {
+        if (std::string(env) == "generic") return false;
+    }
+    if (!jit_family_ok(k, m, bytes)) return false;
+    JitConfig c;
+    c.k = k;
+    c.m = m;
+    c.bytes = bytes;
+    c.sub = bytes / 8;
+    c.W = 8;
+    c.nch = (c.sub + 7) / 8;
+    c.spw = 64 / c.nch;
+    c.wps = 0;
+    c.lds = 1;
+    c.role = 1;
+    c.plain = 0;
+    c.family = 1;
+    if (const char *d = std::getenv("LONGHAIR_AMD_JIT_DEFINES")) c.defines = d;
+    auto knob = [&](const char *name, int dflt) {
+        const size_t at = c.defines.find(name);
+        return at == std::string::npos ? dflt : std::atoi(c.defines.c_str() + at + std::strlen(name));
+    };
+    c.cps = std::max(2, std::min(5, k / 2));
+    // (tuning knobs that switch off what the family kernel is made of leave it out)
+    if (knob("LH_LDS=", 1) == 0 || knob("LH_CPS=", c.cps) < 2 || knob("LH_WPB=", 4) != 4) return false;
+    c.wgcu = knob("LH_WGCU=", 1);
+    c.enc_wpb = 4;
+    *cfg = c;
     return true;
 }
 
 bool jit_ptr_config_for(int k, int m, int bytes, bool decode, JitConfig *cfg) {
-    if (!jit_config_for(k, m, bytes, decode, cfg)) return false;
+    if (!config_impl(k, m, bytes, decode, cfg, false)) return false;
     // (the multi-column steps read a stripe's columns as one contiguous run: strided batches only)
     cfg->cps = 1;
     cfg->enc_wpb = 4;
@@ -536,6 +596,12 @@ std::string jit_source_for(const JitConfig &c) {
             }
         }
     }
+    if (c.family) {  // (block-size family: the size macros are placeholders the family kernel ignores)
+        os << "#define LH_FAMILY 1\n#define LH_K " << c.k << "\n#define LH_M " << c.m
+           << "\n#define LH_BYTES 1024\n#define LH_SUB 128\n#define LH_W 8\n#define LH_NCH 16\n#define LH_SPW 4"
+              "\n#define LH_WPS 1\n#ifndef LH_LDS\n#define LH_LDS 1\n#endif\n#ifndef LH_CPS\n#define LH_CPS "
+           << c.cps << "\n#endif\n#define LH_ROLE 1\n#define LH_DEC_PLAIN 0\n";
+    } else {
     os << "#define LH_K " << c.k << "\n#define LH_M " << c.m << "\n#define LH_BYTES " << c.bytes
        << "\n#define LH_SUB " << c.sub << "\n#define LH_W " << c.W << "\n#define LH_NCH " << c.nch
        << "\n#define LH_SPW " << (c.spw ? c.spw : 1) << "\n#define LH_WPS " << (c.wps ? c.wps : 1) << "\n";
@@ -543,6 +609,7 @@ std::string jit_source_for(const JitConfig &c) {
     if (c.lds) os << "#ifndef LH_LDS\n#define LH_LDS 1\n#endif\n";  // (a LONGHAIR_AMD_JIT_DEFINES value wins)
     if (c.cps > 1 && !c.ptr) os << "#ifndef LH_CPS\n#define LH_CPS " << c.cps << "\n#endif\n";
     if (c.role) os << "#define LH_ROLE " << c.role << "\n#define LH_DEC_PLAIN " << c.plain << "\n";
+    }
     const std::vector<uint8_t> g = generator_matrix(c.k, c.m);
     os << "static constexpr unsigned char LH_BM[" << c.m << "][" << c.k << "][8] = {";
     for (int r = 0; r < c.m; ++r) {
@@ -569,7 +636,7 @@ std::string jit_source_for(const JitConfig &c) {
 
 JitCache::Key JitCache::key_of(const JitConfig &cfg) {
     // (windowed modules take the block size as an argument: one per (k, m, W, ...))
-    return Key(cfg.k, cfg.m, cfg.win ? 0 : cfg.bytes, cfg.W, cfg.defines,
+    return Key(cfg.k, cfg.m, (cfg.win || cfg.family) ? 0 : cfg.bytes, cfg.W, cfg.defines + (cfg.family ? "|family" : ""),
                cfg.lds * 1000000000 + cfg.ptr * 100000000 + (cfg.role + 3 * cfg.plain) * 10000000 +
                    cfg.win_split * 1000000 + cfg.win * 100000 + cfg.win_lds * 10000 +
                    cfg.rows_per_wave * 100 + cfg.win_pf);

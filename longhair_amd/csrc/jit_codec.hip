@@ -205,9 +205,17 @@ struct lh_col_net {
         }
     }
 };
+#ifndef LH_PROBE_LIGHT
+#define LH_PROBE_LIGHT 0  // (probe, wrong bytes: one XOR per sub-row of row 0 instead of the network)
+#endif
 template <int X>
 __device__ __forceinline__ void lh_column(lh_word (&acc)[LH_M][8], const lh_word (&d)[8]) {
+#if LH_PROBE_LIGHT
+#pragma unroll
+    for (int y = 0; y < 8; ++y) lh_xor(acc[0][y], d[(y + X) & 7]);
+#else
     lh_col_net<X>::run(acc, d);
+#endif
 }
 
 struct lh_lane {
@@ -1033,7 +1041,213 @@ __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned ch
 #define LH_ROLE 0
 #define LH_DEC_PLAIN 0
 #endif
-#if LH_ROLE != 2
+// ------------------------------------------------------------ block-size family (LH_FAMILY)
+// One module per (k, m) serves every 16-byte-multiple block size whose sub-blocks fit 8-byte
+// lanes with at most 64 lanes per stripe (bytes <= 4096): the multi-column-step encode above
+// with the block size a kernel argument (the reference serves any size at full
+// speed on its first call, cauchy_256.cpp:423-481).  Run-time per wave (all wave-uniform):
+// sub = bytes / 8, lanes per stripe nch = ceil(sub / 8), stripes per wave spw = 64 / nch, DMA
+// instructions per step sq = ceil(spw x LH_CPS x bytes / 1024) <= 4 LH_CPS (spw x bytes <=
+// 4096).  A lane's LDS word of sub-block B sits (B x sub) mod 8 bytes past an 8-byte boundary:
+// with even sub that is one of four patterns, so each column's LDS reads are one of four
+// compile-time funnel forms picked by a wave-uniform branch on sub mod 8; the XOR network is
+// shared.  The sub-block addresses (lane offset + B x sub, aligned) are 16 per-lane registers
+// computed once; a column adds its offset in the slot.
+#ifndef LH_FAMILY
+#define LH_FAMILY 0
+#endif
+#if LH_FAMILY && LH_ROLE != 2
+#define LH_FSQ (4 * LH_CPS)  // DMA instructions per step, at most
+#ifndef LH_FAM_SPLIT
+#define LH_FAM_SPLIT 0
+#endif
+#if LH_FAM_SPLIT
+#define LH_FAM_AD8 ad8[b]
+#else
+#define LH_FAM_AD8 (ad[b] + 8)
+#endif
+struct lh_fam {
+    int bytes, sub, nch, spw, sch, sq, r8;
+};
+// The 8 sub-block words of one column, sub mod 8 = R (compile-time form): `ad[b]` is the lane's
+// LDS address of sub-block b's first aligned word in this column, computed once per wave
+// (sub-block b starts b x sub = b (sub - R) + b R bytes in: the first part a multiple of 8, the
+// second a constant).  All reads are issued before any is used (the empty asm takes every
+// word): left alone, the compiler placed each read next to its use with a wait of its own,
+// which with one wave per SIMD exposed the LDS latency 16 times per column (k29/m4 encode
+// 0.587 ms).
+template <int R>
+__device__ __forceinline__ void lh_fam_col(lh_word (&d)[8], const unsigned char *slot, const int (&ad)[8],
+                                           const int (&ad8)[8]) {
+    lh_u32x2a x[8], y[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        x[b] = *(const lh_u32x2a *)(slot + ad[b] + ((b * R) & ~7));
+        if (((b * R) & 7) != 0) y[b] = *(const lh_u32x2a *)(slot + LH_FAM_AD8 + ((b * R) & ~7));
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        asm volatile("" : "+v"(x[b]));
+        if (((b * R) & 7) != 0) asm volatile("" : "+v"(y[b]));
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const int S = (b * R) & 7;  // (constant after unrolling)
+        if (S == 0) {
+            d[b].v[0] = x[b].x;
+            d[b].v[1] = x[b].y;
+        } else if (S == 2) {
+            d[b] = lh_funnel<2>(x[b].x, x[b].y, y[b].x, y[b].y);
+        } else if (S == 4) {
+            d[b] = lh_funnel<4>(x[b].x, x[b].y, y[b].x, y[b].y);
+        } else {
+            d[b] = lh_funnel<6>(x[b].x, x[b].y, y[b].x, y[b].y);
+        }
+    }
+}
+template <int T, int CC, int R>
+struct lh_fam_cols {
+    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], const unsigned char *slot,
+                                               const int (&ad)[LH_CPS][8], const int (&ad8)[LH_CPS][8]) {
+        if constexpr (CC < LH_CPS && T * LH_CPS + CC < LH_K) {
+            lh_word d[8];
+            lh_fam_col<R>(d, slot, ad[CC], ad8[CC]);
+            lh_column<T * LH_CPS + CC>(acc, d);
+            lh_opaque(acc);
+            lh_fam_cols<T, CC + 1, R>::run(acc, slot, ad, ad8);
+        }
+    }
+};
+template <int T, int R>
+struct lh_unroll_fam {
+    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], const lh_u32x4r &rs, const int (&voff)[LH_FSQ],
+                                               const int (&voffl)[LH_FSQ], unsigned char *slot, const lh_fam &F,
+                                               const int (&ad)[LH_CPS][8], const int (&ad8)[LH_CPS][8]) {
+        if constexpr (T < LH_NSTEP) {
+            lh_wait_vmcnt<0>();  // this step's DMAs landed (the only ones in flight)
+            asm volatile("" ::: "memory");
+            lh_fam_cols<T, 0, R>::run(acc, slot, ad, ad8);
+            if constexpr (T + 1 < LH_NSTEP) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done
+                const int x1b = (T + 1) * LH_CPS * F.bytes;
+#pragma unroll
+                for (int q = 0; q < LH_FSQ; ++q) {
+                    if (q < F.sq) {  // wave-uniform
+                        // (the last step: the chunks of columns < LH_K only)
+                        const int v = (T + 2 == LH_NSTEP && LH_LASTC < LH_CPS) ? voffl[q] : voff[q];
+                        lh_dma16_bufs<LH_NT>(rs, v, x1b, slot + q * 1024);
+                    }
+                }
+            }
+            lh_unroll_fam<T + 1, R>::run(acc, rs, voff, voffl, slot, F, ad, ad8);
+        }
+    }
+};
+// The recovery blocks from the accumulators, per lane; the last lane of a stripe keeps the
+// sub-block's last VL (= sub - 8 (nch - 1)) bytes, funnelled with its neighbour's word.
+template <int VL>
+__device__ __forceinline__ void lh_fam_store(const lh_word (&acc)[LH_M][8], unsigned char *o, const lh_fam &F, bool last) {
+#pragma unroll
+    for (int r = 0; r < LH_M; ++r)
+#pragma unroll
+        for (int y = 0; y < 8; ++y) {
+            lh_word w = acc[r][y];
+            if constexpr (VL != 8) {
+                const lh_word f = lh_funnel<VL>(lh_row_shr1(w.v[0]), lh_row_shr1(w.v[1]), w.v[0], w.v[1]);
+                w.v[0] = last ? f.v[0] : w.v[0];
+                w.v[1] = last ? f.v[1] : w.v[1];
+            }
+            lh_store(o + (long long)r * F.bytes + y * F.sub, w);
+        }
+}
+// One wave's stripes; R = sub mod 8 (0, 2, 4 or 6), a compile-time form chosen once per launch,
+// so every column's LDS reads are scheduled as in the size-specialised kernel.
+template <int R>
+__device__ __forceinline__ void lh_encode_wave_fam(long long wave, const lh_fam &F, const unsigned char *__restrict__ in,
+                                                   long long in_stride, unsigned char *__restrict__ out,
+                                                   long long out_stride, int stripes, unsigned char *slot) {
+    const int lane = threadIdx.x & 63;
+    const int sl = lane / F.nch, c = lane - sl * F.nch;
+    const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)wave) * F.spw;  // wave-uniform
+    if (s0 >= stripes) return;
+    const int nst = (int)((stripes - s0) < F.spw ? (stripes - s0) : F.spw);
+    const lh_u32x4r rs = lh_rsrc(in + s0 * in_stride, (unsigned)(nst * in_stride));
+    int voff[LH_FSQ], voffl[LH_FSQ];  // (voffl: the last step's, chunks past column LH_K out of range)
+    const float inv = 1.0f / (float)F.sch;  // (j < 2^12: the float quotient is off by at most one)
+#pragma unroll
+    for (int q = 0; q < LH_FSQ; ++q) {
+        const int j = 64 * q + lane;
+        int js = (int)((float)j * inv);
+        js -= js * F.sch > j;
+        js += (js + 1) * F.sch <= j;
+        const int r = j - js * F.sch;
+        voff[q] = js < nst ? js * (int)in_stride + r * 16 : (int)0x80000000;
+        voffl[q] = r < LH_LASTC * (F.bytes >> 4) ? voff[q] : (int)0x80000000;
+    }
+#pragma unroll
+    for (int q = 0; q < LH_FSQ; ++q)
+        if (q < F.sq) lh_dma16_bufs<LH_NT>(rs, voff[q], 0, slot + q * 1024);
+    lh_word acc[LH_M][8];
+#pragma unroll
+    for (int r = 0; r < LH_M; ++r)
+#pragma unroll
+        for (int y = 0; y < 8; ++y)
+#pragma unroll
+            for (int i = 0; i < LH_NW; ++i) acc[r][y].v[i] = 0;
+    const int lo = (sl < F.spw ? sl : F.spw - 1) * (LH_CPS * F.bytes) + 8 * c;
+    // column cc, sub-block b: lo + cc bytes + b (sub - R) (the constant part in the reads).
+    // LH_FAM_SPLIT: the second word's address in registers of its own, hidden from the compiler
+    // (two ds_read_b64, 2 LDS cycles each, instead of one ds_read2_b64, 8) -- measured slower
+    // here (0.540 against 0.529 ms), unlike in the size-specialised kernels.
+    int ad[LH_CPS][8], ad8[LH_CPS][8];
+#pragma unroll
+    for (int cc = 0; cc < LH_CPS; ++cc)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            ad[cc][b] = lo + cc * F.bytes + b * (F.sub - R);
+            ad8[cc][b] = ad[cc][b] + 8;
+#if LH_FAM_SPLIT
+            asm volatile("" : "+v"(ad8[cc][b]));
+#endif
+        }
+    lh_unroll_fam<0, R>::run(acc, rs, voff, voffl, slot, F, ad, ad8);
+    if (sl >= nst) return;
+    const bool last = c == F.nch - 1;
+    unsigned char *o = out + (s0 + sl) * out_stride + (last ? F.sub - 8 : 8 * c);
+    lh_fam_store<R == 0 ? 8 : R>(acc, o, F, last);  // (sub - 8 (nch - 1) = R, or 8 when R = 0)
+}
+template <int R>
+__device__ __forceinline__ void lh_encode_fam(const lh_fam &F, const unsigned char *__restrict__ in, long long in_stride,
+                                              unsigned char *__restrict__ out, long long out_stride, int stripes,
+                                              unsigned char *slot) {
+    const long long nw = ((long long)stripes + F.spw - 1) / F.spw;
+    const long long ws = (long long)gridDim.x * (blockDim.x >> 6);
+    for (long long w = (lh_block_id() * blockDim.x + threadIdx.x) >> 6; w < nw; w += ws)
+        lh_encode_wave_fam<R>(w, F, in, in_stride, out, out_stride, stripes, slot);
+}
+extern "C" __global__ void __launch_bounds__(256, 1)
+lh_jit_encode(const unsigned char *__restrict__ in, long long in_stride, unsigned char *__restrict__ out,
+              long long out_stride, int stripes, int bytes) {
+    lh_fam F;
+    F.bytes = bytes;
+    F.sub = bytes >> 3;
+    F.nch = (F.sub + 7) >> 3;
+    F.spw = 64 / F.nch;
+    F.sch = LH_CPS * (bytes >> 4);
+    F.sq = (F.spw * F.sch + 63) >> 6;
+    F.r8 = F.sub & 7;
+    __shared__ __attribute__((aligned(16))) unsigned char lh_fring[LH_WPB][LH_FSQ * 1024 + 16];
+    unsigned char *slot = lh_fring[threadIdx.x >> 6];
+    switch (F.r8) {  // (launch-uniform; bytes % 16 == 0 makes sub even)
+        case 0: lh_encode_fam<0>(F, in, in_stride, out, out_stride, stripes, slot); break;
+        case 2: lh_encode_fam<2>(F, in, in_stride, out, out_stride, stripes, slot); break;
+        case 4: lh_encode_fam<4>(F, in, in_stride, out, out_stride, stripes, slot); break;
+        default: lh_encode_fam<6>(F, in, in_stride, out, out_stride, stripes, slot); break;
+    }
+}
+#endif  // LH_FAMILY
+
+#if LH_ROLE != 2 && !LH_FAMILY
 // recovery[s][r] = sum_x B(G[r][x]) data[s][x]   (cauchy_256_encode for m > 1, valid k, m)
 #ifndef LH_ENC_LB
 #define LH_ENC_LB 1  // min waves per SIMD the register allocator must allow (tools/tune.py)

@@ -1,0 +1,78 @@
+"""GPU parity of the encode's block-size family (jit_codec.hip LH_FAMILY, jit.cpp
+jit_family_ok): one module per (k, m) serves every qualifying block size, the size a kernel
+argument (the reference serves any (k, m, bytes) at full speed on its first
+call, cauchy_256.cpp:423-481).  Bytes against the C oracle at block sizes of every sub-block
+alignment (sub mod 8 = 0, 2, 4, 6), one and several stripes per wave, partial waves, and
+the last lane's partial word (one module serving several sizes: tests/test_family_build.py).
+`-m gpu`: needs an MI355X."""
+import os
+
+import numpy as np
+import pytest
+
+import lhutil
+
+pytestmark = pytest.mark.gpu
+
+# (k, m, bytes, stripes): sub = bytes / 8 -> nch = ceil(sub / 8) lanes, 64 // nch stripes per wave
+FAMILY_SHAPES = [
+    (29, 4, 1296, 97),   # sub 162 (mod 8 = 2), 21 lanes, 3 stripes per wave: the headline shape
+    (29, 4, 1312, 50),   # sub 164 (4)
+    (29, 4, 2592, 9),    # sub 324 (4), 41 lanes, 1 stripe per wave
+    (29, 4, 1280, 31),   # sub 160 (0): full last word
+    (29, 4, 1328, 20),   # sub 166 (6)
+    (29, 4, 4096, 5),    # sub 512: 64 lanes
+    (29, 4, 64, 70),     # sub 8: one lane, 64 stripes per wave
+    (10, 3, 384, 33),    # k 10: two steps of 5 columns, 6 lanes, 10 stripes per wave
+    (17, 6, 784, 21),    # m 6 (the register budget's limit), k 17: last step of 2 columns
+    (64, 2, 2112, 7),    # k 64, sub 264: 33 lanes
+    (4, 5, 96, 40),      # k 4 (two steps of 2), sub 12
+]
+
+
+@pytest.fixture(scope="module")
+def lh():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need an MI355X"
+    import longhair_amd
+    assert longhair_amd.cauchy_256_init() == 0
+    return longhair_amd
+
+
+@pytest.mark.parametrize("k,m,nbytes,stripes", FAMILY_SHAPES, ids=[f"k{k}m{m}b{b}" for k, m, b, _ in FAMILY_SHAPES])
+def test_family_encode_matches_oracle(lh, oracle, monkeypatch, k, m, nbytes, stripes):
+    import torch
+    monkeypatch.setenv("LONGHAIR_AMD_JIT_DEFINES", "LH_FAMILY=1")
+    monkeypatch.setenv("LONGHAIR_AMD_JIT_SYNC", "1")
+    data = lhutil.fill(k * 1000 + nbytes, stripes * k * nbytes).reshape(stripes, k, nbytes)
+    x = torch.from_numpy(data).cuda()
+    # a strided recovery buffer with a gap between stripes (the bench layout's form)
+    rbuf = torch.full((stripes, m + 1, nbytes), 0x5A, dtype=torch.uint8, device="cuda")
+    rec = rbuf[:, :m]
+    assert lh.lib().cauchy_256_batch_path(k, m, nbytes, 8) == 1  # served by the family module
+    lh.encode_batch(x, m, recovery=rec)
+    torch.cuda.synchronize()
+    assert lh.last_launch() == ["lh_jit_encode(family)"], lh.last_launch()
+    got = rec.cpu().numpy()
+    for s in range(stripes):
+        rc, exp = oracle.encode(k, m, data[s], nbytes)
+        assert rc == 0 and got[s].tobytes() == exp.tobytes(), f"stripe {s}"
+    assert (rbuf[:, m].cpu().numpy() == 0x5A).all()  # nothing written past the recovery blocks
+
+
+def test_family_serves_sizes_without_a_module(lh, oracle, monkeypatch, tmp_path):
+    """Default policy: a k29/m4 block size with no size-specialised module cached, and no
+    compiling allowed (as for every drop-in call), runs on the (k, m) family module that the
+    precompile of another size left in the cache -- not on the generic kernels."""
+    import torch
+    monkeypatch.delenv("LONGHAIR_AMD_JIT_DEFINES", raising=False)
+    monkeypatch.setenv("LONGHAIR_AMD_CACHE_DIR", str(tmp_path))
+    monkeypatch.setenv("LONGHAIR_AMD_PRECOMPILE_PART", "enc")
+    assert lh.lib().cauchy_256_jit_precompile(29, 4, 1296) == 0  # the 1 296-byte module + the family
+    monkeypatch.setenv("LONGHAIR_AMD_JIT_COMPILE", "0")
+    for nbytes, stripes in ((1456, 13), (2592, 5), (784, 40)):
+        data = lhutil.fill(nbytes + 7, stripes * 29 * nbytes).reshape(stripes, 29, nbytes)
+        rec = lh.encode_batch(torch.from_numpy(data).cuda(), 4).cpu().numpy()
+        assert lh.last_launch() == ["lh_jit_encode(family)"], (nbytes, lh.last_launch())
+        for s in range(stripes):
+            assert rec[s].tobytes() == oracle.encode(29, 4, data[s], nbytes)[1].tobytes(), (nbytes, s)

@@ -105,6 +105,11 @@ def main():
             jobs_list = [(s, None) for s in dict.fromkeys(DEFAULT + TESTS)]
             ptr_jobs = [(s, (part, {"LONGHAIR_AMD_PRECOMPILE_PTR": "1"})) for s in PTR_SHAPES for part in ("dec", "enc")]
             jobs_list += [(s, (None, env)) for s, env in KNOB_JOBS]
+            # the block-size family modules the GPU tests force (tests/test_gpu_family.py)
+            sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+            import test_gpu_family as tf
+            jobs_list += [((k, m, b), ("enc", {"LONGHAIR_AMD_JIT_DEFINES": "LH_FAMILY=1"}))
+                          for k, m, b, _ in tf.FAMILY_SHAPES]
             jobs_list = ptr_jobs[-4:] + jobs_list + ptr_jobs[:-4]
             # kernel-selection boundaries and the reference-main sweep (test_gpu_boundaries.py)
             bj, tb = boundary_jobs()
