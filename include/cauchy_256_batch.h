@@ -109,7 +109,8 @@ const char *cauchy_256_last_launch(void);
 int cauchy_256_batch_path(int k, int m, int block_bytes, int what);
 
 /* Compile the specialised kernels of a shape into the on-disk code-object cache
- * ($LONGHAIR_AMD_CACHE_DIR, else jit_cache/ beside the library).  Needs no GPU.
+ * ($LONGHAIR_AMD_CACHE_DIR, else jit_cache/ beside the library).  Needs no GPU.  With
+ * LONGHAIR_AMD_PRECOMPILE_FAMILY=1 also the encode's (k, m) block-size family module.
  * Returns 0 or -3. */
 int cauchy_256_jit_precompile(int k, int m, int block_bytes);
 

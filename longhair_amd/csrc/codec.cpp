@@ -1627,9 +1627,11 @@ LH_API int cauchy_256_jit_precompile(int k, int m, int block_bytes) {
             if (part && std::string(part) != (dec ? "dec" : "enc")) continue;
             if (lh::jit_config_for(k, m, block_bytes, dec == 1, &cfg)) {
                 if (!lh::compile_code_object(cfg, &code, &err)) return lh::fail(lh::kHipError, err);
-                // the (k, m) block-size family's encode module too (one per (k, m): shared)
-                if (!dec && !cfg.family && lh::jit_family_config_for(k, m, block_bytes, &cfg) &&
-                    !lh::compile_code_object(cfg, &code, &err))
+                // the (k, m) block-size family's encode module too (one per (k, m), shared by every
+                // block size), with LONGHAIR_AMD_PRECOMPILE_FAMILY=1
+                const char *fam = std::getenv("LONGHAIR_AMD_PRECOMPILE_FAMILY");
+                if (!dec && !cfg.family && fam && std::string(fam) == "1" &&
+                    lh::jit_family_config_for(k, m, block_bytes, &cfg) && !lh::compile_code_object(cfg, &code, &err))
                     return lh::fail(lh::kHipError, err);
                 // the pointer-table form (cauchy_256_*_batch_ptrs) as well, with LONGHAIR_AMD_PRECOMPILE_PTR=1
                 const char *ptr = std::getenv("LONGHAIR_AMD_PRECOMPILE_PTR");

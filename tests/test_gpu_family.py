@@ -68,6 +68,7 @@ def test_family_serves_sizes_without_a_module(lh, oracle, monkeypatch, tmp_path)
     monkeypatch.delenv("LONGHAIR_AMD_JIT_DEFINES", raising=False)
     monkeypatch.setenv("LONGHAIR_AMD_CACHE_DIR", str(tmp_path))
     monkeypatch.setenv("LONGHAIR_AMD_PRECOMPILE_PART", "enc")
+    monkeypatch.setenv("LONGHAIR_AMD_PRECOMPILE_FAMILY", "1")
     assert lh.lib().cauchy_256_jit_precompile(29, 4, 1296) == 0  # the 1 296-byte module + the family
     monkeypatch.setenv("LONGHAIR_AMD_JIT_COMPILE", "0")
     for nbytes, stripes in ((1456, 13), (2592, 5), (784, 40)):

@@ -102,7 +102,9 @@ def main():
         jobs = max(1, min(8, os.cpu_count() or 2))
         cmd = [sys.executable, os.path.abspath(__file__)]
         with ThreadPoolExecutor(jobs) as pool:
-            jobs_list = [(s, None) for s in dict.fromkeys(DEFAULT + TESTS)]
+            # the BASELINE shapes with their encode's (k, m) block-size family module
+            jobs_list = [(s, ("enc", {"LONGHAIR_AMD_PRECOMPILE_FAMILY": "1"})) for s in DEFAULT]
+            jobs_list += [(s, None) for s in dict.fromkeys(DEFAULT + TESTS)]
             ptr_jobs = [(s, (part, {"LONGHAIR_AMD_PRECOMPILE_PTR": "1"})) for s in PTR_SHAPES for part in ("dec", "enc")]
             jobs_list += [(s, (None, env)) for s, env in KNOB_JOBS]
             # the block-size family modules the GPU tests force (tests/test_gpu_family.py)
