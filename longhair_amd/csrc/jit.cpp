@@ -140,10 +140,13 @@ static bool config_impl(int k, int m, int bytes, bool decode, JitConfig *cfg, bo
         const size_t at = cfg->defines.find(name);
         return at == std::string::npos ? dflt : std::atoi(cfg->defines.c_str() + at + std::strlen(name));
     };
+    // The fused decode's memory-order form (jit_codec.hip LH_DMO) streams slots in the same
+    // multi-slot steps.
+    const bool dmo = decode && cfg->lds && !cfg->plain && knob("LH_DMO=", 0) == 1;
     cfg->cps = 1;
-    if (!decode && cfg->lds) cfg->cps = std::max(1, std::min(5, k / 2));
+    if ((!decode || dmo) && cfg->lds) cfg->cps = std::max(1, std::min(5, k / 2));
     cfg->cps = knob("LH_CPS=", cfg->cps);
-    if (cfg->cps > 1 && !(!decode && cfg->lds && k >= 2 * cfg->cps)) cfg->cps = 1;
+    if (cfg->cps > 1 && !((!decode || dmo) && cfg->lds && k >= 2 * cfg->cps)) cfg->cps = 1;
     cfg->wgcu = knob("LH_WGCU=", cfg->cps > 1 ? 1 : 0);
     const int wpb = knob("LH_WPB=", 4);
     cfg->enc_wpb = (cfg->cps > 1 && wpb >= 1 && wpb <= 4) ? wpb : 4;
@@ -827,6 +830,14 @@ bool compile_code_object(const JitConfig &cfg, std::vector<char> *code, std::str
     if (!compile) {
         *err = "not cached";
         return false;
+    }
+    if (const char *dump = std::getenv("LONGHAIR_AMD_JIT_DUMP")) {  // (diagnostics: the generated source)
+        const size_t slash = path.rfind('/');
+        const std::string name = std::string(dump) + "/" + (slash == std::string::npos ? path : path.substr(slash + 1)) + ".hip";
+        if (FILE *f = fopen(name.c_str(), "wb")) {
+            fwrite(src.data(), 1, src.size(), f);
+            fclose(f);
+        }
     }
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "lh_jit_codec.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {

@@ -178,33 +178,38 @@ __device__ __forceinline__ void lh_xor2(lh_word &a, const lh_word &b, const lh_w
     for (int i = 0; i < LH_NW; ++i) a.v[i] = lh_x3(a.v[i], b.v[i], c.v[i]);
 }
 
-// a ^= sum of d[b] over the set bits b of S, the terms taken two at a time (XOR3).
-template <unsigned S, int B = 0, int P = -1>
-struct lh_net {
-    __device__ __forceinline__ static void run(lh_word &a, const lh_word (&d)[8]) {
-        if constexpr (B == 8) {
-            if constexpr (P >= 0) lh_xor(a, d[P]);
-        } else if constexpr (((S >> B) & 1u) == 0) {
-            lh_net<S, B + 1, P>::run(a, d);
-        } else if constexpr (P < 0) {
-            lh_net<S, B + 1, B>::run(a, d);
-        } else {
-            lh_xor2(a, d[P], d[B]);
-            lh_net<S, B + 1, -1>::run(a, d);
-        }
-    }
+// a ^= sum of d[b] over the set bits b of S, the terms taken two at a time (XOR3): bits
+// (b0, b1), (b2, b3), ... in ascending order, an odd last one alone.  Written flat (the set
+// bits' positions computed at compile time) rather than as a recursion over the 8 bits, and
+// the column's 8 LH_M row words through a pack expansion rather than a recursion over them:
+// the recursions' forced inlining made the front end emit ~4 500 IR lines per column (572 000
+// for a k127/m3 encode, 147 s in hiprtc, mostly inliner and instcombine) for the same code.
+struct lh_bits {
+    int n, b[8];
 };
+__device__ constexpr lh_bits lh_bits_of(unsigned S) {
+    lh_bits r{0, {0, 0, 0, 0, 0, 0, 0, 0}};
+    for (int b = 0; b < 8; ++b)
+        if ((S >> b) & 1u) r.b[r.n++] = b;
+    return r;
+}
+template <unsigned S>
+__device__ __forceinline__ void lh_net(lh_word &a, const lh_word (&d)[8]) {
+    constexpr lh_bits t = lh_bits_of(S);
+    if constexpr (t.n >= 2) lh_xor2(a, d[t.b[0]], d[t.b[1]]);
+    if constexpr (t.n >= 4) lh_xor2(a, d[t.b[2]], d[t.b[3]]);
+    if constexpr (t.n >= 6) lh_xor2(a, d[t.b[4]], d[t.b[5]]);
+    if constexpr (t.n >= 8) lh_xor2(a, d[t.b[6]], d[t.b[7]]);
+    if constexpr (t.n % 2 == 1) lh_xor(a, d[t.b[t.n - 1]]);
+}
 
 // acc[r][y] ^= sum_x B(G[r][x]) d_x, one column x at a time, all constants.
-template <int X, int I = 0>
-struct lh_col_net {
-    __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], const lh_word (&d)[8]) {
-        if constexpr (I < LH_M * 8) {
-            lh_net<LH_BM[I / 8][X][I % 8]>::run(acc[I / 8][I % 8], d);
-            lh_col_net<X, I + 1>::run(acc, d);
-        }
-    }
-};
+template <class T, T... I>
+struct lh_iseq {};
+template <int X, int... I>
+__device__ __forceinline__ void lh_col_net(lh_word (&acc)[LH_M][8], const lh_word (&d)[8], lh_iseq<int, I...>) {
+    (lh_net<LH_BM[I / 8][X][I % 8]>(acc[I / 8][I % 8], d), ...);
+}
 #ifndef LH_PROBE_LIGHT
 #define LH_PROBE_LIGHT 0  // (probe, wrong bytes: one XOR per sub-row of row 0 instead of the network)
 #endif
@@ -214,7 +219,7 @@ __device__ __forceinline__ void lh_column(lh_word (&acc)[LH_M][8], const lh_word
 #pragma unroll
     for (int y = 0; y < 8; ++y) lh_xor(acc[0][y], d[(y + X) & 7]);
 #else
-    lh_col_net<X>::run(acc, d);
+    lh_col_net<X>(acc, d, __make_integer_seq<lh_iseq, int, LH_M * 8>{});
 #endif
 }
 
@@ -2016,6 +2021,60 @@ __device__ __forceinline__ void lh_decode_lds_prologue(const lh_dldsrc &S) {
         lh_decode_lds_prologue<X + 1>(S);
     }
 }
+// Phase B and the stores of a stripe's recovered blocks: block i = sum_r coef[i][r] V_r, stored
+// at the slot `dst(out slot i)` returns (the lane's chunk of it); the last lane of a stripe
+// funnels the previous lane's word (its chunk's last LH_VLAST bytes are its own).
+template <class DST>
+__device__ __forceinline__ void lh_fused_out(const lh_word (&v)[LH_M][8], const lh_plan_regs &pr, bool last, DST dst) {
+    const int e = pr.e;
+#pragma unroll
+    for (int i = 0; i < LH_EMAX; ++i) {
+        if (i < e) {  // stripe-uniform: the funnel's source lane is active too
+            lh_word o[8];
+#pragma unroll
+            for (int y = 0; y < 8; ++y)
+#pragma unroll
+                for (int q = 0; q < LH_NW; ++q) o[y].v[q] = 0;
+#pragma unroll
+            for (int t = 7; t >= 0; --t) {
+                if (t != 7) {
+                    lh_word t7;
+#pragma unroll
+                    for (int q = 0; q < LH_NW; ++q) t7.v[q] = lh_x3(o[0].v[q], o[1].v[q], o[2].v[q]) ^ o[7].v[q];
+#pragma unroll
+                    for (int y = 0; y < 7; ++y) o[y] = o[y + 1];
+                    o[7] = t7;
+                }
+#pragma unroll
+                for (int r = 0; r < LH_M; ++r) {
+                    const int idx = i * LH_M + r;
+                    const unsigned int mask =
+                        (unsigned int)((int)(pr.coefw[idx / 4] << (31 - (8 * (idx % 4) + t))) >> 31);
+#pragma unroll
+                    for (int y = 0; y < 8; ++y)
+#pragma unroll
+                        for (int q = 0; q < LH_NW; ++q) o[y].v[q] = lh_xand(o[y].v[q], v[r][y].v[q], mask);
+                }
+#if LH_PIN_WORDS & 2
+                lh_pin8w(o);
+#else
+                lh_pin8(o);
+#endif
+            }
+            unsigned char *d = dst((int)LH_BYTE(pr.outw, i));
+#pragma unroll
+            for (int y = 0; y < 8; ++y) {
+                lh_word w = o[y];
+                if constexpr (LH_VLAST != 8) {
+                    const lh_word f = lh_funnel<LH_VLAST>(lh_row_shr1(w.v[0]), lh_row_shr1(w.v[1]), w.v[0], w.v[1]);
+                    w.v[0] = last ? f.v[0] : w.v[0];
+                    w.v[1] = last ? f.v[1] : w.v[1];
+                }
+                lh_store(d + y * LH_SUB, w);
+            }
+        }
+    }
+}
 // One wave's stripe group; `work`: this lane's stripe has a plan (lh_fused_plan true).
 // Every lane of the wave runs this (the DMAs need them all); only working lanes solve and store.
 __device__ __forceinline__ void lh_fused_wave_lds(const lh_lane &l, long long wave, int c, int sl, bool work,
@@ -2086,64 +2145,215 @@ __device__ __forceinline__ void lh_fused_wave_lds(const lh_lane &l, long long wa
     // Phase B as lh_dec_phase_b; the stores as the LDS encode's.  (Storing the recovered
     // blocks through the ring as the encode does measured slower in place:
     // profiles/r5l_tune_k29m4_flat_dec.txt, 0.604 against 0.574 ms.)
-    const int e = pr.e;
-    const bool last = l.last;
-#if !LH_PTR
-    unsigned char *base = blocks + l.stripe * stripe_stride + (last ? LH_SUB - 8 : 8 * c);
-#endif
-#pragma unroll
-    for (int i = 0; i < LH_EMAX; ++i) {
-        if (i < e) {  // stripe-uniform: the funnel's source lane is active too
-            lh_word o[8];
-#pragma unroll
-            for (int y = 0; y < 8; ++y)
-#pragma unroll
-                for (int q = 0; q < LH_NW; ++q) o[y].v[q] = 0;
-#pragma unroll
-            for (int t = 7; t >= 0; --t) {
-                if (t != 7) {
-                    lh_word t7;
-#pragma unroll
-                    for (int q = 0; q < LH_NW; ++q) t7.v[q] = lh_x3(o[0].v[q], o[1].v[q], o[2].v[q]) ^ o[7].v[q];
-#pragma unroll
-                    for (int y = 0; y < 7; ++y) o[y] = o[y + 1];
-                    o[7] = t7;
-                }
-#pragma unroll
-                for (int r = 0; r < LH_M; ++r) {
-                    const int idx = i * LH_M + r;
-                    const unsigned int mask =
-                        (unsigned int)((int)(pr.coefw[idx / 4] << (31 - (8 * (idx % 4) + t))) >> 31);
-#pragma unroll
-                    for (int y = 0; y < 8; ++y)
-#pragma unroll
-                        for (int q = 0; q < LH_NW; ++q) o[y].v[q] = lh_xand(o[y].v[q], v[r][y].v[q], mask);
-                }
-#if LH_PIN_WORDS & 2
-                lh_pin8w(o);
-#else
-                lh_pin8(o);
-#endif
-            }
 #if LH_PTR
-            unsigned char *dst = (unsigned char *)S.pt[sl * (LH_K + 1) + LH_BYTE(pr.outw, i)] + (last ? LH_SUB - 8 : 8 * c);
+    lh_fused_out(v, pr, l.last, [&](int slot) {
+        return (unsigned char *)S.pt[sl * (LH_K + 1) + slot] + (l.last ? LH_SUB - 8 : 8 * c);
+    });
 #else
-            unsigned char *dst = base + (long long)LH_BYTE(pr.outw, i) * LH_BYTES;
+    unsigned char *base = blocks + l.stripe * stripe_stride + (l.last ? LH_SUB - 8 : 8 * c);
+    lh_fused_out(v, pr, l.last, [&](int slot) { return base + (long long)slot * LH_BYTES; });
 #endif
-#pragma unroll
-            for (int y = 0; y < 8; ++y) {
-                lh_word w = o[y];
-                if constexpr (LH_VLAST != 8) {
-                    const lh_word f = lh_funnel<LH_VLAST>(lh_row_shr1(w.v[0]), lh_row_shr1(w.v[1]), w.v[0], w.v[1]);
-                    w.v[0] = last ? f.v[0] : w.v[0];
-                    w.v[1] = last ? f.v[1] : w.v[1];
-                }
-                lh_store(dst + y * LH_SUB, w);
-            }
-        }
-    }
 }
 #endif  // LH_LDS
+
+// ------------------------------------------------------------ memory-order decode (LH_DMO)
+// The fused decode above reads a stripe's slots in row order (its networks are compiled per
+// row), so in a shuffled stripe each slot is a lone 1 296-byte run and the 64-byte sector two
+// neighbouring slots share is fetched once per slot: k29/m4 HBM traffic 1.075x the algorithmic
+// bytes (profiles/r9g_pmc_k29m4_decode_variants.txt).  LH_DMO = 1 reads the slots in memory
+// order instead, LH_CPS slots of every stripe per step (one contiguous run per stripe, as the
+// multi-column encode), and runs each slot's network by its row, known only at run time: the
+// wave takes the rows present at that slot one at a time (a stripe's lanes hold one row; the
+// wave's stripes usually hold different ones), each through a binary tree of wave-uniform
+// branches down to the row's compile-time network, executed by the lanes holding that row.
+// The networks cost up to LH_SPW times their VALU work of the row-order form -- affordable, the
+// decode's VALU runs below 10 % of its time -- for the encode's memory stream.  Strided batches
+// (LH_PTR keeps the row-order form); plan, solve, phase B and stores as above.
+#ifndef LH_DMO
+#define LH_DMO 0
+#endif
+#if LH_DMO && !(LH_LDS && LH_CPS > 1 && !LH_PTR && defined(LH_FUSED))
+#undef LH_DMO
+#define LH_DMO 0
+#endif
+#if LH_DMO
+#ifndef LH_DMO_AHEAD
+#define LH_DMO_AHEAD 1  // two step slots: step T + 1 lands while step T is combined
+#endif
+// Row r's contribution (wave-uniform r < LH_DCOLS): original column r's network, or recovery
+// row r - LH_K XORed into V_(r - LH_K).  The dispatch is a sequence of one-sided uniform tests,
+// first on r / 8, then on r, each test against r passed through an empty asm so the compiler
+// cannot chain them into a switch: a branch tree (an if / else nest or a lowered switch) is
+// structurised with flow blocks whose paths carry the accumulators past the leaves, and each
+// such path cost up to 64 register copies; a one-sided test updates them in place.
+#ifndef LH_DMO_PROBE
+#define LH_DMO_PROBE 0  // (probes, wrong bytes: 1 no dispatch, one XOR per slot; 2 the dispatch with one-XOR leaves)
+#endif
+template <int X>
+__device__ __forceinline__ void lh_rowleaf(lh_word (&v)[LH_M][8], const lh_word (&d)[8]) {
+    if constexpr (LH_DMO_PROBE == 2) {
+#pragma unroll
+        for (int y = 0; y < 8; ++y) lh_xor(v[X % LH_M][y], d[(y + X) & 7]);
+    } else if constexpr (X < LH_K) {
+        lh_column<X>(v, d);
+    } else {
+#pragma unroll
+        for (int y = 0; y < 8; ++y) lh_xor(v[X - LH_K][y], d[y]);
+    }
+    asm volatile("; row %0" ::"i"(X));  // (a leaf of its own: no merging of leaves by the compiler)
+}
+template <int X, int END>
+struct lh_rowgrp {
+    __device__ __forceinline__ static void run(unsigned r, lh_word (&v)[LH_M][8], const lh_word (&d)[8]) {
+        if constexpr (X < END) {
+            asm volatile("" : "+s"(r));
+            if (r == (unsigned)X) lh_rowleaf<X>(v, d);
+            lh_rowgrp<X + 1, END>::run(r, v, d);
+        }
+    }
+};
+template <int G>
+struct lh_rowdisp {
+    __device__ __forceinline__ static void run(unsigned r, lh_word (&v)[LH_M][8], const lh_word (&d)[8]) {
+        if constexpr (8 * G < LH_DCOLS) {
+            unsigned g = r >> 3;
+            asm volatile("" : "+s"(g));
+            if (g == (unsigned)G) lh_rowgrp<8 * G, (8 * G + 8 < LH_DCOLS ? 8 * G + 8 : LH_DCOLS)>::run(r, v, d);
+            lh_rowdisp<G + 1>::run(r, v, d);
+        }
+    }
+};
+// The lane's 8 words of one slot in the ring (`col` its run-time address): every read issued
+// before any is used (a wait per read, placed by the compiler next to each use, exposes the
+// LDS latency 8 times per slot with one wave per SIMD; as lh_fam_col).
+template <int B>
+__device__ __forceinline__ void lh_dmo_rd(lh_u32x2a (&x)[8], lh_u32x2a (&y)[8], const unsigned char *col, int lo, int lo8) {
+    if constexpr (B < 8) {
+        constexpr int S = (B * LH_SUB) % 8, O = B * LH_SUB - S;
+        x[B] = *(const lh_u32x2a *)(col + lo + O);
+        if constexpr (S != 0) y[B] = *(const lh_u32x2a *)(col + lo8 + O);
+        lh_dmo_rd<B + 1>(x, y, col, lo, lo8);
+    }
+}
+template <int B>
+__device__ __forceinline__ void lh_dmo_fn(lh_word (&d)[8], const lh_u32x2a (&x)[8], const lh_u32x2a (&y)[8]) {
+    if constexpr (B < 8) {
+        constexpr int S = (B * LH_SUB) % 8;
+        if constexpr (S == 0) {
+            d[B].v[0] = x[B].x;
+            d[B].v[1] = x[B].y;
+        } else {
+            d[B] = lh_funnel<S>(x[B].x, x[B].y, y[B].x, y[B].y);
+        }
+        lh_dmo_fn<B + 1>(d, x, y);
+    }
+}
+__device__ __forceinline__ void lh_dmo_col(lh_word (&d)[8], const unsigned char *col, int lo, int lo8) {
+    lh_u32x2a x[8], y[8];
+    lh_dmo_rd<0>(x, y, col, lo, lo8);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        asm volatile("" : "+v"(x[b]));
+        if ((b * LH_SUB) % 8 != 0) asm volatile("" : "+v"(y[b]));
+    }
+    lh_dmo_fn<0>(d, x, y);
+}
+// Step t's DMAs (slots t LH_CPS .. of every working stripe) into `ring`; in the last step the
+// chunks past slot LH_K are out of range.
+__device__ __forceinline__ void lh_dmo_issue(const lh_u32x4r &rs, const int (&voff)[LH_SQ], int t, unsigned char *ring) {
+    const int lane = threadIdx.x & 63;
+    const bool lastep = t + 1 == LH_NSTEP;
+#pragma unroll
+    for (int q = 0; q < LH_SQ; ++q) {
+        int v = voff[q];
+        if (LH_LASTC < LH_CPS && lastep) v = ((64 * q + lane) % LH_SCH) < LH_LASTC * LH_CCH ? v : (int)0x80000000;
+        lh_dma16_bufs<LH_LDS_NT_DEC>(rs, v, t * (LH_CPS * LH_BYTES), ring + q * 1024);
+    }
+}
+__device__ __forceinline__ void lh_fused_wave_dmo(const lh_lane &l, long long wave, int c, int sl, bool work,
+                                                  const unsigned char *scr, unsigned char *__restrict__ blocks,
+                                                  long long stripe_stride, int stripes, const lh_fused_solve &sv,
+                                                  lh_plan_regs &pr) {
+    __shared__ __attribute__((aligned(16))) unsigned char lh_mring[4][(1 + LH_DMO_AHEAD) * LH_SSLOT];
+    const int lane = threadIdx.x & 63;
+    const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)wave) * LH_SPW;  // wave-uniform
+    if (s0 >= stripes) return;  // wave-uniform
+    const int nst = (int)((stripes - s0) < LH_SPW ? (stripes - s0) : LH_SPW);
+    const unsigned long long wm = __ballot(work);
+    if (wm == 0) return;  // wave-uniform
+    unsigned char *ring = lh_mring[threadIdx.x >> 6];
+    const lh_u32x4r rs = lh_rsrc(blocks + s0 * stripe_stride, (unsigned)(nst * stripe_stride));
+    int voff[LH_SQ];  // chunk j = 64 q + lane of the step image [stripe][LH_CPS x bytes]
+#pragma unroll
+    for (int q = 0; q < LH_SQ; ++q) {
+        const int j = 64 * q + lane, js = j / LH_SCH, r = j - js * LH_SCH;
+        const bool on = js < nst && ((wm >> (js * LH_NCH)) & 1ull);  // (a stripe with nothing to do: no reads)
+        voff[q] = on ? js * (int)stripe_stride + r * 16 : (int)0x80000000;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous group's ring reads are done
+    lh_dmo_issue(rs, voff, 0, ring);
+    if (work) sv(pr);  // the solve, while the first step lands
+    lh_word v[LH_M][8];
+#pragma unroll
+    for (int r = 0; r < LH_M; ++r)
+#pragma unroll
+        for (int y = 0; y < 8; ++y)
+#pragma unroll
+            for (int i = 0; i < LH_NW; ++i) v[r][y].v[i] = 0;
+    const int sc = sl < LH_SPW ? sl : LH_SPW - 1;
+    const int lo = sc * (LH_CPS * LH_BYTES) + 8 * c;
+    int lo8 = lo + 8;
+    asm volatile("" : "+v"(lo8));
+    const unsigned char *lrows = scr + sc * LH_SR;  // the lane's stripe's slot rows (lh_fused_plan)
+#pragma unroll 1
+    for (int t = 0; t < LH_NSTEP; ++t) {
+#if LH_DMO_AHEAD
+        unsigned char *cur = ring + (t & 1) * LH_SSLOT;
+        if (t + 1 < LH_NSTEP) {
+            lh_dmo_issue(rs, voff, t + 1, ring + ((t + 1) & 1) * LH_SSLOT);  // (its slot's reads ended at t - 1)
+            lh_wait_vmcnt<LH_SQ>();  // step t landed, t + 1 in flight
+        } else {
+            lh_wait_vmcnt<0>();
+        }
+#else
+        unsigned char *cur = ring;
+        lh_wait_vmcnt<0>();  // this step's DMAs landed (the only ones in flight)
+#endif
+        asm volatile("" ::: "memory");  // no LDS read moves above the wait
+        const int ncol = t + 1 < LH_NSTEP ? LH_CPS : LH_LASTC;
+#pragma unroll 1
+        for (int cc = 0; cc < ncol; ++cc) {
+            lh_word d[8];
+            lh_dmo_col(d, cur + cc * LH_BYTES, lo, lo8);
+            const unsigned row = work ? (unsigned)lrows[t * LH_CPS + cc] : 0xFFu;
+            unsigned long long rem = wm;
+            if (LH_DMO_PROBE == 1) {
+#pragma unroll
+                for (int y = 0; y < 8; ++y) lh_xor(v[0][y], d[y]);
+                rem = 0;
+            }
+            while (rem) {  // wave-uniform: one pass per distinct row among the working lanes
+                const unsigned r = (unsigned)__builtin_amdgcn_readlane((int)row, (int)__builtin_ctzll(rem));
+                // (the test through an opaque difference: from `row == r` the compiler would
+                // substitute the lane's row for r under the branch, making the tree per-lane)
+                unsigned diff = row ^ r;
+                asm volatile("" : "+v"(diff));
+                const bool mine = diff == 0u;
+                rem &= ~__ballot(mine);
+                if (mine) lh_rowdisp<0>::run(r, v, d);
+            }
+            lh_dopaque(v);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done
+#if !LH_DMO_AHEAD
+        if (t + 1 < LH_NSTEP) lh_dmo_issue(rs, voff, t + 1, ring);
+#endif
+    }
+    if (!work) return;
+    unsigned char *base = blocks + l.stripe * stripe_stride + (l.last ? LH_SUB - 8 : 8 * c);
+    lh_fused_out(v, pr, l.last, [&](int slot) { return base + (long long)slot * LH_BYTES; });
+}
+#endif  // LH_DMO
 
 #ifndef LH_DEC_LB
 #define LH_DEC_LB 1  // min waves per SIMD the register allocator must allow (tools/tune.py)
@@ -2178,7 +2388,10 @@ __device__ __forceinline__ void lh_fused_body(unsigned char *__restrict__ blocks
         sv.gmat = gmat;
         unsigned int rowv[LH_NRW];
         lh_fused_rows(l, c, rows, rowv);
-#if LH_LDS
+#if LH_DMO
+        const bool work = l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr);
+        lh_fused_wave_dmo(l, lh_w, c, sl, work, &scratch[wid][0][0], blocks, stripe_stride, stripes, sv, pr);
+#elif LH_LDS
         const bool work = l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr);
         lh_fused_wave_lds(l, lh_w, c, sl, work, &scratch[wid][0][0], blocks, stripe_stride, stripes, sv, pr, zero_page);
 #else

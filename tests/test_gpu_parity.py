@@ -681,6 +681,11 @@ KNOB_VARIANTS = [
     ("defines-cps1", {"LONGHAIR_AMD_JIT_DEFINES": "LH_CPS=1"}, ["lh_jit_decode_fused"]),
     ("defines-cps3-wpb2-ahead-flat", {"LONGHAIR_AMD_JIT_DEFINES": "LH_CPS=3,LH_WPB=2,LH_WGCU=2,LH_CPS_AHEAD=1,LH_CPS_FLAT=1"},
      ["lh_jit_decode_fused"]),
+    # the decode's memory-order form (slots read in multi-slot steps, each slot's network picked
+    # by its run-time row), with two step slots and with one (3 slots per step: partial last step)
+    ("defines-dmo", {"LONGHAIR_AMD_JIT_DEFINES": "LH_DMO=1"}, ["lh_jit_decode_fused"]),
+    ("defines-dmo-noahead-cps3", {"LONGHAIR_AMD_JIT_DEFINES": "LH_DMO=1,LH_DMO_AHEAD=0,LH_CPS=3"},
+     ["lh_jit_decode_fused"]),
 ]
 
 

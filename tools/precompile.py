@@ -29,7 +29,9 @@ KNOB_JOBS = [((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_LDS=0,LH_PF=2,LH_N
              ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_LDG=3"}),
              ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_ASM_DMA=1"}),
              ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_CPS=1"}),
-             ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_CPS=3,LH_WPB=2,LH_WGCU=2,LH_CPS_AHEAD=1,LH_CPS_FLAT=1"})]
+             ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_CPS=3,LH_WPB=2,LH_WGCU=2,LH_CPS_AHEAD=1,LH_CPS_FLAT=1"}),
+             ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_DMO=1"}),
+             ((29, 4, 1296), {"LONGHAIR_AMD_JIT_DEFINES": "LH_DMO=1,LH_DMO_AHEAD=0,LH_CPS=3"})]
 
 
 def lds_sample(n, seed=606):
