@@ -544,6 +544,21 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         jk = jit_lookup(d, cfg, allow_compile, &err, &hard);
         if (hard) return fail(kHipError, err);
     }
+    // No size-specialised module yet (compiling in the background, or a drop-in call, which
+    // never compiles): the (k, m) block-size family's fused decode, if loaded or cached (a batch
+    // call queues its compilation too), as encode_batch does.
+    JitConfig fcfg;
+    if (!jk && k > 1 && m > 1 && !cfg.family && jit_family_config_for(k, m, bytes, &fcfg, true) &&
+        stride * fcfg.spw < (1ll << 31)) {
+        std::string ferr;
+        bool fhard = false;
+        if (const JitKernels *fk = jit_lookup(d, fcfg, allow_compile, &ferr, &fhard)) {
+            if (fk->decode_fused) {
+                jk = fk;
+                cfg = fcfg;
+            }
+        }
+    }
     const bool generic = (k > 1 && m > 1) && !jk;
     if (jk && jk->decode_fused && std::getenv("LONGHAIR_AMD_NO_FUSED_PLAN") == nullptr) {
         // Plan computed inside the decode kernel: one launch, no plan workspace.
@@ -556,12 +571,12 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         // (Stripes past the last whole round of resident waves on a prefetch-depth-3 copy of
         // this kernel measured slower, 0.627 vs 0.610 ms at k29/m4 x 65 536: the partial round
         // costs < 1 %, the second launch more; profiles/r3w_decode_tail.txt.)
-        int n = stripes;
+        int n = stripes, bb = bytes;  // (bb: the family kernel's block-size argument; cfg.spw follows it)
         void *args[] = {(void *)&d_blocks, &s1, (void *)&d_rows, (void *)&d_status, (void *)&zero,
-                        (void *)&gexp, (void *)&glog, &n};
+                        (void *)&gexp, (void *)&glog, &n, &bb};
         LH_HIP(hipModuleLaunchKernel(fn, (unsigned)jit_blocks(cfg, stripes), 1, 1, 256, 1, 1, jk->dyn_lds, st, args,
                                      nullptr));
-        note_launch("lh_jit_decode_fused");
+        note_launch(cfg.family ? "lh_jit_decode_fused(family)" : "lh_jit_decode_fused");
         return kOk;
     }
     // Large m (<= 64), sub % (64 W) == 0, after the planner: the windowed phase-A kernel
@@ -1627,11 +1642,12 @@ LH_API int cauchy_256_jit_precompile(int k, int m, int block_bytes) {
             if (part && std::string(part) != (dec ? "dec" : "enc")) continue;
             if (lh::jit_config_for(k, m, block_bytes, dec == 1, &cfg)) {
                 if (!lh::compile_code_object(cfg, &code, &err)) return lh::fail(lh::kHipError, err);
-                // the (k, m) block-size family's encode module too (one per (k, m), shared by every
+                // the (k, m) block-size family modules too (one per (k, m) and role, shared by every
                 // block size), with LONGHAIR_AMD_PRECOMPILE_FAMILY=1
                 const char *fam = std::getenv("LONGHAIR_AMD_PRECOMPILE_FAMILY");
-                if (!dec && !cfg.family && fam && std::string(fam) == "1" &&
-                    lh::jit_family_config_for(k, m, block_bytes, &cfg) && !lh::compile_code_object(cfg, &code, &err))
+                if (!cfg.family && fam && std::string(fam) == "1" &&
+                    lh::jit_family_config_for(k, m, block_bytes, &cfg, dec == 1) &&
+                    !lh::compile_code_object(cfg, &code, &err))
                     return lh::fail(lh::kHipError, err);
                 // the pointer-table form (cauchy_256_*_batch_ptrs) as well, with LONGHAIR_AMD_PRECOMPILE_PTR=1
                 const char *ptr = std::getenv("LONGHAIR_AMD_PRECOMPILE_PTR");
@@ -1655,8 +1671,8 @@ LH_API int cauchy_256_batch_path(int k, int m, int block_bytes, int what) {
         lh::JitConfig cfg;
         if (what == 2 || what == 5)  // 1: the register network stages its columns by LDS-DMA (LH_LDS)
             return lh::jit_config_for(k, m, block_bytes, what == 5, &cfg) && cfg.lds ? 1 : 0;
-        if (what == 8)  // 1: a block-size family module can serve the encode (jit_codec.hip LH_FAMILY)
-            return lh::jit_family_ok(k, m, block_bytes) ? 1 : 0;
+        if (what == 8 || what == 9)  // 1: a block-size family module can serve the encode / decode (LH_FAMILY)
+            return lh::jit_family_ok(k, m, block_bytes, what == 9) ? 1 : 0;
         if (what == 6 || what == 7) {  // the generic jump kernel's lane width (jump_layout)
             if (block_bytes <= 0 || block_bytes % 8 || block_bytes / 8 < 4) return 0;
             lh::Device *d = nullptr;

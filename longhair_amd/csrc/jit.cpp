@@ -41,11 +41,14 @@ long long generator_ones(int k, int m) {
 // lanes within the register budget (m <= 6), at least two steps of columns (k >= 4), and, when
 // the last lane of a stripe holds a partial word, every stripe's last lane in the same DPP row
 // of 16 as its neighbour (its stores funnel that lane's word).
-bool jit_family_ok(int k, int m, int bytes) {
-    if (k < 4 || m < 2 || k + m > 256 || k > kMaxJitColumns || bytes <= 0 || bytes % 16 != 0) return false;
+// The decode's family (jit_codec.hip, decode block-size family): the fused plan's shapes
+// (e_max = min(k, m) <= 4, k <= 64) with at most 8 Block.row bytes per lane (nch >= ceil(k / 8)).
+bool jit_family_ok(int k, int m, int bytes, bool decode) {
+    if (decode ? (k < 2 || std::min(k, m) > 4 || k > 64) : k < 4) return false;
+    if (m < 2 || k + m > 256 || k > kMaxJitColumns || bytes <= 0 || bytes % 16 != 0) return false;
     if (m * 8 * 2 > kMaxAccDwords) return false;
     const int sub = bytes / 8, nch = (sub + 7) / 8;
-    if (nch > 64) return false;
+    if (nch > 64 || (decode && nch < (k + 7) / 8)) return false;
     const int spw = 64 / nch;
     if (sub - 8 * (nch - 1) != 8)
         for (int s = 0; s < spw; ++s)
@@ -154,15 +157,16 @@ static bool config_impl(int k, int m, int bytes, bool decode, JitConfig *cfg, bo
     // size a kernel argument, keyed by (k, m) alone.
     cfg->family = 0;
     // (LH_FAMILY=1, tests: the family module even where a size-specialised one would serve)
-    if (allow_family && !decode && knob("LH_FAMILY=", 0) && jit_family_config_for(k, m, bytes, cfg)) return true;
+    if (allow_family && knob("LH_FAMILY=", 0) && jit_family_config_for(k, m, bytes, cfg, decode)) return true;
     return true;
 }
 
-bool jit_family_config_for(int k, int m, int bytes, JitConfig *cfg) {
+bool jit_family_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode) {
     if (const char *env = std::getenv("LONGHAIR_AMD_PATH")) {
         if (std::string(env) == "generic") return false;
     }
-    if (!jit_family_ok(k, m, bytes)) return false;
+    if (!jit_family_ok(k, m, bytes, decode)) return false;
+    if (decode && std::getenv("LONGHAIR_AMD_NO_FUSED_PLAN") != nullptr) return false;
     JitConfig c;
     c.k = k;
     c.m = m;
@@ -173,7 +177,7 @@ bool jit_family_config_for(int k, int m, int bytes, JitConfig *cfg) {
     c.spw = 64 / c.nch;
     c.wps = 0;
     c.lds = 1;
-    c.role = 1;
+    c.role = decode ? 2 : 1;
     c.plain = 0;
     c.family = 1;
     if (const char *d = std::getenv("LONGHAIR_AMD_JIT_DEFINES")) c.defines = d;
@@ -184,7 +188,7 @@ bool jit_family_config_for(int k, int m, int bytes, JitConfig *cfg) {
     c.cps = std::max(2, std::min(5, k / 2));
     // (tuning knobs that switch off what the family kernel is made of leave it out)
     if (knob("LH_LDS=", 1) == 0 || knob("LH_CPS=", c.cps) < 2 || knob("LH_WPB=", 4) != 4) return false;
-    c.wgcu = knob("LH_WGCU=", 1);
+    c.wgcu = knob("LH_WGCU=", decode ? 0 : 1);  // (the decode: two workgroups per CU, as its size-specialised form)
     c.enc_wpb = 4;
     *cfg = c;
     return true;
@@ -603,7 +607,7 @@ std::string jit_source_for(const JitConfig &c) {
         os << "#define LH_FAMILY 1\n#define LH_K " << c.k << "\n#define LH_M " << c.m
            << "\n#define LH_BYTES 1024\n#define LH_SUB 128\n#define LH_W 8\n#define LH_NCH 16\n#define LH_SPW 4"
               "\n#define LH_WPS 1\n#ifndef LH_LDS\n#define LH_LDS 1\n#endif\n#ifndef LH_CPS\n#define LH_CPS "
-           << c.cps << "\n#endif\n#define LH_ROLE 1\n#define LH_DEC_PLAIN 0\n";
+           << c.cps << "\n#endif\n#define LH_ROLE " << c.role << "\n#define LH_DEC_PLAIN 0\n";
     } else {
     os << "#define LH_K " << c.k << "\n#define LH_M " << c.m << "\n#define LH_BYTES " << c.bytes
        << "\n#define LH_SUB " << c.sub << "\n#define LH_W " << c.W << "\n#define LH_NCH " << c.nch

@@ -37,7 +37,7 @@ struct JitConfig {
     int wgcu = 0;         // register networks: resident workgroups per CU of the module's kernel,
                           // forced by dynamic LDS (0: natural)
     int cps = 1;          // LDS encode of strided batches: columns per DMA step (LH_CPS)
-    int family = 0;       // encode: the block-size family module (LH_FAMILY: one module per (k, m)
+    int family = 0;       // the block-size family module (LH_FAMILY: one module per (k, m)
                           // serves every qualifying block size, which the kernel takes as an argument)
     int enc_wpb = 4;      // encode: waves per workgroup (LH_WPB, multi-column-step encode only)
     int lanes_per_launch_unit() const { return 64; }
@@ -74,12 +74,14 @@ long long generator_ones(int k, int m);
 
 // Whether the encode's block-size family module (one per (k, m), the block size a kernel
 // argument; jit_codec.hip LH_FAMILY) can serve (k, m, bytes).
-bool jit_family_ok(int k, int m, int bytes);
+// decode: the fused, LDS-staged decode's family (e_max <= 4, k <= 64, at least ceil(k / 8)
+// lanes per stripe).
+bool jit_family_ok(int k, int m, int bytes, bool decode = false);
 // The family module's configuration for (k, m, bytes), when jit_family_ok.  Batch and drop-in
 // encodes take it when the size-specialised module is neither loaded nor cached: one cached
 // module per (k, m) serves every qualifying block size at near-specialised speed (k29/m4
 // encode 0.528 against 0.489 ms) instead of the generic kernels (0.665 ms).
-bool jit_family_config_for(int k, int m, int bytes, JitConfig *cfg);
+bool jit_family_config_for(int k, int m, int bytes, JitConfig *cfg, bool decode = false);
 
 // How a lookup may obtain a module that is neither loaded nor in the on-disk cache.
 enum class JitMode {

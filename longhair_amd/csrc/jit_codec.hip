@@ -1061,8 +1061,7 @@ __device__ __forceinline__ void lh_encode_wave(long long wave, const unsigned ch
 #ifndef LH_FAMILY
 #define LH_FAMILY 0
 #endif
-#if LH_FAMILY && LH_ROLE != 2
-#define LH_FSQ (4 * LH_CPS)  // DMA instructions per step, at most
+#if LH_FAMILY
 #ifndef LH_FAM_SPLIT
 #define LH_FAM_SPLIT 0
 #endif
@@ -1110,6 +1109,9 @@ __device__ __forceinline__ void lh_fam_col(lh_word (&d)[8], const unsigned char 
         }
     }
 }
+#endif  // LH_FAMILY
+#if LH_FAMILY && LH_ROLE != 2
+#define LH_FSQ (4 * LH_CPS)  // DMA instructions per step, at most
 template <int T, int CC, int R>
 struct lh_fam_cols {
     __device__ __forceinline__ static void run(lh_word (&acc)[LH_M][8], const unsigned char *slot,
@@ -1140,7 +1142,9 @@ struct lh_unroll_fam {
                     if (q < F.sq) {  // wave-uniform
                         // (the last step: the chunks of columns < LH_K only)
                         const int v = (T + 2 == LH_NSTEP && LH_LASTC < LH_CPS) ? voffl[q] : voff[q];
-                        lh_dma16_bufs<LH_NT>(rs, v, x1b, slot + q * 1024);
+                        int off = q * 1024;  // (opaque: no SGPR held per chunk address for the whole kernel)
+                        asm volatile("" : "+s"(off));
+                        lh_dma16_bufs<LH_NT>(rs, v, x1b, slot + off);
                     }
                 }
             }
@@ -1191,7 +1195,11 @@ __device__ __forceinline__ void lh_encode_wave_fam(long long wave, const lh_fam 
     }
 #pragma unroll
     for (int q = 0; q < LH_FSQ; ++q)
-        if (q < F.sq) lh_dma16_bufs<LH_NT>(rs, voff[q], 0, slot + q * 1024);
+        if (q < F.sq) {
+            int off = q * 1024;
+            asm volatile("" : "+s"(off));
+            lh_dma16_bufs<LH_NT>(rs, voff[q], 0, slot + off);
+        }
     lh_word acc[LH_M][8];
 #pragma unroll
     for (int r = 0; r < LH_M; ++r)
@@ -1242,7 +1250,9 @@ lh_jit_encode(const unsigned char *__restrict__ in, long long in_stride, unsigne
     F.sq = (F.spw * F.sch + 63) >> 6;
     F.r8 = F.sub & 7;
     __shared__ __attribute__((aligned(16))) unsigned char lh_fring[LH_WPB][LH_FSQ * 1024 + 16];
-    unsigned char *slot = lh_fring[threadIdx.x >> 6];
+    // (the wave index made wave-uniform explicitly, so the DMAs' LDS addresses live in SGPRs:
+    // as the decode's family, lh_jit_decode_fused below)
+    unsigned char *slot = lh_fring[__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))];
     switch (F.r8) {  // (launch-uniform; bytes % 16 == 0 makes sub even)
         case 0: lh_encode_fam<0>(F, in, in_stride, out, out_stride, stripes, slot); break;
         case 2: lh_encode_fam<2>(F, in, in_stride, out, out_stride, stripes, slot); break;
@@ -1633,14 +1643,24 @@ static constexpr unsigned char LH_GRAW[LH_M][LH_K] = LH_G_INIT;
 // Lanes of one stripe as a ballot mask (LH_NCH may be 64: a 64-bit shift by 64 is UB).
 #define LH_STRIPE_LANES (LH_NCH >= 64 ? ~0ull : ((1ull << (LH_NCH & 63)) - 1))
 
-// The lane's Block.row bytes (slots c, c + LH_NCH, ...), loaded ahead of the plan.
-__device__ __forceinline__ void lh_fused_rows(const lh_lane &l, int c, const unsigned char *__restrict__ rows,
-                                              unsigned int (&rowv)[LH_NRW]) {
+// Stripe geometry of the fused plan: lanes per stripe (nch), Block.row bytes per lane
+// (nrw = ceil(LH_K / nch), at most maxrw) and a stripe's lanes as a ballot mask.  Compile-time
+// constants in the size-specialised modules (lh_gct), run-time values in the block-size family
+// (lh_grt, below).
+struct lh_gct {
+    static constexpr int nch = LH_NCH, nrw = LH_NRW, maxrw = LH_NRW;
+    static constexpr unsigned long long lanes = LH_STRIPE_LANES;
+};
+
+// The lane's Block.row bytes (slots c, c + nch, ...), loaded ahead of the plan.
+template <class G>
+__device__ __forceinline__ void lh_fused_rows(const G &g, const lh_lane &l, int c, const unsigned char *__restrict__ rows,
+                                              unsigned int (&rowv)[G::maxrw]) {
     const unsigned char *grow = rows + l.stripe * LH_K;
 #pragma unroll
-    for (int t = 0; t < LH_NRW; ++t) {
-        const int i = c + t * LH_NCH;
-        rowv[t] = (l.active && i < LH_K) ? (unsigned int)grow[i] : 0u;
+    for (int t = 0; t < G::maxrw; ++t) {
+        const int i = c + t * g.nch;
+        rowv[t] = (l.active && t < g.nrw && i < LH_K) ? (unsigned int)grow[i] : 0u;
     }
 }
 
@@ -1665,8 +1685,9 @@ struct lh_fused_solve {
 
 // Part 1: slot maps, validity and the erasure / recovery lists.  Returns false when the
 // stripe has nothing to do (no erasure or invalid rows).
-__device__ __forceinline__ bool lh_fused_plan(const lh_lane &l, int c, int sl, unsigned char *scr,
-                                              const unsigned int (&rowv)[LH_NRW],
+template <class G>
+__device__ __forceinline__ bool lh_fused_plan(const G &g, const lh_lane &l, int c, int sl, unsigned char *scr,
+                                              const unsigned int (&rowv)[G::maxrw],
                                               unsigned char *__restrict__ rows, signed char *__restrict__ status,
                                               lh_fused_solve &sv, lh_plan_regs &pr) {
     unsigned char *lrows = scr;
@@ -1674,37 +1695,37 @@ __device__ __forceinline__ bool lh_fused_plan(const lh_lane &l, int c, int sl, u
     unsigned char *lrec = lsrc + LH_P4(LH_K);
     unsigned char *grow = rows + l.stripe * LH_K;
     // Clear the maps (0xFF = absent), then every lane records the rows of its slots.
-    for (int q = c; q < (LH_P4(LH_K) + LH_P4(LH_M)) / 4; q += LH_NCH) ((unsigned int *)lsrc)[q] = 0xFFFFFFFFu;
+    for (int q = c; q < (LH_P4(LH_K) + LH_P4(LH_M)) / 4; q += g.nch) ((unsigned int *)lsrc)[q] = 0xFFFFFFFFu;
     bool bad = false;
 #pragma unroll
-    for (int t = 0; t < LH_NRW; ++t) {
-        const int i = c + t * LH_NCH;
-        if (i >= LH_K) continue;
+    for (int t = 0; t < G::maxrw; ++t) {
+        const int i = c + t * g.nch;
+        if (t >= g.nrw || i >= LH_K) continue;
         const unsigned int r = rowv[t];
         lrows[i] = (unsigned char)r;
         if (r < LH_K) lsrc[r] = (unsigned char)i;
         else if (r < LH_K + LH_M) lrec[r - LH_K] = (unsigned char)i;
         else bad = true;
     }
-    for (int i = c; i < LH_K; i += LH_NCH) {  // a repeated row leaves another slot in the map
+    for (int i = c; i < LH_K; i += g.nch) {  // a repeated row leaves another slot in the map
         const unsigned int r = lrows[i];
         if (r < LH_K + LH_M && (r < LH_K ? lsrc[r] : lrec[r - LH_K]) != i) bad = true;
     }
     const unsigned long long lanes_bad = __ballot(bad);
-    const unsigned long long my = LH_STRIPE_LANES << (sl * LH_NCH);
+    const unsigned long long my = g.lanes << (sl * g.nch);
     const bool invalid = (lanes_bad & my) != 0;
     // Recovery slots in array order and missing originals ascending, as per-stripe bit
-    // masks gathered with wave ballots (slot/row i = c + t * LH_NCH), then unpacked by
+    // masks gathered with wave ballots (slot/row i = c + t * nch), then unpacked by
     // lowest-set-bit extraction.
     unsigned long long rcvmask = 0, ermask = 0;
 #pragma unroll
-    for (int t = 0; t < (LH_K + LH_NCH - 1) / LH_NCH; ++t) {
-        const int i = c + t * LH_NCH;
+    for (int t = 0; t < G::maxrw; ++t) {
+        if (t >= g.nrw) break;  // (uniform; never taken in the size-specialised modules)
+        const int i = c + t * g.nch;
         const bool isrcv = (i < LH_K) && (lrows[i] >= LH_K);
         const bool iser = (i < LH_K) && (lsrc[i] == 0xFF);
-        const unsigned long long lanes = LH_STRIPE_LANES;
-        rcvmask |= ((__ballot(isrcv) >> (sl * LH_NCH)) & lanes) << (t * LH_NCH);
-        ermask |= ((__ballot(iser) >> (sl * LH_NCH)) & lanes) << (t * LH_NCH);
+        rcvmask |= ((__ballot(isrcv) >> (sl * g.nch)) & g.lanes) << (t * g.nch);
+        ermask |= ((__ballot(iser) >> (sl * g.nch)) & g.lanes) << (t * g.nch);
     }
     const int nr = __builtin_popcountll(rcvmask);
     unsigned int rs[LH_EMAX], rr[LH_EMAX], er[LH_EMAX];
@@ -2024,8 +2045,11 @@ __device__ __forceinline__ void lh_decode_lds_prologue(const lh_dldsrc &S) {
 // Phase B and the stores of a stripe's recovered blocks: block i = sum_r coef[i][r] V_r, stored
 // at the slot `dst(out slot i)` returns (the lane's chunk of it); the last lane of a stripe
 // funnels the previous lane's word (its chunk's last LH_VLAST bytes are its own).
-template <class DST>
-__device__ __forceinline__ void lh_fused_out(const lh_word (&v)[LH_M][8], const lh_plan_regs &pr, bool last, DST dst) {
+// (VL: the last lane's own bytes, sub: the sub-block size -- LH_VLAST, LH_SUB except in the
+// block-size family)
+template <int VL, class DST>
+__device__ __forceinline__ void lh_fused_out_g(const lh_word (&v)[LH_M][8], const lh_plan_regs &pr, bool last, int sub,
+                                               DST dst) {
     const int e = pr.e;
 #pragma unroll
     for (int i = 0; i < LH_EMAX; ++i) {
@@ -2065,15 +2089,19 @@ __device__ __forceinline__ void lh_fused_out(const lh_word (&v)[LH_M][8], const 
 #pragma unroll
             for (int y = 0; y < 8; ++y) {
                 lh_word w = o[y];
-                if constexpr (LH_VLAST != 8) {
-                    const lh_word f = lh_funnel<LH_VLAST>(lh_row_shr1(w.v[0]), lh_row_shr1(w.v[1]), w.v[0], w.v[1]);
+                if constexpr (VL != 8) {
+                    const lh_word f = lh_funnel<VL>(lh_row_shr1(w.v[0]), lh_row_shr1(w.v[1]), w.v[0], w.v[1]);
                     w.v[0] = last ? f.v[0] : w.v[0];
                     w.v[1] = last ? f.v[1] : w.v[1];
                 }
-                lh_store(d + y * LH_SUB, w);
+                lh_store(d + y * sub, w);
             }
         }
     }
+}
+template <class DST>
+__device__ __forceinline__ void lh_fused_out(const lh_word (&v)[LH_M][8], const lh_plan_regs &pr, bool last, DST dst) {
+    lh_fused_out_g<LH_VLAST>(v, pr, last, LH_SUB, dst);
 }
 // One wave's stripe group; `work`: this lane's stripe has a plan (lh_fused_plan true).
 // Every lane of the wave runs this (the DMAs need them all); only working lanes solve and store.
@@ -2386,22 +2414,22 @@ __device__ __forceinline__ void lh_fused_body(unsigned char *__restrict__ blocks
         sv.gexp = gexp;
         sv.glog = glog;
         sv.gmat = gmat;
-        unsigned int rowv[LH_NRW];
-        lh_fused_rows(l, c, rows, rowv);
+        unsigned int rowv[lh_gct::maxrw];
+        lh_fused_rows(lh_gct(), l, c, rows, rowv);
 #if LH_DMO
-        const bool work = l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr);
+        const bool work = l.active && lh_fused_plan(lh_gct(), l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr);
         lh_fused_wave_dmo(l, lh_w, c, sl, work, &scratch[wid][0][0], blocks, stripe_stride, stripes, sv, pr);
 #elif LH_LDS
-        const bool work = l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr);
+        const bool work = l.active && lh_fused_plan(lh_gct(), l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr);
         lh_fused_wave_lds(l, lh_w, c, sl, work, &scratch[wid][0][0], blocks, stripe_stride, stripes, sv, pr, zero_page);
 #else
-        if (l.active && lh_fused_plan(l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr))
+        if (l.active && lh_fused_plan(lh_gct(), l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr))
             lh_decode_body<PF>(l, lh_w, blocks, stripe_stride, pr, zero_page, stripes, sv);
 #endif
     }
 }
 
-#if LH_ROLE == 0 || (LH_ROLE == 2 && !LH_DEC_PLAIN)
+#if (LH_ROLE == 0 || (LH_ROLE == 2 && !LH_DEC_PLAIN)) && !LH_FAMILY
 extern "C" __global__ void __launch_bounds__(256, LH_DEC_LB)
 lh_jit_decode_fused(unsigned char *__restrict__ blocks, long long stripe_stride, unsigned char *__restrict__ rows,
                     signed char *__restrict__ status, const unsigned char *__restrict__ zero_page,
@@ -2409,5 +2437,245 @@ lh_jit_decode_fused(unsigned char *__restrict__ blocks, long long stripe_stride,
     lh_fused_body<LH_PF_DEC>(blocks, stripe_stride, rows, status, zero_page, gf_exp, gf_log, stripes);
 }
 #endif
+
+// ------------------------------------------------------------ decode block-size family
+// The fused, LDS-staged decode of lh_fused_wave_lds with the block size a kernel argument (one
+// module per (k, m) for every 16-byte-multiple size with 8-byte lanes, at most 64 lanes and at
+// least ceil(k / 8) lanes per stripe; jit.cpp jit_family_ok): the wave's geometry (lanes and
+// stripes per wave, DMA instructions per column) is run-time and wave-uniform; every column
+// issues 4 DMA instructions (one column of 4 KiB at most), those past the wave's stripes with an
+// out-of-range offset (no memory request), so the waits count a constant; the LDS reads take
+// the per-lane sub-block addresses computed once per wave with the alignment form R = sub mod 8
+// fixed per launch (lh_fam_col, as the encode's family).
+#if LH_FAMILY && LH_ROLE == 2 && LH_LDS && !LH_PTR
+#define LH_FNRW 8                                   // Block.row bytes per lane, at most
+#define LH_FSPW (64 / ((LH_K + LH_FNRW - 1) / LH_FNRW))  // stripes per wave, at most
+#define LH_FRS (4 * 1024 + 16)                      // ring slot: 4 KiB (+16: the last lane's second word)
+struct lh_grt {
+    int nch, nrw;
+    unsigned long long lanes;
+    static constexpr int maxrw = LH_FNRW;
+};
+struct lh_dfam {
+    int bytes, sub, nch, spw, cch;
+};
+struct lh_fdsrc {
+    __amdgpu_buffer_rsrc_t rs;
+    int joff[4], jsc[4];  // DMA chunk q: byte offset in the wave's stripes (block 0); its stripe's scratch offset or < 0
+    int bytes;
+    const unsigned char *scr;
+    unsigned char *ring;
+    template <int X>
+    __device__ __forceinline__ void slots(unsigned (&sv)[4]) const {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const unsigned b = scr[(jsc[q] & 0x7FFFFFFF) + lh_dmoff<X>::v];
+            sv[q] = jsc[q] < 0 ? 0xFFu : b;
+        }
+    }
+    __device__ __forceinline__ void issue(const unsigned (&sv)[4], int slot) const {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            // (the LDS offset made opaque where it is used: left alone, the compiler keeps all 16
+            // slot / chunk addresses in SGPRs for the whole kernel and spills others for them)
+            int off = slot * LH_FRS + q * 1024;
+            asm volatile("" : "+s"(off));
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, (__attribute__((address_space(3))) void *)(ring + off), 16,
+                sv[q] == 0xFFu ? (int)0x80000000 : joff[q] + (int)sv[q] * bytes, 0, 0, LH_LDS_NT_DEC ? 2 : 0);
+        }
+    }
+};
+template <int C, int N>
+__device__ __forceinline__ void lh_fdslots(const lh_fdsrc &S, unsigned (&sv)[LH_LDG][4]) {
+    if constexpr (N > 0 && C < LH_DCOLS) {
+        S.slots<C>(sv[LH_LDG - N]);
+        lh_fdslots<C + 1, N - 1>(S, sv);
+    }
+}
+template <int C, int N>
+__device__ __forceinline__ void lh_fdissue(const lh_fdsrc &S, const unsigned (&sv)[LH_LDG][4]) {
+    if constexpr (N > 0 && C < LH_DCOLS) {
+        S.issue(sv[LH_LDG - N], C % LH_LD);
+        lh_fdissue<C + 1, N - 1>(S, sv);
+    }
+}
+#ifndef LH_DFAM_PIN
+#define LH_DFAM_PIN 0  // 1: a column's 16 LDS reads all issued before any is used (lh_fam_col)
+#endif
+// A column's words, each read next to its use (the compiler's schedule).
+template <int R>
+__device__ __forceinline__ void lh_dfam_col(lh_word (&d)[8], const unsigned char *slot, const int (&ad)[8]) {
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const int S = (b * R) & 7;  // (constant after unrolling)
+        const lh_u32x2a x = *(const lh_u32x2a *)(slot + ad[b] + ((b * R) & ~7));
+        if (S == 0) {
+            d[b].v[0] = x.x;
+            d[b].v[1] = x.y;
+        } else {
+            const lh_u32x2a y = *(const lh_u32x2a *)(slot + ad[b] + 8 + ((b * R) & ~7));
+            if (S == 2) d[b] = lh_funnel<2>(x.x, x.y, y.x, y.y);
+            else if (S == 4) d[b] = lh_funnel<4>(x.x, x.y, y.x, y.y);
+            else d[b] = lh_funnel<6>(x.x, x.y, y.x, y.y);
+        }
+    }
+}
+// Phase A over the k + m columns, as lh_unroll_decode_lds (refills of LH_LDG slots).
+template <int X, int R>
+struct lh_unroll_dfam {
+    __device__ __forceinline__ static void run(lh_word (&v)[LH_M][8], const lh_fdsrc &S, const int (&ad)[8], const int (&ad8)[8]) {
+        if constexpr (X < LH_DCOLS) {
+            constexpr int issued = (LH_LD + LH_LDG * (X / LH_LDG)) < LH_DCOLS ? (LH_LD + LH_LDG * (X / LH_LDG)) : LH_DCOLS;
+            constexpr int ahead = issued - 1 - X;
+            unsigned sv[4];
+            if constexpr (LH_LDG == 1 && X + LH_LD < LH_DCOLS) S.slots<(X + LH_LD < LH_DCOLS ? X + LH_LD : 0)>(sv);
+            constexpr bool refill = LH_LDG > 1 && (X + 1) % LH_LDG == 0 && LH_LD + X + 1 - LH_LDG < LH_DCOLS;
+            unsigned svg[LH_LDG][4];
+            if constexpr (refill) lh_fdslots<LH_LD + X + 1 - LH_LDG, LH_LDG>(S, svg);
+            lh_wait_vmcnt<4 * ahead>();
+            asm volatile("" ::: "memory");  // no LDS read moves above the wait
+            lh_word d[8];
+#if LH_DFAM_PIN
+            lh_fam_col<R>(d, S.ring + (X % LH_LD) * LH_FRS, ad, ad8);
+#else
+            lh_dfam_col<R>(d, S.ring + (X % LH_LD) * LH_FRS, ad);
+#endif
+            lh_dcombine<X, LH_LDS_REC_FIRST>(v, d);
+            lh_dopaque(v);
+            if constexpr (LH_LDG == 1 && X + LH_LD < LH_DCOLS) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done
+                S.issue(sv, X % LH_LD);
+            } else if constexpr (refill) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slots' reads are done
+                lh_fdissue<LH_LD + X + 1 - LH_LDG, LH_LDG>(S, svg);
+            }
+            lh_unroll_dfam<X + 1, R>::run(v, S, ad, ad8);
+        }
+    }
+};
+template <int X = 0>
+__device__ __forceinline__ void lh_dfam_prologue(const lh_fdsrc &S) {
+    if constexpr (X < LH_LD && X < LH_DCOLS) {
+        unsigned sv[4];
+        S.slots<X>(sv);
+        S.issue(sv, X);
+        lh_dfam_prologue<X + 1>(S);
+    }
+}
+template <int R>
+__device__ __forceinline__ void lh_fused_wave_fam(const lh_dfam &F, const lh_lane &l, long long wave, int c, int sl, bool work,
+                                                  const unsigned char *scr, unsigned char *__restrict__ blocks,
+                                                  long long stripe_stride, int stripes, const lh_fused_solve &sv,
+                                                  lh_plan_regs &pr, unsigned char *ring) {
+    const int lane = threadIdx.x & 63;
+    const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)wave) * F.spw;  // wave-uniform
+    if (s0 >= stripes) return;  // wave-uniform
+    const int nst = (int)((stripes - s0) < F.spw ? (stripes - s0) : F.spw);
+    const unsigned long long wm = __ballot(work);
+    if (wm == 0) return;  // wave-uniform
+    lh_fdsrc S;
+    S.rs = __builtin_amdgcn_make_buffer_rsrc(blocks + s0 * stripe_stride, 0, (int)(nst * stripe_stride), 0x00020000);
+    S.bytes = F.bytes;
+    S.scr = scr;
+    S.ring = ring;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // chunk j = 64 q + lane of the image [stripe][bytes]
+        const int j = 64 * q + lane;
+        const int js = j / F.cch;
+        const bool on = js < nst && ((wm >> (js * F.nch)) & 1ull);
+        S.joff[q] = js * (int)stripe_stride + (j - js * F.cch) * 16;
+        S.jsc[q] = on ? js * LH_SR : (int)0x80000000;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous group's ring reads are done
+    lh_dfam_prologue(S);
+    if (work) sv(pr);  // the solve, while the first columns land
+    lh_word v[LH_M][8];
+#pragma unroll
+    for (int r = 0; r < LH_M; ++r)
+#pragma unroll
+        for (int y = 0; y < 8; ++y)
+#pragma unroll
+            for (int i = 0; i < LH_NW; ++i) v[r][y].v[i] = 0;
+    const int lo = (sl < F.spw ? sl : F.spw - 1) * F.bytes + 8 * c;
+    int ad[8], ad8[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        ad[b] = lo + b * (F.sub - R);
+        ad8[b] = ad[b] + 8;
+#if LH_FAM_SPLIT
+        asm volatile("" : "+v"(ad8[b]));
+#endif
+    }
+    lh_unroll_dfam<0, R>::run(v, S, ad, ad8);
+    if (!work) return;
+    unsigned char *base = blocks + l.stripe * stripe_stride + (l.last ? F.sub - 8 : 8 * c);
+    lh_fused_out_g<R == 0 ? 8 : R>(v, pr, l.last, F.sub, [&](int slot) { return base + (long long)slot * F.bytes; });
+}
+template <int R>
+__device__ __forceinline__ void lh_dfam_body(const lh_dfam &F, const lh_grt &g, unsigned char *__restrict__ blocks,
+                                             long long stripe_stride, unsigned char *__restrict__ rows,
+                                             signed char *__restrict__ status, const unsigned char *gexp, const short *glog,
+                                             const unsigned char *gmat, unsigned char (*scratch)[LH_FSPW][LH_SR],
+                                             unsigned char *ring, int stripes) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int sl = lane / F.nch, c = lane - sl * F.nch;
+    const long long nw = ((long long)stripes + F.spw - 1) / F.spw;
+    const long long ws = (long long)gridDim.x * (blockDim.x >> 6);
+    for (long long w = (lh_block_id() * blockDim.x + threadIdx.x) >> 6; w < nw; w += ws) {
+        lh_lane l;
+        l.stripe = w * F.spw + sl;
+        l.active = sl < F.spw && l.stripe < stripes;
+        l.last = c == F.nch - 1;
+        l.p = 0;  // (unused here)
+        lh_plan_regs pr;
+        lh_fused_solve sv;
+        sv.gexp = gexp;
+        sv.glog = glog;
+        sv.gmat = gmat;
+        unsigned int rowv[LH_FNRW];
+        lh_fused_rows(g, l, c, rows, rowv);
+        const bool work = l.active && lh_fused_plan(g, l, c, sl, &scratch[wid][sl][0], rowv, rows, status, sv, pr);
+        lh_fused_wave_fam<R>(F, l, w, c, sl, work, &scratch[wid][0][0], blocks, stripe_stride, stripes, sv, pr, ring);
+    }
+}
+extern "C" __global__ void __launch_bounds__(256, LH_DEC_LB)
+lh_jit_decode_fused(unsigned char *__restrict__ blocks, long long stripe_stride, unsigned char *__restrict__ rows,
+                    signed char *__restrict__ status, const unsigned char *__restrict__ zero_page,
+                    const unsigned char *__restrict__ gf_exp, const short *__restrict__ gf_log, int stripes, int bytes) {
+    (void)zero_page;
+    __shared__ unsigned char gexp[1024];  // exp(i mod 255) for i < 1024 (lh_inv_adj)
+    __shared__ short glog[256];
+    __shared__ unsigned char gmat[LH_M * LH_K];
+    __shared__ __attribute__((aligned(16))) unsigned char scratch[4][LH_FSPW][LH_SR];
+    __shared__ __attribute__((aligned(16))) unsigned char lh_fdring[4][LH_LD * LH_FRS];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gexp[i + 256 * q] = gf_exp[(i + 256 * q) % 255];
+        glog[i] = gf_log[i];
+    }
+    for (int i = threadIdx.x; i < LH_M * LH_K; i += blockDim.x) gmat[i] = LH_GRAW[i / LH_K][i % LH_K];
+    __syncthreads();
+    lh_dfam F;
+    F.bytes = bytes;
+    F.sub = bytes >> 3;
+    F.nch = (F.sub + 7) >> 3;
+    F.spw = 64 / F.nch;
+    F.cch = bytes >> 4;
+    lh_grt g;
+    g.nch = F.nch;
+    g.nrw = (LH_K + F.nch - 1) / F.nch;
+    g.lanes = F.nch >= 64 ? ~0ull : ((1ull << F.nch) - 1);
+    // (the wave index made wave-uniform explicitly: the ring's LDS addresses, the DMAs' M0, then
+    // live in SGPRs, not in 16 VGPRs read back with readfirstlane before every DMA)
+    unsigned char *ring = lh_fdring[__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))];
+    switch (F.sub & 7) {  // (launch-uniform; bytes % 16 == 0 makes sub even)
+        case 0: lh_dfam_body<0>(F, g, blocks, stripe_stride, rows, status, gexp, glog, gmat, scratch, ring, stripes); break;
+        case 2: lh_dfam_body<2>(F, g, blocks, stripe_stride, rows, status, gexp, glog, gmat, scratch, ring, stripes); break;
+        case 4: lh_dfam_body<4>(F, g, blocks, stripe_stride, rows, status, gexp, glog, gmat, scratch, ring, stripes); break;
+        default: lh_dfam_body<6>(F, g, blocks, stripe_stride, rows, status, gexp, glog, gmat, scratch, ring, stripes); break;
+    }
+}
+#endif  // LH_FAMILY && LH_ROLE == 2
 
 #endif  // LH_EMAX <= 4 && LH_NCH <= 64 && LH_K <= 64

@@ -1,7 +1,7 @@
-"""GPU parity of the encode's block-size family (jit_codec.hip LH_FAMILY, jit.cpp
-jit_family_ok): one module per (k, m) serves every qualifying block size, the size a kernel
-argument (the reference serves any (k, m, bytes) at full speed on its first
-call, cauchy_256.cpp:423-481).  Bytes against the C oracle at block sizes of every sub-block
+"""GPU parity of the block-size families (jit_codec.hip LH_FAMILY, jit.cpp jit_family_ok), the
+encode's and the fused decode's: one module per (k, m) and role serves every qualifying block
+size, the size a kernel argument (the reference serves any (k, m, bytes) at full
+speed on its first call, cauchy_256.cpp:423-481).  Bytes against the C oracle at block sizes of every sub-block
 alignment (sub mod 8 = 0, 2, 4, 6), one and several stripes per wave, partial waves, and
 the last lane's partial word (one module serving several sizes: tests/test_family_build.py).
 `-m gpu`: needs an MI355X."""
@@ -27,6 +27,22 @@ FAMILY_SHAPES = [
     (17, 6, 784, 21),    # m 6 (the register budget's limit), k 17: last step of 2 columns
     (64, 2, 2112, 7),    # k 64, sub 264: 33 lanes
     (4, 5, 96, 40),      # k 4 (two steps of 2), sub 12
+]
+
+
+# The fused decode's family: (k, m, bytes, stripes); at least ceil(k / 8) lanes per stripe
+FAMILY_DEC_SHAPES = [
+    (29, 4, 1296, 97),   # sub 162 (mod 8 = 2), 21 lanes, 3 stripes per wave: the headline shape
+    (29, 4, 1312, 50),   # sub 164 (4)
+    (29, 4, 2592, 9),    # sub 324 (4), 41 lanes, 1 stripe per wave
+    (29, 4, 1280, 31),   # sub 160 (0): full last word
+    (29, 4, 1328, 20),   # sub 166 (6)
+    (29, 4, 4096, 5),    # 64 lanes
+    (29, 4, 464, 40),    # sub 58, 8 lanes: 4 Block.row bytes per lane, 8 stripes per wave
+    (10, 3, 384, 33),    # 6 lanes, 10 stripes per wave, e <= 3
+    (17, 4, 784, 21),    # sub 98 (2), 13 lanes
+    (64, 2, 2112, 7),    # k 64, 33 lanes, e <= 2
+    (4, 5, 96, 40),      # k 4 < m: e <= 4, 2 lanes, 32 stripes per wave
 ]
 
 
@@ -60,20 +76,31 @@ def test_family_encode_matches_oracle(lh, oracle, monkeypatch, k, m, nbytes, str
     assert (rbuf[:, m].cpu().numpy() == 0x5A).all()  # nothing written past the recovery blocks
 
 
+@pytest.mark.parametrize("k,m,nbytes,stripes", FAMILY_DEC_SHAPES, ids=[f"k{k}m{m}b{b}" for k, m, b, _ in FAMILY_DEC_SHAPES])
+def test_family_decode_matches_oracle(lh, oracle, monkeypatch, k, m, nbytes, stripes):
+    """Bytes and rewritten rows of the fused decode's family module against the oracle: random
+    e per stripe (the first at e_max), random recovery rows, shuffled slots (as every
+    specialised decode is tested, test_gpu_boundaries.roundtrip)."""
+    import test_gpu_boundaries as tb
+    monkeypatch.setenv("LONGHAIR_AMD_JIT_DEFINES", "LH_FAMILY=1")
+    monkeypatch.setenv("LONGHAIR_AMD_JIT_SYNC", "1")
+    assert lh.lib().cauchy_256_batch_path(k, m, nbytes, 9) == 1  # served by the family module
+    _, dec = tb.roundtrip(lh, oracle, k, m, nbytes, stripes, seed=k * 7 + nbytes)
+    assert dec == ["lh_jit_decode_fused(family)"], dec
+
+
 def test_family_serves_sizes_without_a_module(lh, oracle, monkeypatch, tmp_path):
     """Default policy: a k29/m4 block size with no size-specialised module cached, and no
-    compiling allowed (as for every drop-in call), runs on the (k, m) family module that the
-    precompile of another size left in the cache -- not on the generic kernels."""
-    import torch
+    compiling allowed (as for every drop-in call), encodes and decodes on the (k, m) family
+    modules that the precompile of another size left in the cache -- not on the generic
+    kernels."""
+    import test_gpu_boundaries as tb
     monkeypatch.delenv("LONGHAIR_AMD_JIT_DEFINES", raising=False)
     monkeypatch.setenv("LONGHAIR_AMD_CACHE_DIR", str(tmp_path))
-    monkeypatch.setenv("LONGHAIR_AMD_PRECOMPILE_PART", "enc")
     monkeypatch.setenv("LONGHAIR_AMD_PRECOMPILE_FAMILY", "1")
-    assert lh.lib().cauchy_256_jit_precompile(29, 4, 1296) == 0  # the 1 296-byte module + the family
+    assert lh.lib().cauchy_256_jit_precompile(29, 4, 1296) == 0  # the 1 296-byte modules + the families
     monkeypatch.setenv("LONGHAIR_AMD_JIT_COMPILE", "0")
     for nbytes, stripes in ((1456, 13), (2592, 5), (784, 40)):
-        data = lhutil.fill(nbytes + 7, stripes * 29 * nbytes).reshape(stripes, 29, nbytes)
-        rec = lh.encode_batch(torch.from_numpy(data).cuda(), 4).cpu().numpy()
-        assert lh.last_launch() == ["lh_jit_encode(family)"], (nbytes, lh.last_launch())
-        for s in range(stripes):
-            assert rec[s].tobytes() == oracle.encode(29, 4, data[s], nbytes)[1].tobytes(), (nbytes, s)
+        enc, dec = tb.roundtrip(lh, oracle, 29, 4, nbytes, stripes, seed=nbytes + 7)
+        assert enc == ["lh_jit_encode(family)"], (nbytes, enc)
+        assert dec == ["lh_jit_decode_fused(family)"], (nbytes, dec)

@@ -104,8 +104,8 @@ def main():
         jobs = max(1, min(8, os.cpu_count() or 2))
         cmd = [sys.executable, os.path.abspath(__file__)]
         with ThreadPoolExecutor(jobs) as pool:
-            # the BASELINE shapes with their encode's (k, m) block-size family module
-            jobs_list = [(s, ("enc", {"LONGHAIR_AMD_PRECOMPILE_FAMILY": "1"})) for s in DEFAULT]
+            # the BASELINE shapes with their (k, m) block-size family modules
+            jobs_list = [(s, (part, {"LONGHAIR_AMD_PRECOMPILE_FAMILY": "1"})) for s in DEFAULT for part in ("enc", "dec")]
             jobs_list += [(s, None) for s in dict.fromkeys(DEFAULT + TESTS)]
             ptr_jobs = [(s, (part, {"LONGHAIR_AMD_PRECOMPILE_PTR": "1"})) for s in PTR_SHAPES for part in ("dec", "enc")]
             jobs_list += [(s, (None, env)) for s, env in KNOB_JOBS]
@@ -114,6 +114,8 @@ def main():
             import test_gpu_family as tf
             jobs_list += [((k, m, b), ("enc", {"LONGHAIR_AMD_JIT_DEFINES": "LH_FAMILY=1"}))
                           for k, m, b, _ in tf.FAMILY_SHAPES]
+            jobs_list += [((k, m, b), (part, {"LONGHAIR_AMD_JIT_DEFINES": "LH_FAMILY=1"}))
+                          for k, m, b, _ in tf.FAMILY_DEC_SHAPES for part in ("dec", "enc")]
             jobs_list = ptr_jobs[-4:] + jobs_list + ptr_jobs[:-4]
             # kernel-selection boundaries and the reference-main sweep (test_gpu_boundaries.py)
             bj, tb = boundary_jobs()
