@@ -277,6 +277,20 @@ __device__ __forceinline__ long long lh_block_id() {
 #endif
 }
 
+// The wave's index in its workgroup, wave-uniform to the compiler (LH_UNIWID): the per-wave LDS
+// rings indexed by it then have their addresses -- the LDS-DMAs' M0 -- in SGPRs.  With
+// threadIdx.x >> 6 the compiler treats the index as per-lane, keeps every ring slot / chunk
+// address in a VGPR (16 in the k29/m4 decode) and reads one back with v_readfirstlane before
+// each DMA.
+#ifndef LH_UNIWID
+#define LH_UNIWID 1
+#endif
+template <int ROLE>  // (LH_UNIWID bit 0: the encode's rings, bit 1: the decode's)
+__device__ __forceinline__ int lh_wid() {
+    if constexpr ((LH_UNIWID >> ROLE) & 1) return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    return (int)(threadIdx.x >> 6);
+}
+
 #define LH_WAVE_LOOP(stripes)                                                                   \
     const long long lh_nw = lh_total_waves(stripes);                                           \
     const long long lh_ws = (long long)gridDim.x * (blockDim.x >> 6);                          \
@@ -708,7 +722,7 @@ __device__ __forceinline__ void lh_encode_wave_lds(long long wave, const unsigne
     if (s0 >= stripes) return;  // wave-uniform
     const int nst = (int)((stripes - s0) < LH_SPW ? (stripes - s0) : LH_SPW);
     lh_ldsrc S;
-    S.ring = lh_lring[threadIdx.x >> 6];
+    S.ring = lh_lring[lh_wid<0>()];
     // LH_PTR: in / out are the data and recovery pointer tables (rows of LH_K / LH_M pointers)
     __shared__ unsigned long long lh_lpt[4][LH_SPW * LH_LPR];
     unsigned long long *prow = lh_lpt[threadIdx.x >> 6];
@@ -938,7 +952,7 @@ __device__ __forceinline__ void lh_encode_wave_cps(long long wave, const unsigne
     const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)wave) * LH_SPW;  // wave-uniform
     if (s0 >= stripes) return;  // wave-uniform
     const int nst = (int)((stripes - s0) < LH_SPW ? (stripes - s0) : LH_SPW);
-    unsigned char *slot = lh_cring[threadIdx.x >> 6];
+    unsigned char *slot = lh_cring[lh_wid<0>()];
     const lh_u32x4r rs = lh_rsrc(in + s0 * in_stride, (unsigned)(nst * in_stride));
     int voff[LH_SQ];
 #pragma unroll
@@ -1939,6 +1953,9 @@ struct lh_dmoff {  // scratch offset of column X's slot byte
     using D = lh_dcol<X, LH_LDS_REC_FIRST>;
     static constexpr int v = D::rec ? LH_SR_REC + D::r : LH_SR_SRC + D::x;
 };
+#ifndef LH_DOPQ
+#define LH_DOPQ 0  // the DMAs' LDS offsets opaque where used (no SGPR held per slot / chunk address)
+#endif
 struct lh_dldsrc {
 #if LH_PTR
     const unsigned long long *pt;  // LDS: the wave's pointer rows [stripe][LH_K + 1]
@@ -1972,9 +1989,13 @@ struct lh_dldsrc {
             lh_dma16_buf<LH_LDS_NT_DEC>(rs, sv[q] == 0xFFu ? (int)0x80000000 : joff[q] + (int)sv[q] * LH_BYTES,
                                         ring + slot * (LH_LQ * 1024) + q * 1024);
 #else
+        {
+            int off = slot * (LH_LQ * 1024) + q * 1024;
+            if (LH_DOPQ) asm volatile("" : "+s"(off));  // (opaque: see lh_fdsrc::issue)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rs, (__attribute__((address_space(3))) void *)(ring + slot * (LH_LQ * 1024) + q * 1024), 16,
+                rs, (__attribute__((address_space(3))) void *)(ring + off), 16,
                 sv[q] == 0xFFu ? (int)0x80000000 : joff[q] + (int)sv[q] * LH_BYTES, 0, 0, LH_LDS_NT_DEC ? 2 : 0);
+        }
 #endif
     }
 };
@@ -2141,7 +2162,7 @@ __device__ __forceinline__ void lh_fused_wave_lds(const lh_lane &l, long long wa
 #endif
 #endif
     S.scr = scr;
-    S.ring = lh_dring[threadIdx.x >> 6];
+    S.ring = lh_dring[lh_wid<1>()];
 #pragma unroll
     for (int q = 0; q < LH_LQ; ++q) {
         int j = 64 * q + lane;
@@ -2309,7 +2330,7 @@ __device__ __forceinline__ void lh_fused_wave_dmo(const lh_lane &l, long long wa
     const int nst = (int)((stripes - s0) < LH_SPW ? (stripes - s0) : LH_SPW);
     const unsigned long long wm = __ballot(work);
     if (wm == 0) return;  // wave-uniform
-    unsigned char *ring = lh_mring[threadIdx.x >> 6];
+    unsigned char *ring = lh_mring[lh_wid<1>()];
     const lh_u32x4r rs = lh_rsrc(blocks + s0 * stripe_stride, (unsigned)(nst * stripe_stride));
     int voff[LH_SQ];  // chunk j = 64 q + lane of the step image [stripe][LH_CPS x bytes]
 #pragma unroll
