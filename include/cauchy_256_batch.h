@@ -105,12 +105,14 @@ const char *cauchy_256_last_launch(void);
  * lh_apply_jump2_kernel), 0 when the generic kernels below dword lanes serve the shape; -2
  * without a device.  `what` = 8: 1 when the (k, m) block-size family module (one module per
  * (k, m) for every 16-byte-multiple size up to 4 KiB with m <= 6) can serve the encode: batch
- * and drop-in encodes take it while no size-specialised module is loaded or cached. */
+ * and drop-in encodes take it while no size-specialised module is loaded or cached.  `what` =
+ * 9: the same for the decode's family (the fused decode: min(k, m) <= 4, k <= 64, at least
+ * ceil(k / 8) 8-byte lanes per stripe). */
 int cauchy_256_batch_path(int k, int m, int block_bytes, int what);
 
 /* Compile the specialised kernels of a shape into the on-disk code-object cache
  * ($LONGHAIR_AMD_CACHE_DIR, else jit_cache/ beside the library).  Needs no GPU.  With
- * LONGHAIR_AMD_PRECOMPILE_FAMILY=1 also the encode's (k, m) block-size family module.
+ * LONGHAIR_AMD_PRECOMPILE_FAMILY=1 also the (k, m) block-size family modules.
  * Returns 0 or -3. */
 int cauchy_256_jit_precompile(int k, int m, int block_bytes);
 
