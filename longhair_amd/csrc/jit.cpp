@@ -152,7 +152,7 @@ static bool config_impl(int k, int m, int bytes, bool decode, JitConfig *cfg, bo
     if (cfg->cps > 1 && !((!decode || dmo) && cfg->lds && k >= 2 * cfg->cps)) cfg->cps = 1;
     cfg->wgcu = knob("LH_WGCU=", cfg->cps > 1 ? 1 : 0);
     const int wpb = knob("LH_WPB=", 4);
-    cfg->enc_wpb = (cfg->cps > 1 && wpb >= 1 && wpb <= 4) ? wpb : 4;
+    cfg->enc_wpb = (cfg->cps > 1 && wpb >= 1 && wpb <= 8) ? wpb : 4;
     // Block-size family (jit_codec.hip LH_FAMILY): the multi-column-step encode with the block
     // size a kernel argument, keyed by (k, m) alone.
     cfg->family = 0;

@@ -1281,7 +1281,10 @@ lh_jit_encode(const unsigned char *__restrict__ in, long long in_stride, unsigne
 #ifndef LH_ENC_LB
 #define LH_ENC_LB 1  // min waves per SIMD the register allocator must allow (tools/tune.py)
 #endif
-extern "C" __global__ void __launch_bounds__(256, LH_ENC_LB)
+#ifndef LH_WPB
+#define LH_WPB 4
+#endif
+extern "C" __global__ void __launch_bounds__(LH_WPB > 4 ? 64 * LH_WPB : 256, LH_ENC_LB)
 lh_jit_encode(const unsigned char *__restrict__ in, long long in_stride,
               unsigned char *__restrict__ out, long long out_stride, int stripes) {
 #if LH_LDS && LH_CPS > 1 && !LH_PTR
