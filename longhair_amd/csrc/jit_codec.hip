@@ -995,6 +995,10 @@ __device__ __forceinline__ void lh_encode_wave_cps(long long wave, const unsigne
                 w.v[1] = last ? f.v[1] : w.v[1];
             }
             lh_store(o + (long long)r * LH_BYTES + y * LH_SUB, w);
+            // (stores kept in address order: a line two neighbouring sub-rows share then gets
+            // both halves back to back; reordered by the scheduler, the non-temporal halves
+            // left as partial-line writes, +14 MB per k29/m4 launch, profiles/r10x/r10y PMC)
+            asm volatile("" ::: "memory");
         }
 #endif
 }
@@ -2069,12 +2073,21 @@ __device__ __forceinline__ void lh_decode_lds_prologue(const lh_dldsrc &S) {
 // Phase B and the stores of a stripe's recovered blocks: block i = sum_r coef[i][r] V_r, stored
 // at the slot `dst(out slot i)` returns (the lane's chunk of it); the last lane of a stripe
 // funnels the previous lane's word (its chunk's last LH_VLAST bytes are its own).
+#ifndef LH_DEC_ST_PEND
+#define LH_DEC_ST_PEND 0  // (1: measured no change in write bytes, decode 0.5548 -> 0.5598 ms; profiles/r10w_*)
+#endif
 // (VL: the last lane's own bytes, sub: the sub-block size -- LH_VLAST, LH_SUB except in the
 // block-size family)
 template <int VL, class DST>
 __device__ __forceinline__ void lh_fused_out_g(const lh_word (&v)[LH_M][8], const lh_plan_regs &pr, bool last, int sub,
                                                DST dst) {
     const int e = pr.e;
+#if LH_DEC_ST_PEND
+    lh_word pend;  // the last block's last sub-row, stored with the next block
+    unsigned char *pd = nullptr;
+#pragma unroll
+    for (int q = 0; q < LH_NW; ++q) pend.v[q] = 0;
+#endif
 #pragma unroll
     for (int i = 0; i < LH_EMAX; ++i) {
         if (i < e) {  // stripe-uniform: the funnel's source lane is active too
@@ -2110,6 +2123,16 @@ __device__ __forceinline__ void lh_fused_out_g(const lh_word (&v)[LH_M][8], cons
 #endif
             }
             unsigned char *d = dst((int)LH_BYTE(pr.outw, i));
+#if LH_DEC_ST_PEND
+            // the previous block's last sub-row right before this block's first: when the two
+            // blocks are neighbours (the recovery slots usually are), the line they share gets
+            // both parts back to back instead of a block's phase B apart (non-temporal stores
+            // leave the earlier part as a partial-line write)
+            if (i > 0) {
+                lh_store(pd + 7 * sub, pend);
+                asm volatile("" ::: "memory");
+            }
+#endif
 #pragma unroll
             for (int y = 0; y < 8; ++y) {
                 lh_word w = o[y];
@@ -2118,10 +2141,21 @@ __device__ __forceinline__ void lh_fused_out_g(const lh_word (&v)[LH_M][8], cons
                     w.v[0] = last ? f.v[0] : w.v[0];
                     w.v[1] = last ? f.v[1] : w.v[1];
                 }
+#if LH_DEC_ST_PEND
+                if (y == 7) {
+                    pend = w;
+                    pd = d;
+                    continue;
+                }
+#endif
                 lh_store(d + y * sub, w);
+                asm volatile("" ::: "memory");
             }
         }
     }
+#if LH_DEC_ST_PEND
+    if (e > 0) lh_store(pd + 7 * sub, pend);
+#endif
 }
 template <class DST>
 __device__ __forceinline__ void lh_fused_out(const lh_word (&v)[LH_M][8], const lh_plan_regs &pr, bool last, DST dst) {
