@@ -1762,7 +1762,10 @@ __device__ __forceinline__ bool lh_fused_plan(const G &g, const lh_lane &l, int 
         if (c == 0 && status) status[l.stripe] = -1;
         return false;
     }
-    if (c == 0 && status) status[l.stripe] = 0;
+#ifndef LH_PROBE_NOMETA
+#define LH_PROBE_NOMETA 0  // (probe, wrong rows / status: neither written -- their share of the HBM writes)
+#endif
+    if (c == 0 && status && !LH_PROBE_NOMETA) status[l.stripe] = 0;
     pr.e = nr;
     if (nr == 0) return false;
 #pragma unroll
@@ -1919,7 +1922,7 @@ __device__ __forceinline__ void lh_fused_solve::operator()(lh_plan_regs &pr) con
     // Recovery slot i takes missing row er[i] (reference generate_bitmatrix, :786).
     if (c == 0)
 #pragma unroll
-        for (int i = 0; i < LH_EMAX; ++i) if (i < nr) grow[rs[i]] = (unsigned char)er[i];
+        for (int i = 0; i < LH_EMAX; ++i) if (i < nr && !LH_PROBE_NOMETA) grow[rs[i]] = (unsigned char)er[i];
     // Materialise the packed plan here, so the solve's matrices die before phase A: left
     // alone, the compiler sinks the packing into phase B and keeps the e x e inverse and
     // the row lists live across all k + m columns (k29/m4: 218 -> 158 VGPRs, 2 -> 3

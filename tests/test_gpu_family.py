@@ -46,6 +46,28 @@ FAMILY_DEC_SHAPES = [
 ]
 
 
+
+def family_sample(pairs=((5, 3), (13, 4), (22, 2), (37, 4), (50, 3), (64, 4)), sizes=25, seed=611):
+    """A seeded sample for the families' randomised parity: for each (k, m) (one module per
+    role serves all its sizes), `sizes` random 16-byte-multiple block sizes that both families
+    serve, with a random stripe count.  tools/precompile.py builds the modules."""
+    import longhair_amd as lh
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = []
+    for k, m in pairs:
+        got = 0
+        while got < sizes:
+            b = 16 * int(rng.integers(1, 257))
+            if (lh.lib().cauchy_256_batch_path(k, m, b, 8) == 1 and lh.lib().cauchy_256_batch_path(k, m, b, 9) == 1
+                    and (k, m, b) not in [o[:3] for o in out]):
+                out.append((k, m, b, int(rng.integers(1, 40))))
+                got += 1
+    return out
+
+
+FAMILY_SAMPLE_PAIRS = ((5, 3), (13, 4), (22, 2), (37, 4), (50, 3), (64, 4))
+
+
 @pytest.fixture(scope="module")
 def lh():
     import torch
@@ -104,3 +126,18 @@ def test_family_serves_sizes_without_a_module(lh, oracle, monkeypatch, tmp_path)
         enc, dec = tb.roundtrip(lh, oracle, 29, 4, nbytes, stripes, seed=nbytes + 7)
         assert enc == ["lh_jit_encode(family)"], (nbytes, enc)
         assert dec == ["lh_jit_decode_fused(family)"], (nbytes, dec)
+
+
+def test_family_random_sizes(lh, oracle, monkeypatch):
+    """Randomised parity of both families: 150 seeded (k, m, bytes, stripes) cases over six
+    (k, m) modules, encode and decode (random e, recovery rows and slot order per stripe)
+    against the oracle, each through the family kernels."""
+    import test_gpu_boundaries as tb
+    monkeypatch.setenv("LONGHAIR_AMD_JIT_DEFINES", "LH_FAMILY=1")
+    monkeypatch.setenv("LONGHAIR_AMD_JIT_SYNC", "1")
+    cases = family_sample(FAMILY_SAMPLE_PAIRS)
+    assert len(cases) == 150
+    for k, m, nbytes, stripes in cases:
+        enc, dec = tb.roundtrip(lh, oracle, k, m, nbytes, stripes, seed=k * 100003 + nbytes)
+        assert enc == ["lh_jit_encode(family)"], (k, m, nbytes, enc)
+        assert dec == ["lh_jit_decode_fused(family)"], (k, m, nbytes, dec)

@@ -116,6 +116,10 @@ def main():
                           for k, m, b, _ in tf.FAMILY_SHAPES]
             jobs_list += [((k, m, b), (part, {"LONGHAIR_AMD_JIT_DEFINES": "LH_FAMILY=1"}))
                           for k, m, b, _ in tf.FAMILY_DEC_SHAPES for part in ("dec", "enc")]
+            # the families' randomised parity (test_family_random_sizes): one module per (k, m, role)
+            jobs_list += [(sh, (part, {"LONGHAIR_AMD_JIT_DEFINES": "LH_FAMILY=1"}))
+                          for sh in dict.fromkeys(c[:3] for c in tf.family_sample(tf.FAMILY_SAMPLE_PAIRS, sizes=1))
+                          for part in ("dec", "enc")]
             jobs_list = ptr_jobs[-4:] + jobs_list + ptr_jobs[:-4]
             # kernel-selection boundaries and the reference-main sweep (test_gpu_boundaries.py)
             bj, tb = boundary_jobs()
