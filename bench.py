@@ -85,6 +85,8 @@ def parse(argv=None):
                     help="per-call drop-in latency leg (host pointers, one stripe per call); 0 = off")
     ap.add_argument("--ptr", default="on", choices=["on", "off"],
                     help="also time the step through the pointer-table batch calls (after the timed region)")
+    ap.add_argument("--family", default="on", choices=["on", "off"],
+                    help="also time the step on the block-size family modules (shapes they serve; untimed region)")
     ap.add_argument("--pcie", default="on", choices=["on", "off"],
                     help="PCIe-inclusive leg: cauchy_256_*_host_batch from pinned host memory on every rank")
     ap.add_argument("--pcie-stripes", type=int, default=0,
@@ -644,6 +646,66 @@ def ptr_leg(lh, k, m, nbytes, X, D, rows0, rec_view, rec_index=None, reps=5, set
                     f"HIP events, mean of {reps} after {warm} untimed passes"}
 
 
+def family_leg(lh, k, m, nbytes, X, D, rows0, rec_view, reps=5, settle_s=0.25):
+    """The same step on the (k, m) block-size family modules (jit_codec.hip LH_FAMILY: the
+    block size a kernel argument, one module per (k, m) and role), which serve
+    every block size that has no size-specialised module -- the first call at a new size.
+    Forced with LONGHAIR_AMD_JIT_DEFINES=LH_FAMILY=1 for the leg only; HIP events on the launch
+    stream, mean of `reps` after untimed passes for `settle_s`; the decoded data is checked.
+    None when neither family serves the shape."""
+    import torch
+    enc_ok = lh.lib().cauchy_256_batch_path(k, m, nbytes, 8) == 1
+    dec_ok = lh.lib().cauchy_256_batch_path(k, m, nbytes, 9) == 1
+    if not (enc_ok or dec_ok):
+        return None
+    saved = os.environ.get("LONGHAIR_AMD_JIT_DEFINES")
+    os.environ["LONGHAIR_AMD_JIT_DEFINES"] = "LH_FAMILY=1"
+    try:
+        stripes = X.shape[0]
+        lh.prepare(k, m, nbytes, stripes)  # the family modules (cached at build time for the BASELINE shapes)
+        rows = rows0.clone()
+        stream = torch.cuda.current_stream()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        enc = dec = 0.0
+        traces = {}
+        t_s, warm = time.perf_counter(), 0
+        while True:
+            lh.encode_batch(X, m, recovery=rec_view, stream=stream)
+            rows.copy_(rows0)
+            lh.decode_batch(D, rows, m, stream=stream)
+            warm += 1
+            if warm % 4 == 0:
+                torch.cuda.synchronize()
+                if time.perf_counter() - t_s >= settle_s:
+                    break
+        for i in range(reps + 1):
+            ev[0].record(stream)
+            lh.encode_batch(X, m, recovery=rec_view, stream=stream)
+            ev[1].record(stream)
+            traces.setdefault("encode", lh.last_launch())
+            rows.copy_(rows0)
+            ev[2].record(stream)
+            lh.decode_batch(D, rows, m, stream=stream)
+            ev[3].record(stream)
+            traces.setdefault("decode", lh.last_launch())
+            torch.cuda.synchronize()
+            if i:
+                enc += ev[0].elapsed_time(ev[1]) / reps
+                dec += ev[2].elapsed_time(ev[3]) / reps
+        order = rows.long().argsort(dim=1)
+        ok = bool(torch.equal(torch.gather(D, 1, order.unsqueeze(-1).expand(-1, -1, nbytes)), X))
+    finally:
+        if saved is None:
+            os.environ.pop("LONGHAIR_AMD_JIT_DEFINES", None)
+        else:
+            os.environ["LONGHAIR_AMD_JIT_DEFINES"] = saved
+    return {"encode_ms": round(enc, 4), "decode_ms": round(dec, 4),
+            "encode_kernels": traces["encode"], "decode_kernels": traces["decode"], "ok": ok,
+            "what": "the step on the (k, m) block-size family modules (the block size a kernel argument: what a "
+                    "block size without a size-specialised module runs), forced for this leg, HIP events, "
+                    f"mean of {reps} after {warm} untimed passes"}
+
+
 def load_profile(name):
     path = os.path.join(REPO, "profiles", name)
     return json.load(open(path)) if os.path.exists(path) else None
@@ -859,6 +921,10 @@ def main():
                                                     / HBM_PEAK_GBS, 4)})
     if not dry and args.ptr == "on":
         out["ptr_tables"] = ptr_leg(lh, k, m, nbytes, X, D, rows0, rec_view, rec_index)
+    if not dry and rank == 0 and args.family == "on" and rec_index is None:
+        fam = family_leg(lh, k, m, nbytes, X, D, rows0, rec_view)
+        if fam is not None:
+            out["family"] = fam
     if not dry and args.pcie == "on":
         # every rank at once: the node's host links and memory are shared
         out["pcie"] = pcie_leg(lh, args, k, m, nbytes, X, D, rows0, rec_view, rec_index, world, rank)
