@@ -706,6 +706,58 @@ def family_leg(lh, k, m, nbytes, X, D, rows0, rec_view, reps=5, settle_s=0.25):
                     f"mean of {reps} after {warm} untimed passes"}
 
 
+def reflayout_leg(lh, k, m, nbytes, X, rows0, reps=5, settle_s=0.25):
+    """The decode on the reference benchmark's block order (tests/cauchy_256_tests.cpp:296-307:
+    every surviving original in its own slot, the recovery blocks in the erased originals'
+    slots) instead of the bench's shuffled survivors: the same erasures (rows0), the slots in
+    row order, so the decode reads each stripe's survivors in memory order.  HIP events, mean
+    of `reps` after untimed passes for `settle_s`; the recovery blocks are put back before
+    every pass (outside the events) and the decoded stripes are checked against X."""
+    import torch
+    stripes, e = X.shape[0], m
+    stream = torch.cuda.current_stream()
+    R = lh.encode_batch(X, m, stream=stream)  # [S, m, bytes]
+    keep = rows0[:, : k - e].long()
+    present = torch.zeros((stripes, k), dtype=torch.int32, device="cuda").scatter_(1, keep, 1)
+    er = torch.argsort(present, dim=1, stable=True)[:, :e]  # erased originals, ascending
+    D2 = X.clone()
+    rows_ref = torch.arange(k, device="cuda").repeat(stripes, 1).scatter_(
+        1, er, (k + torch.arange(e, device="cuda")).repeat(stripes, 1)).to(torch.uint8)
+    rows = rows_ref.clone()
+    idx = er.unsqueeze(-1).expand(-1, -1, nbytes)
+
+    def reset():
+        D2.scatter_(1, idx, R[:, :e])
+        rows.copy_(rows_ref)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    t_s, warm = time.perf_counter(), 0
+    while True:
+        reset()
+        lh.decode_batch(D2, rows, m, stream=stream)
+        warm += 1
+        if warm % 4 == 0:
+            torch.cuda.synchronize()
+            if time.perf_counter() - t_s >= settle_s:
+                break
+    dec = 0.0
+    trace = None
+    for i in range(reps + 1):
+        reset()
+        ev[0].record(stream)
+        lh.decode_batch(D2, rows, m, stream=stream)
+        ev[1].record(stream)
+        trace = trace or lh.last_launch()
+        torch.cuda.synchronize()
+        if i:
+            dec += ev[0].elapsed_time(ev[1]) / reps
+    ok = bool(torch.equal(D2, X))
+    return {"decode_ms": round(dec, 4), "decode_GBps": round(k * nbytes * stripes / (dec * 1e-3) / 1e9, 1),
+            "decode_kernels": trace, "ok": ok,
+            "what": "decode_batch on the reference benchmark's block order (survivors in their own slots, "
+                    "recovery blocks in the erased slots; same erasures), HIP events, "
+                    f"mean of {reps} after {warm} untimed passes"}
+
+
 def load_profile(name):
     path = os.path.join(REPO, "profiles", name)
     return json.load(open(path)) if os.path.exists(path) else None
@@ -922,6 +974,7 @@ def main():
     if not dry and args.ptr == "on":
         out["ptr_tables"] = ptr_leg(lh, k, m, nbytes, X, D, rows0, rec_view, rec_index)
     if not dry and rank == 0 and args.family == "on" and rec_index is None:
+        out["reference_order"] = reflayout_leg(lh, k, m, nbytes, X, rows0)
         fam = family_leg(lh, k, m, nbytes, X, D, rows0, rec_view)
         if fam is not None:
             out["family"] = fam
