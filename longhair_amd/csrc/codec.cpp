@@ -574,8 +574,10 @@ static int decode_batch(int k, int m, int bytes, int stripes, uint8_t *d_blocks,
         int n = stripes, bb = bytes;  // (bb: the family kernel's block-size argument; cfg.spw follows it)
         void *args[] = {(void *)&d_blocks, &s1, (void *)&d_rows, (void *)&d_status, (void *)&zero,
                         (void *)&gexp, (void *)&glog, &n, &bb};
-        LH_HIP(hipModuleLaunchKernel(fn, (unsigned)jit_blocks(cfg, stripes), 1, 1, 256, 1, 1, jk->dyn_lds, st, args,
-                                     nullptr));
+        const long long waves = cfg.spw ? (stripes + cfg.spw - 1) / cfg.spw : (long long)stripes * cfg.wps;
+        const int wpb = cfg.family ? 4 : cfg.dec_wpb;  // (LH_DWPB; the family kernel runs 4-wave workgroups)
+        LH_HIP(hipModuleLaunchKernel(fn, (unsigned)((waves + wpb - 1) / wpb), 1, 1, 64u * (unsigned)wpb, 1, 1,
+                                     jk->dyn_lds, st, args, nullptr));
         note_launch(cfg.family ? "lh_jit_decode_fused(family)" : "lh_jit_decode_fused");
         return kOk;
     }

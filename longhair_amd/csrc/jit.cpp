@@ -153,6 +153,8 @@ static bool config_impl(int k, int m, int bytes, bool decode, JitConfig *cfg, bo
     cfg->wgcu = knob("LH_WGCU=", cfg->cps > 1 ? 1 : 0);
     const int wpb = knob("LH_WPB=", 4);
     cfg->enc_wpb = (cfg->cps > 1 && wpb >= 1 && wpb <= 8) ? wpb : 4;
+    const int dwpb = knob("LH_DWPB=", 4);
+    cfg->dec_wpb = (decode && !cfg->plain && dwpb >= 1 && dwpb <= 8) ? dwpb : 4;
     // Block-size family (jit_codec.hip LH_FAMILY): the multi-column-step encode with the block
     // size a kernel argument, keyed by (k, m) alone.
     cfg->family = 0;

@@ -40,6 +40,7 @@ struct JitConfig {
     int family = 0;       // the block-size family module (LH_FAMILY: one module per (k, m)
                           // serves every qualifying block size, which the kernel takes as an argument)
     int enc_wpb = 4;      // encode: waves per workgroup (LH_WPB, multi-column-step encode only)
+    int dec_wpb = 4;      // fused decode of strided batches: waves per workgroup (LH_DWPB)
     int lanes_per_launch_unit() const { return 64; }
 };
 

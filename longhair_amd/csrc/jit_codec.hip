@@ -1657,6 +1657,9 @@ lh_jit_decode(unsigned char *__restrict__ blocks, long long stripe_stride,
 // assignment (:786); duplicate / out-of-range rows mark the stripe invalid, untouched.
 #if LH_EMAX <= 4 && LH_NCH <= 64 && LH_K <= 64
 #define LH_FUSED 1
+#ifndef LH_DWPB
+#define LH_DWPB 4  // waves per workgroup of the fused decode (strided batches; jit.cpp dec_wpb)
+#endif
 static constexpr unsigned char LH_GRAW[LH_M][LH_K] = LH_G_INIT;
 #define LH_P4(n) (((n) + 3) / 4 * 4)
 #define LH_SR (2 * LH_P4(LH_K) + LH_P4(LH_M))  // per-stripe scratch: rows | src map | rec map
@@ -2170,7 +2173,7 @@ __device__ __forceinline__ void lh_fused_wave_lds(const lh_lane &l, long long wa
                                                   const unsigned char *scr, unsigned char *__restrict__ blocks,
                                                   long long stripe_stride, int stripes, const lh_fused_solve &sv,
                                                   lh_plan_regs &pr, const unsigned char *zero_page) {
-    __shared__ __attribute__((aligned(16))) unsigned char lh_dring[4][LH_LD * LH_LQ * 1024 + LH_LPAD];
+    __shared__ __attribute__((aligned(16))) unsigned char lh_dring[LH_DWPB][LH_LD * LH_LQ * 1024 + LH_LPAD];
     const int lane = threadIdx.x & 63;
     const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)wave) * LH_SPW;  // wave-uniform
     if (s0 >= stripes) return;  // wave-uniform
@@ -2180,7 +2183,7 @@ __device__ __forceinline__ void lh_fused_wave_lds(const lh_lane &l, long long wa
     lh_dldsrc S;
 #if LH_PTR
     // blocks: the pointer table (rows of LH_K block pointers, stride stripe_stride bytes)
-    __shared__ unsigned long long lh_dpt[4][LH_SPW * (LH_K + 1)];
+    __shared__ unsigned long long lh_dpt[LH_DWPB][LH_SPW * (LH_K + 1)];
     unsigned long long *prow = lh_dpt[threadIdx.x >> 6];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous stripe group's reads
     __builtin_amdgcn_wave_barrier();
@@ -2363,7 +2366,7 @@ __device__ __forceinline__ void lh_fused_wave_dmo(const lh_lane &l, long long wa
                                                   const unsigned char *scr, unsigned char *__restrict__ blocks,
                                                   long long stripe_stride, int stripes, const lh_fused_solve &sv,
                                                   lh_plan_regs &pr) {
-    __shared__ __attribute__((aligned(16))) unsigned char lh_mring[4][(1 + LH_DMO_AHEAD) * LH_SSLOT];
+    __shared__ __attribute__((aligned(16))) unsigned char lh_mring[LH_DWPB][(1 + LH_DMO_AHEAD) * LH_SSLOT];
     const int lane = threadIdx.x & 63;
     const long long s0 = (long long)__builtin_amdgcn_readfirstlane((int)wave) * LH_SPW;  // wave-uniform
     if (s0 >= stripes) return;  // wave-uniform
@@ -2456,7 +2459,7 @@ __device__ __forceinline__ void lh_fused_body(unsigned char *__restrict__ blocks
     __shared__ unsigned char gexp[1024];  // exp(i mod 255) for i < 1024 (lh_inv_adj)
     __shared__ short glog[256];
     __shared__ unsigned char gmat[LH_M * LH_K];
-    __shared__ __attribute__((aligned(16))) unsigned char scratch[4][LH_SPW > 0 ? LH_SPW : 1][LH_SR];
+    __shared__ __attribute__((aligned(16))) unsigned char scratch[LH_DWPB][LH_SPW > 0 ? LH_SPW : 1][LH_SR];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) gexp[i + 256 * q] = gf_exp[(i + 256 * q) % 255];
@@ -2491,7 +2494,7 @@ __device__ __forceinline__ void lh_fused_body(unsigned char *__restrict__ blocks
 }
 
 #if (LH_ROLE == 0 || (LH_ROLE == 2 && !LH_DEC_PLAIN)) && !LH_FAMILY
-extern "C" __global__ void __launch_bounds__(256, LH_DEC_LB)
+extern "C" __global__ void __launch_bounds__(64 * LH_DWPB, LH_DEC_LB)
 lh_jit_decode_fused(unsigned char *__restrict__ blocks, long long stripe_stride, unsigned char *__restrict__ rows,
                     signed char *__restrict__ status, const unsigned char *__restrict__ zero_page,
                     const unsigned char *__restrict__ gf_exp, const short *__restrict__ gf_log, int stripes) {
