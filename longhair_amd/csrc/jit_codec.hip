@@ -1185,6 +1185,7 @@ __device__ __forceinline__ void lh_fam_store(const lh_word (&acc)[LH_M][8], unsi
                 w.v[1] = last ? f.v[1] : w.v[1];
             }
             lh_store(o + (long long)r * F.bytes + y * F.sub, w);
+            asm volatile("" ::: "memory");  // (in address order, as lh_encode_wave_cps's stores)
         }
 }
 // One wave's stripes; R = sub mod 8 (0, 2, 4 or 6), a compile-time form chosen once per launch,
