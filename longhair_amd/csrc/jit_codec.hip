@@ -2080,6 +2080,9 @@ __device__ __forceinline__ void lh_decode_lds_prologue(const lh_dldsrc &S) {
 // Phase B and the stores of a stripe's recovered blocks: block i = sum_r coef[i][r] V_r, stored
 // at the slot `dst(out slot i)` returns (the lane's chunk of it); the last lane of a stripe
 // funnels the previous lane's word (its chunk's last LH_VLAST bytes are its own).
+#ifndef LH_PROBE_NOPB
+#define LH_PROBE_NOPB 0
+#endif
 #ifndef LH_DEC_ST_PEND
 #define LH_DEC_ST_PEND 0  // (1: measured no change in write bytes, decode 0.5548 -> 0.5598 ms; profiles/r10w_*)
 #endif
@@ -2103,6 +2106,10 @@ __device__ __forceinline__ void lh_fused_out_g(const lh_word (&v)[LH_M][8], cons
             for (int y = 0; y < 8; ++y)
 #pragma unroll
                 for (int q = 0; q < LH_NW; ++q) o[y].v[q] = 0;
+#if LH_PROBE_NOPB  // (probe, wrong bytes: no phase B, V_(i mod m) stored as block i -- what phase B costs)
+#pragma unroll
+            for (int y = 0; y < 8; ++y) o[y] = v[i % LH_M][y];
+#else
 #pragma unroll
             for (int t = 7; t >= 0; --t) {
                 if (t != 7) {
@@ -2129,6 +2136,7 @@ __device__ __forceinline__ void lh_fused_out_g(const lh_word (&v)[LH_M][8], cons
                 lh_pin8(o);
 #endif
             }
+#endif
             unsigned char *d = dst((int)LH_BYTE(pr.outw, i));
 #if LH_DEC_ST_PEND
             // the previous block's last sub-row right before this block's first: when the two
